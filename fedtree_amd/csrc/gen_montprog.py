@@ -1,0 +1,361 @@
+#!/usr/bin/env python3
+"""Generator for the hand-scheduled gfx950 Montgomery "program" kernel.
+
+The kernel runs one big-integer modular computation per LANE (64 independent
+ciphertexts per wavefront).  Every lane executes the same uniform op program
+(an exponent schedule produced on the host), so all control flow is
+wave-uniform.  The hot loop is a radix-2^B CIOS Montgomery product
+
+    X <- A * X * R^-1 mod N,      R = 2^(B*S)
+
+with the S limbs of X in VGPRs, the A operand streamed one limb per outer
+iteration from LDS (lane-interleaved, one column per lane, conflict-free),
+the modulus N in SGPRs (it is the same for the whole launch) and a window of
+64-bit column accumulators T[] in VGPRs.  B < 32 leaves headroom in the 64-bit
+accumulators, so every 32x32 partial product is exactly ONE v_mad_u64_u32
+(half-rate on gfx950, measured 3.45e13/s chip-wide) -- no add-with-carry
+chains.  R > 4N ("almost Montgomery"), so no conditional subtraction is ever
+needed inside an exponentiation; results stay < 2N.
+
+Why hand-written assembly: the CIOS state is ~250 VGPRs per lane.  hipcc's
+scheduler hoists the LDS reads and spills hundreds of registers at this size
+(measured: 116-913 spilled VGPRs across formulations), so the register
+allocation is done here, explicitly.
+
+Ops (uint32 pairs, read with s_load from the program buffer):
+    0 END
+    1 LOADX  slot   X <- slot
+    2 STOREX slot   slot <- X
+    3 SQR    count  repeat count times: A <- X ; X <- MontMul(A, X)
+    4 MUL    slot   A <- slot ; X <- MontMul(A, X)
+    5 ADDSLOT slot  X <- X + slot          (integer add, limbs renormalised)
+    6 ADDSMALL k    X <- X + k             (k < 2^B)
+
+Slot memory: slot s, limb k, lane g at  slots + s*slot_stride + k*L*4 + g*4
+(limb-major, lane-interleaved: every global access is fully coalesced).
+
+Kernel arguments (kernarg segment):
+    0  u64 slots         8  u64 prog        16 u64 ctx (N[S] u32, nprime u32)
+    24 u32 limb_stride (=L*4 bytes)          28 u32 slot_stride (=S*L*4 bytes)
+"""
+import argparse
+import sys
+
+
+def gen(S: int, B: int, U: int, name: str) -> str:
+    assert U % 2 == 0 and U >= 2
+    MASK = (1 << B) - 1
+    NTRIPS = S // U
+    TAIL = S % U
+    # ---- VGPR plan -------------------------------------------------------
+    V_TID, V_GOFF, V_LDSA = 0, 1, 2
+    V_AI = (3, 4)          # double-buffered a_i
+    V_Q = 5
+    V_LDSI = 6
+    V_TMP = 8              # v[8:9] 64-bit temp (even aligned)
+    XB = 10                # X limbs v[10 .. 10+S-1]
+    TB = XB + S
+    if TB % 2:
+        TB += 1
+    NT = S + U              # T window entries (64-bit)
+    NVGPR = TB + 2 * NT
+    assert NVGPR <= 256, f"VGPR budget exceeded: {NVGPR}"
+    # ---- SGPR plan -------------------------------------------------------
+    # s[0:1] kernarg, s2 wg id, s[4:5] slots, s[6:7] prog, s[8:9] ctx,
+    # s10 limb stride, s11 slot stride, s12 nprime, s[14:15] op/arg,
+    # s[16:17] addr, s18 trip counter, s19 sqr counter, s20.. N limbs
+    SN = 20
+    NSGPR = SN + S
+    assert NSGPR <= 100, f"SGPR budget exceeded: {NSGPR}"
+
+    def T(k):
+        return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
+
+    def Tlo(k):
+        return f"v{TB + 2 * k}"
+
+    def X(k):
+        return f"v{XB + k}"
+
+    o = []
+    e = o.append
+    lds_per_wave = S * 256
+    lds_bytes = 4 * lds_per_wave
+    e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
+    e('.amdhsa_code_object_version 5')
+    e('.text')
+    e(f'.globl {name}')
+    e('.p2align 8')
+    e(f'.type {name},@function')
+    e(f'{name}:')
+    # -- prologue: kernel args
+    e('  s_load_dwordx2 s[4:5], s[0:1], 0x0')
+    e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
+    e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
+    e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
+    e('  s_waitcnt lgkmcnt(0)')
+    # -- modulus limbs into SGPRs
+    off = 0
+    sreg = SN
+    rem = S
+    for width in (16, 8, 4, 2, 1):
+        while rem >= width:
+            assert sreg % min(width, 4) == 0
+            suffix = f"x{width}" if width > 1 else ""
+            dst = f"s[{sreg}:{sreg + width - 1}]" if width > 1 else f"s{sreg}"
+            e(f'  s_load_dword{suffix} {dst}, s[8:9], {hex(off)}')
+            off += 4 * width
+            sreg += width
+            rem -= width
+    e(f'  s_load_dword s12, s[8:9], {hex(4 * S)}')
+    # -- per-lane addresses
+    e('  s_lshl_b32 s14, s2, 10')                 # wg*256*4
+    e(f'  v_lshlrev_b32_e32 v{V_GOFF}, 2, v{V_TID}')
+    e(f'  v_add_u32_e32 v{V_GOFF}, s14, v{V_GOFF}')
+    e(f'  v_lshrrev_b32_e32 v{V_LDSA}, 6, v{V_TID}')
+    e(f'  v_mul_u32_u24_e32 v{V_LDSA}, {hex(lds_per_wave)}, v{V_LDSA}')
+    e(f'  v_and_b32_e32 v{V_Q}, 63, v{V_TID}')
+    e(f'  v_lshl_add_u32 v{V_LDSA}, v{V_Q}, 2, v{V_LDSA}')
+    e('  s_waitcnt lgkmcnt(0)')
+
+    # -- op dispatcher
+    e('.Lprog:')
+    e('  s_load_dwordx2 s[14:15], s[6:7], 0x0')
+    e('  s_add_u32 s6, s6, 8')
+    e('  s_addc_u32 s7, s7, 0')
+    e('  s_waitcnt lgkmcnt(0)')
+    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
+                      (5, '.Laddslot'), (6, '.Laddsmall')):
+        e(f'  s_cmp_eq_u32 s14, {code}')
+        e(f'  s_cbranch_scc1 {lab}')
+    e('  s_branch .Lend')
+
+    def slot_addr():
+        # s[16:17] = slots + arg*slot_stride
+        e('  s_mul_i32 s16, s15, s11')
+        e('  s_add_u32 s16, s4, s16')
+        e('  s_addc_u32 s17, s5, 0')
+
+    def step_addr():
+        e('  s_add_u32 s16, s16, s10')
+        e('  s_addc_u32 s17, s17, 0')
+
+    # LOADX
+    e('.Lloadx:')
+    slot_addr()
+    for k in range(S):
+        e(f'  global_load_dword {X(k)}, v{V_GOFF}, s[16:17]')
+        if k != S - 1:
+            step_addr()
+        if k % 32 == 31:
+            e('  s_waitcnt vmcnt(0)')
+    e('  s_waitcnt vmcnt(0)')
+    e('  s_branch .Lprog')
+
+    # STOREX
+    e('.Lstorex:')
+    slot_addr()
+    for k in range(S):
+        e(f'  global_store_dword v{V_GOFF}, {X(k)}, s[16:17]')
+        if k != S - 1:
+            step_addr()
+        if k % 32 == 31:
+            e('  s_waitcnt vmcnt(0)')
+    e('  s_waitcnt vmcnt(0)')
+    e('  s_branch .Lprog')
+
+    def normalise32():
+        # X limbs < 2^31 -> radix-2^B limbs (sequential carry; value < R)
+        c = f"v{V_TMP}"
+        e(f'  v_lshrrev_b32_e32 {c}, {B}, {X(0)}')
+        e(f'  v_and_b32_e32 {X(0)}, {hex(MASK)}, {X(0)}')
+        for k in range(1, S):
+            e(f'  v_add_u32_e32 {X(k)}, {X(k)}, {c}')
+            if k != S - 1:
+                e(f'  v_lshrrev_b32_e32 {c}, {B}, {X(k)}')
+                e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, {X(k)}')
+
+    # ADDSLOT: X <- X + slot (plain integer add, value must stay < R)
+    e('.Laddslot:')
+    slot_addr()
+    for k in range(S):
+        e(f'  global_load_dword v{TB + k}, v{V_GOFF}, s[16:17]')
+        if k != S - 1:
+            step_addr()
+        if k % 32 == 31:
+            e('  s_waitcnt vmcnt(0)')
+    e('  s_waitcnt vmcnt(0)')
+    for k in range(S):
+        e(f'  v_add_u32_e32 {X(k)}, {X(k)}, v{TB + k}')
+    normalise32()
+    e('  s_branch .Lprog')
+
+    # ADDSMALL: X <- X + arg (arg < 2^B)
+    e('.Laddsmall:')
+    e(f'  v_add_u32_e32 {X(0)}, s15, {X(0)}')
+    normalise32()
+    e('  s_branch .Lprog')
+
+    # MUL: A <- slot (through the free T registers), then MontMul
+    e('.Lmul:')
+    slot_addr()
+    for k in range(S):
+        e(f'  global_load_dword v{TB + k}, v{V_GOFF}, s[16:17]')
+        if k != S - 1:
+            step_addr()
+        if k % 32 == 31:
+            e('  s_waitcnt vmcnt(0)')
+    e('  s_waitcnt vmcnt(0)')
+    for k in range(S):
+        e(f'  ds_write_b32 v{V_LDSA}, v{TB + k} offset:{k * 256}')
+        if k % 8 == 7:
+            e('  s_waitcnt lgkmcnt(0)')
+    e('  s_waitcnt lgkmcnt(0)')
+    e('  s_mov_b32 s19, 0')      # after the product: back to the dispatcher
+    e('  s_branch .Lmontmul')
+
+    # SQR: count in s15
+    e('.Lsqr:')
+    e('  s_mov_b32 s19, s15')
+    e('.Lsqr_loop:')
+    e('  s_cmp_eq_u32 s19, 0')
+    e('  s_cbranch_scc1 .Lprog')
+    for k in range(S):
+        e(f'  ds_write_b32 v{V_LDSA}, {X(k)} offset:{k * 256}')
+        if k % 8 == 7:
+            e('  s_waitcnt lgkmcnt(0)')
+    e('  s_waitcnt lgkmcnt(0)')
+    e('  s_branch .Lmontmul')
+
+    # ---------------- Montgomery product ---------------------------------
+    def iteration(u, last_in_block):
+        ai = f"v{V_AI[u % 2]}"
+        nai = f"v{V_AI[(u + 1) % 2]}"
+        q = f"v{V_Q}"
+        # a_i * X into T[u..u+S-1]; q computed off the first column
+        for j in range(S):
+            e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {ai}, {X(j)}, {T(u + j)}')
+            if j == 3:
+                e(f'  v_mul_lo_u32 {q}, {Tlo(u)}, s12')
+            if j == 6:
+                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+            if j == 8:
+                # prefetch next a limb (next iteration / next trip / tail)
+                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * 256}')
+        # q * N into T[u..u+S-1]; carry out of column u into column u+1
+        for j in range(S):
+            e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {q}, s{SN + j}, {T(u + j)}')
+            if j == 3:
+                e(f'  v_lshrrev_b64 v[{V_TMP}:{V_TMP + 1}], {B}, {T(u)}')
+            if j == 7:
+                e(f'  v_lshl_add_u64 {T(u + 1)}, v[{V_TMP}:{V_TMP + 1}], 0, {T(u + 1)}')
+        e('  s_waitcnt lgkmcnt(0)')
+
+    e('.Lmontmul:')
+    for k in range(NT):
+        e(f'  v_mov_b64_e32 {T(k)}, 0')
+    e(f'  v_mov_b32_e32 v{V_LDSI}, v{V_LDSA}')
+    e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
+    e('  s_waitcnt lgkmcnt(0)')
+    if NTRIPS > 0:
+        e(f'  s_mov_b32 s18, {NTRIPS}')
+        e('.Ltrip:')
+        for u in range(U):
+            iteration(u, u == U - 1)
+        # slide the window by U columns
+        for k in range(S):
+            e(f'  v_mov_b64_e32 {T(k)}, {T(k + U)}')
+        for k in range(S, S + U):
+            e(f'  v_mov_b64_e32 {T(k)}, 0')
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(U * 256)}, v{V_LDSI}')
+        e('  s_sub_u32 s18, s18, 1')
+        e('  s_cmp_lg_u32 s18, 0')
+        e('  s_cbranch_scc1 .Ltrip')
+    for u in range(TAIL):
+        iteration(u, u == TAIL - 1)
+    # normalise T[TAIL .. TAIL+S-1] into S radix-2^B limbs of X
+    tmp = f"v[{V_TMP}:{V_TMP + 1}]"
+    e(f'  v_and_b32_e32 {X(0)}, {hex(MASK)}, {Tlo(TAIL)}')
+    e(f'  v_lshrrev_b64 {tmp}, {B}, {T(TAIL)}')
+    for k in range(1, S):
+        e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TAIL + k)}')
+        e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+        if k != S - 1:
+            e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+    # return: s19 == 0 -> dispatcher, else one more squaring
+    e('  s_cmp_eq_u32 s19, 0')
+    e('  s_cbranch_scc1 .Lprog')
+    e('  s_sub_u32 s19, s19, 1')
+    e('  s_branch .Lsqr_loop')
+
+    e('.Lend:')
+    e('  s_endpgm')
+    e(f'.Lfunc_end_{name}:')
+    e(f'  .size {name}, .Lfunc_end_{name}-{name}')
+    e('')
+    # ---- kernel descriptor ------------------------------------------------
+    e('.rodata')
+    e('.p2align 6')
+    e(f'.amdhsa_kernel {name}')
+    e(f'  .amdhsa_group_segment_fixed_size {lds_bytes}')
+    e('  .amdhsa_private_segment_fixed_size 0')
+    e('  .amdhsa_kernarg_size 32')
+    e('  .amdhsa_user_sgpr_count 2')
+    e('  .amdhsa_user_sgpr_kernarg_segment_ptr 1')
+    e('  .amdhsa_system_sgpr_workgroup_id_x 1')
+    e('  .amdhsa_system_vgpr_workitem_id 0')
+    e(f'  .amdhsa_next_free_vgpr {NVGPR}')
+    e(f'  .amdhsa_next_free_sgpr {NSGPR}')
+    e(f'  .amdhsa_accum_offset {((NVGPR + 3) // 4) * 4}')
+    e('  .amdhsa_reserve_vcc 1')
+    e('  .amdhsa_ieee_mode 0')
+    e('  .amdhsa_dx10_clamp 0')
+    e('.end_amdhsa_kernel')
+    e('')
+    # ---- metadata -----------------------------------------------------
+    e('.amdgpu_metadata')
+    e('---')
+    e('amdhsa.kernels:')
+    e('  - .args:')
+    for off_, sz, kind in ((0, 8, 'global_buffer'), (8, 8, 'global_buffer'),
+                           (16, 8, 'global_buffer'), (24, 4, 'by_value'),
+                           (28, 4, 'by_value')):
+        e(f'      - .offset: {off_}')
+        e(f'        .size: {sz}')
+        e(f'        .value_kind: {kind}')
+        if kind == 'global_buffer':
+            e('        .address_space: global')
+    e(f'    .group_segment_fixed_size: {lds_bytes}')
+    e('    .kernarg_segment_align: 8')
+    e('    .kernarg_segment_size: 32')
+    e('    .max_flat_workgroup_size: 256')
+    e(f'    .name: {name}')
+    e('    .private_segment_fixed_size: 0')
+    e(f'    .sgpr_count: {NSGPR + 2}')
+    e(f'    .symbol: {name}.kd')
+    e(f'    .vgpr_count: {NVGPR}')
+    e('    .wavefront_size: 64')
+    e('amdhsa.target: amdgcn-amd-amdhsa--gfx950')
+    e('amdhsa.version:')
+    e('  - 1')
+    e('  - 2')
+    e('...')
+    e('.end_amdgpu_metadata')
+    return "\n".join(o) + "\n"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--limbs', type=int, required=True)
+    ap.add_argument('--bits', type=int, default=28)
+    ap.add_argument('--unroll', type=int, default=12)
+    ap.add_argument('--name', required=True)
+    ap.add_argument('-o', '--out', required=True)
+    a = ap.parse_args()
+    src = gen(a.limbs, a.bits, a.unroll, a.name)
+    with open(a.out, 'w') as f:
+        f.write(src)
+
+
+if __name__ == '__main__':
+    sys.exit(main())
