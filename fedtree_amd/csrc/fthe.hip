@@ -1,0 +1,859 @@
+// fthe.hip -- host side of the MI355X batch Paillier engine: C ABI (include/fthe.h),
+// key set-up, program construction, chunked launch of the montprog kernel and
+// the glue kernels.
+//
+// Data flow of one batch call (device-resident variant):
+//   inputs (AoS u32 words / u64 plaintexts)  --pack-->  slots (radix-2^28, limb-major)
+//   montprog kernel (one ciphertext per lane, uniform op program per modulus)
+//   glue (canonicalise, CRT recombine)  --unpack-->  outputs (AoS u32 words)
+// Batches are processed in chunks of L lanes (default 262144) so the
+// per-lane window tables fit comfortably in HBM.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <vector>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include "../../include/fthe.h"
+#include "bn_host.hpp"
+#include "fthe_glue.h"
+#include "gen/montprog_blobs.h"
+
+using namespace fthe;
+
+#define HIPOK(x) do { if ((x) != hipSuccess) return FTHE_ERR_HIP; } while (0)
+
+namespace {
+
+constexpr int MAX_VARIANTS = 2;
+const int kVariantS[MAX_VARIANTS] = {37, 74};
+
+int variant_index(int S) {
+    for (int i = 0; i < MAX_VARIANTS; i++) if (kVariantS[i] == S) return i;
+    return -1;
+}
+
+uint64_t urandom64() {
+    uint64_t v = 0;
+    int fd = open("/dev/urandom", O_RDONLY);
+    if (fd >= 0) { if (read(fd, &v, sizeof v) != (ssize_t)sizeof v) v = 0; close(fd); }
+    if (!v) v = std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32);
+    return v;
+}
+
+// splitmix64 (seeded key generation / rng keys)
+uint64_t splitmix64(uint64_t &s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+size_t chunk_lanes() {
+    static size_t v = [] {
+        const char *e = getenv("FTHE_CHUNK");
+        size_t c = e ? (size_t)strtoull(e, nullptr, 10) : 262144;
+        c = (c + 255) / 256 * 256;
+        return c < 256 ? (size_t)256 : c;
+    }();
+    return v;
+}
+
+// window width minimising table + multiplications for an e-bit exponent
+int best_window(size_t ebits) {
+    int best = 1; double bc = 1e30;
+    for (int w = 1; w <= 6; w++) {
+        double c = (double)(1 << (w - 1)) + (double)ebits / (w + 1);
+        if (c < bc) { bc = c; best = w; }
+    }
+    return best;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+struct DevBuf {
+    void *p = nullptr; size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return FTHE_OK;
+        if (p) hipFree(p);
+        p = nullptr; n = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) return FTHE_ERR_NOMEM;
+        n = bytes;
+        return FTHE_OK;
+    }
+    ~DevBuf() { if (p) hipFree(p); }
+};
+
+struct fthe_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipModule_t mod[MAX_VARIANTS] = {};
+    hipFunction_t fn[MAX_VARIANTS] = {};
+    DevBuf slots, scratch, io[4];
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_mm = 0;
+    bool timed = false;
+};
+
+// Device copy of one Montgomery modulus.
+struct DevMod {
+    MontMod m;
+    uint32_t *d_ctx = nullptr;     // N limbs (S) + nprime
+};
+
+// A named constant (S limbs) on the device.
+struct fthe_key {
+    int device = 0;
+    int S = 0;                      // kernel limbs for this key
+    int n_bits = 0, n_words = 0;
+    bool priv = false, pub_ok = false;
+    Mpz n, n2, g, p, q, lambda, mu;
+    DevMod mn2, mp2, mq2, mp, mq;
+    int kp = 0, kq = 0;             // limbs of p, q
+    // device constants: one allocation, S limbs each
+    std::vector<std::vector<uint32_t>> host_consts;
+    uint32_t *d_consts = nullptr;
+    // programs: one allocation
+    std::vector<uint32_t> host_progs;
+    uint32_t *d_progs = nullptr;
+    size_t n_words_dev_off = 0;     // offset (in u32) of n words in d_consts
+    uint32_t *d_nwords = nullptr;
+    ~fthe_key() {
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq}) if (d->d_ctx) hipFree(d->d_ctx);
+        if (d_consts) hipFree(d_consts);
+        if (d_progs) hipFree(d_progs);
+        if (d_nwords) hipFree(d_nwords);
+    }
+    // constant handles
+    int add_const(const std::vector<uint32_t> &limbs) {
+        std::vector<uint32_t> v(limbs); v.resize(S, 0);
+        host_consts.push_back(v);
+        return (int)host_consts.size() - 1;
+    }
+    uint32_t *cst(int h) const { return d_consts + (size_t)h * S; }
+    // programs
+    struct PH { size_t off = 0; double mm = 0; };
+    PH add_prog(const Prog &p) {
+        PH h; h.off = host_progs.size(); h.mm = p.montmuls;
+        host_progs.insert(host_progs.end(), p.w.begin(), p.w.end());
+        return h;
+    }
+    const uint32_t *prog(const PH &h) const { return d_progs + h.off; }
+
+    // ---- slot maps and programs --------------------------------------------
+    int w_pub = 5, w_crt = 5, w_dec = 5, tabn_max = 16;
+    // consts
+    int c_one = -1, c_R2n2 = -1, c_nRn2 = -1, c_n2 = -1;
+    int c_R2p = -1, c_R3p = -1, c_nRp = -1, c_R2q = -1, c_R3q = -1, c_nRq = -1;
+    int c_p2 = -1, c_q2 = -1, c_2p2 = -1, c_qinvRp2 = -1;
+    int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
+    PH pr_enc_pub, pr_add, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+};
+
+// slot numbering shared by all programs
+enum Slot : int {
+    SL_IN0 = 0, SL_IN1 = 1, SL_C0 = 2, SL_C1 = 3, SL_C2 = 4, SL_C3 = 5,
+    SL_OUTP = 6, SL_OUTQ = 7, SL_SAVED = 8, SL_SQ = 9, SL_T0 = 10, SL_T1 = 11,
+    SL_T2 = 12, SL_T3 = 13, SL_T4 = 14, SL_T5 = 15, SL_TAB = 16
+};
+
+static int nslots_for(const fthe_key *k) { return SL_TAB + k->tabn_max; }
+
+// ---------------------------------------------------------------------------
+extern "C" int fthe_version(void) { return 100; }
+
+extern "C" const char *fthe_strerror(int s) {
+    switch (s) {
+        case FTHE_OK: return "ok";
+        case FTHE_ERR_ARG: return "invalid argument";
+        case FTHE_ERR_HIP: return "HIP runtime error (no gfx950 device or launch failure)";
+        case FTHE_ERR_NOPRIV: return "private key required";
+        case FTHE_ERR_UNSUPPORTED: return "modulus size not supported by the built kernels";
+        case FTHE_ERR_KEY: return "invalid key material";
+        case FTHE_ERR_NOMEM: return "device allocation failed";
+        default: return "unknown status";
+    }
+}
+
+extern "C" int fthe_kernel_limbs(int bits) { return kernel_limbs_for_bits(bits); }
+
+extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
+    if (!out) return FTHE_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return FTHE_ERR_HIP;
+    HIPOK(hipSetDevice(device));
+    std::unique_ptr<fthe_ctx> c(new fthe_ctx);
+    c->device = device;
+    HIPOK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i < MAX_VARIANTS; i++) {
+        const unsigned char *blob = fthe_montprog_blob(kVariantS[i]);
+        if (!blob) return FTHE_ERR_HIP;
+        HIPOK(hipModuleLoadData(&c->mod[i], blob));
+        char name[64];
+        snprintf(name, sizeof name, "fthe_montprog_s%d", kVariantS[i]);
+        HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
+    }
+    HIPOK(hipEventCreate(&c->ev0));
+    HIPOK(hipEventCreate(&c->ev1));
+    *out = c.release();
+    return FTHE_OK;
+}
+
+extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) hipModuleUnload(c->mod[i]);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" int fthe_ctx_sync(fthe_ctx *c) {
+    if (!c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipStreamSynchronize(c->stream));
+    return FTHE_OK;
+}
+extern "C" void *fthe_ctx_stream(fthe_ctx *c) { return c ? (void *)c->stream : nullptr; }
+extern "C" int fthe_ctx_device(fthe_ctx *c) { return c ? c->device : -1; }
+
+extern "C" double fthe_last_kernel_ms(fthe_ctx *c) {
+    if (!c || !c->timed) return 0.0;
+    float ms = 0;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return 0.0;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return 0.0;
+    return ms;
+}
+extern "C" double fthe_last_montmuls(fthe_ctx *c) { return c ? c->last_mm : 0.0; }
+
+// ---------------------------------------------------------------------------
+// Key set-up
+static int upload_mod(DevMod &d, const mpz_t N, int S) {
+    d.m.init(N, S);
+    if (hipMalloc(&d.d_ctx, d.m.ctx.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    HIPOK(hipMemcpy(d.d_ctx, d.m.ctx.data(), d.m.ctx.size() * 4, hipMemcpyHostToDevice));
+    return FTHE_OK;
+}
+
+static int key_finish(fthe_key *k) {
+    // choose kernel variant
+    int sp = 0;
+    if (k->priv) {
+        Mpz p2; mpz_mul(p2, k->p, k->p);
+        Mpz q2; mpz_mul(q2, k->q, k->q);
+        size_t b = std::max(p2.bits(), q2.bits());
+        sp = kernel_limbs_for_bits((int)b);
+        if (!sp) return FTHE_ERR_UNSUPPORTED;
+    }
+    int sn = kernel_limbs_for_bits((int)k->n2.bits());
+    k->pub_ok = sn != 0;
+    if (!k->pub_ok && !k->priv) return FTHE_ERR_UNSUPPORTED;
+    k->S = std::max(sp, sn);
+    if (!k->pub_ok) k->S = sp;
+    const int S = k->S;
+    Mpz one(1);
+    k->c_one = k->add_const(to_limbs(one, S));
+
+    if (k->pub_ok) {
+        int rc = upload_mod(k->mn2, k->n2, S); if (rc) return rc;
+        k->c_R2n2 = k->add_const(to_limbs(k->mn2.m.R2, S));
+        k->c_nRn2 = k->add_const(k->mn2.m.mont(k->n));
+        k->c_n2 = k->add_const(to_limbs(k->n2, S));
+        // encrypt: X = r R; X^n; (1 + m n) X  (paillier.cpp:135-137 with g^m = 1 + m n)
+        Prog e;
+        k->w_pub = best_window(k->n.bits());
+        e.loadx(SL_IN0); e.mul(SL_C0);
+        e.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
+        e.storex(SL_SAVED);
+        e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);
+        e.storex(SL_OUTP); e.end();
+        k->pr_enc_pub = k->add_prog(e);
+        k->tabn_max = std::max(k->tabn_max, 1 << (k->w_pub - 1));
+        // add: a b R^-1 -> * R2 -> a b mod n^2 (paillier.cpp:103)
+        Prog a;
+        a.loadx(SL_IN0); a.mul(SL_IN1); a.mul(SL_C0); a.storex(SL_OUTP); a.end();
+        k->pr_add = k->add_prog(a);
+    }
+    if (k->priv) {
+        int rc;
+        Mpz p2, q2; mpz_mul(p2, k->p, k->p); mpz_mul(q2, k->q, k->q);
+        if ((rc = upload_mod(k->mp2, p2, S))) return rc;
+        if ((rc = upload_mod(k->mq2, q2, S))) return rc;
+        if ((rc = upload_mod(k->mp, k->p, S))) return rc;
+        if ((rc = upload_mod(k->mq, k->q, S))) return rc;
+        k->kp = (int)((k->p.bits() + RADIX_BITS - 1) / RADIX_BITS);
+        k->kq = (int)((k->q.bits() + RADIX_BITS - 1) / RADIX_BITS);
+        // --- CRT encrypt constants
+        Mpz np, nq, ep, eq, t;
+        mpz_mod(np, k->n, p2); mpz_mod(nq, k->n, q2);
+        Mpz pm1, qm1; mpz_sub_ui(pm1, k->p, 1); mpz_sub_ui(qm1, k->q, 1);
+        mpz_mul(t, k->p, pm1); mpz_mod(ep, k->n, t);     // n mod p(p-1): order of (Z/p^2)^*
+        mpz_mul(t, k->q, qm1); mpz_mod(eq, k->n, t);
+        k->c_R2p = k->add_const(to_limbs(k->mp2.m.R2, S));
+        k->c_nRp = k->add_const(k->mp2.m.mont(np));
+        k->c_R2q = k->add_const(to_limbs(k->mq2.m.R2, S));
+        k->c_nRq = k->add_const(k->mq2.m.mont(nq));
+        k->c_R3p = k->add_const(to_limbs(k->mp2.m.R3, S));
+        k->c_R3q = k->add_const(to_limbs(k->mq2.m.R3, S));
+        k->c_p2 = k->add_const(to_limbs(p2, S));
+        k->c_q2 = k->add_const(to_limbs(q2, S));
+        mpz_mul_2exp(t, p2, 1);
+        k->c_2p2 = k->add_const(to_limbs(t, S));
+        Mpz qi; if (!mpz_invert(qi, q2, p2)) return FTHE_ERR_KEY;
+        k->c_qinvRp2 = k->add_const(k->mp2.m.mont(qi));
+        k->w_crt = best_window(std::max(ep.bits(), eq.bits()));
+        k->tabn_max = std::max(k->tabn_max, 1 << (k->w_crt - 1));
+        for (int side = 0; side < 2; side++) {
+            Prog e;
+            e.loadx(SL_IN0); e.mul(side ? SL_C2 : SL_C0);       // r R mod P^2
+            e.pow(side ? eq : ep, SL_TAB, SL_SQ, k->w_crt);       // r^n R
+            e.storex(SL_SAVED);
+            e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);        // m (n mod P^2)
+            e.addsmall(1); e.mul(SL_SAVED);                      // (1 + m n) r^n mod P^2
+            e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+            (side ? k->pr_enc_q : k->pr_enc_p) = k->add_prog(e);
+        }
+        {   // h = (cp - cq) (q^2)^-1 mod p^2
+            Prog h; h.loadx(SL_T0); h.mul(SL_T1); h.storex(SL_T2); h.end();
+            k->pr_crt_h = k->add_prog(h);
+        }
+        // --- CRT decrypt constants
+        k->c_p = k->add_const(to_limbs(k->p, S));
+        k->c_q = k->add_const(to_limbs(k->q, S));
+        mpz_mul_2exp(t, k->p, 1);
+        k->c_2p = k->add_const(to_limbs(t, S));
+        Mpz m2k, pinv, qinv;
+        mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RADIX_BITS * k->kp);
+        mpz_invert(pinv, k->p, m2k);
+        k->c_pinv = k->add_const(to_limbs(pinv, S));
+        mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RADIX_BITS * k->kq);
+        mpz_invert(qinv, k->q, m2k);
+        k->c_qinv2 = k->add_const(to_limbs(qinv, S));
+        // h_P = L_P(g^(P-1) mod P^2)^-1 mod P
+        for (int side = 0; side < 2; side++) {
+            const Mpz &P = side ? k->q : k->p;
+            const Mpz &P2 = side ? q2 : p2;
+            Mpz Pm1, x, hp; mpz_sub_ui(Pm1, P, 1);
+            mpz_powm(x, k->g, Pm1, P2);
+            mpz_sub_ui(x, x, 1); mpz_tdiv_q(x, x, P);
+            if (!mpz_invert(hp, x, P)) return FTHE_ERR_KEY;
+            int h = k->add_const((side ? k->mq : k->mp).m.mont(hp));
+            (side ? k->c_hRq : k->c_hRp) = h;
+        }
+        Mpz qip; if (!mpz_invert(qip, k->q, k->p)) return FTHE_ERR_KEY;
+        k->c_qinvRp = k->add_const(k->mp.m.mont(qip));
+        k->w_dec = best_window(std::max(pm1.bits(), qm1.bits()));
+        k->tabn_max = std::max(k->tabn_max, 1 << (k->w_dec - 1));
+        for (int side = 0; side < 2; side++) {
+            Prog d;
+            d.loadx(SL_IN1); d.mul(side ? SL_C3 : SL_C1);        // c_hi R^2  (= Montgomery of c_hi R)
+            d.storex(SL_T0);
+            d.loadx(SL_IN0); d.mul(side ? SL_C2 : SL_C0);        // c_lo R
+            d.addslot(SL_T0);                                    // c R mod P^2 (< 4P^2)
+            d.pow(side ? qm1 : pm1, SL_TAB, SL_SQ, k->w_dec);     // c^(P-1) R
+            d.mul(SL_T5);                                        // * 1 -> out of Montgomery
+            d.storex(side ? SL_OUTQ : SL_OUTP); d.end();
+            (side ? k->pr_dec_q : k->pr_dec_p) = k->add_prog(d);
+        }
+        for (int side = 0; side < 2; side++) {
+            Prog d; d.loadx(side ? SL_T2 : SL_T1); d.mul(side ? SL_C1 : SL_C0);
+            d.storex(side ? SL_OUTQ : SL_OUTP); d.end();
+            (side ? k->pr_dec_hq : k->pr_dec_hp) = k->add_prog(d);
+        }
+        {
+            Prog d; d.loadx(SL_T3); d.mul(SL_C2); d.storex(SL_T4); d.end();
+            k->pr_dec_t = k->add_prog(d);
+        }
+    }
+    // upload constants and programs
+    size_t nc = k->host_consts.size();
+    if (hipMalloc(&k->d_consts, nc * S * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    std::vector<uint32_t> flat; flat.reserve(nc * S);
+    for (auto &v : k->host_consts) flat.insert(flat.end(), v.begin(), v.end());
+    HIPOK(hipMemcpy(k->d_consts, flat.data(), flat.size() * 4, hipMemcpyHostToDevice));
+    if (hipMalloc(&k->d_progs, k->host_progs.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    HIPOK(hipMemcpy(k->d_progs, k->host_progs.data(), k->host_progs.size() * 4, hipMemcpyHostToDevice));
+    std::vector<uint32_t> nw(k->n_words);
+    mpz_to_words(k->n, nw.data(), k->n_words);
+    if (hipMalloc(&k->d_nwords, nw.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    HIPOK(hipMemcpy(k->d_nwords, nw.data(), nw.size() * 4, hipMemcpyHostToDevice));
+    return FTHE_OK;
+}
+
+static int key_from_pq(fthe_ctx *ctx, const mpz_t p, const mpz_t q, fthe_key **out) {
+    if (mpz_cmp(p, q) == 0 || mpz_even_p(p) || mpz_even_p(q) || mpz_cmp_ui(p, 2) <= 0 || mpz_cmp_ui(q, 2) <= 0)
+        return FTHE_ERR_KEY;
+    std::unique_ptr<fthe_key> k(new fthe_key);
+    k->device = ctx->device;
+    k->priv = true;
+    mpz_set(k->p, p); mpz_set(k->q, q);
+    mpz_mul(k->n, p, q);                                   // paillier.cpp:82
+    mpz_add_ui(k->g, k->n, 1);                             // :83
+    Mpz pm1, qm1, phi, gcd;
+    mpz_sub_ui(pm1, p, 1); mpz_sub_ui(qm1, q, 1);
+    mpz_mul(phi, pm1, qm1); mpz_gcd(gcd, phi, k->n);
+    if (mpz_cmp_ui(gcd, 1) != 0) return FTHE_ERR_KEY;      // paillier.cpp:60
+    mpz_lcm(k->lambda, pm1, qm1);                          // :84
+    mpz_mul(k->n2, k->n, k->n);
+    Mpz lp; mpz_powm(lp, k->g, k->lambda, k->n2);          // :85
+    mpz_sub_ui(lp, lp, 1); mpz_tdiv_q(lp, lp, k->n);
+    if (!mpz_invert(k->mu, lp, k->n)) return FTHE_ERR_KEY; // :86
+    k->n_bits = (int)k->n.bits();
+    k->n_words = (k->n_bits + 31) / 32;
+    if (hipSetDevice(ctx->device) != hipSuccess) return FTHE_ERR_HIP;
+    int rc = key_finish(k.get());
+    if (rc) return rc;
+    *out = k.release();
+    return FTHE_OK;
+}
+
+extern "C" int fthe_key_from_primes(fthe_ctx *ctx, const uint32_t *p, const uint32_t *q, int w, fthe_key **out) {
+    if (!ctx || !p || !q || w <= 0 || !out) return FTHE_ERR_ARG;
+    Mpz P, Q; mpz_from_words(P, p, w); mpz_from_words(Q, q, w);
+    return key_from_pq(ctx, P, Q, out);
+}
+
+extern "C" int fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out) {
+    if (!ctx || !out || n_bits < 64 || (n_bits & 1)) return FTHE_ERR_ARG;
+    gmp_randstate_t st; gmp_randinit_mt(st);
+    uint64_t s = seed ? seed : urandom64();
+    Mpz sd; mpz_set_ui(sd, (unsigned long)splitmix64(s));
+    mpz_mul_2exp(sd, sd, 64); mpz_add_ui(sd, sd, (unsigned long)splitmix64(s));
+    gmp_randseed(st, sd);
+    int hb = n_bits / 2;
+    int rc = FTHE_ERR_KEY;
+    for (int tries = 0; tries < 64 && rc == FTHE_ERR_KEY; tries++) {
+        Mpz p, q;
+        // top two bits set -> p*q has exactly n_bits bits (GenPrimePair, paillier.cpp:51-61)
+        mpz_urandomb(p, st, hb); mpz_setbit(p, hb - 1); mpz_setbit(p, hb - 2); mpz_nextprime(p, p);
+        mpz_urandomb(q, st, hb); mpz_setbit(q, hb - 1); mpz_setbit(q, hb - 2); mpz_nextprime(q, q);
+        if (p.bits() != (size_t)hb || q.bits() != (size_t)hb) continue;
+        rc = key_from_pq(ctx, p, q, out);
+    }
+    gmp_randclear(st);
+    return rc;
+}
+
+extern "C" int fthe_key_from_n(fthe_ctx *ctx, const uint32_t *n, int n_words, fthe_key **out) {
+    if (!ctx || !n || n_words <= 0 || !out) return FTHE_ERR_ARG;
+    std::unique_ptr<fthe_key> k(new fthe_key);
+    k->device = ctx->device;
+    mpz_from_words(k->n, n, n_words);
+    if (mpz_even_p(k->n) || mpz_cmp_ui(k->n, 3) < 0) return FTHE_ERR_KEY;
+    mpz_add_ui(k->g, k->n, 1);
+    mpz_mul(k->n2, k->n, k->n);
+    k->n_bits = (int)k->n.bits();
+    k->n_words = (k->n_bits + 31) / 32;
+    if (hipSetDevice(ctx->device) != hipSuccess) return FTHE_ERR_HIP;
+    int rc = key_finish(k.get());
+    if (rc) return rc;
+    *out = k.release();
+    return FTHE_OK;
+}
+
+extern "C" void fthe_key_destroy(fthe_key *k) { delete k; }
+extern "C" int fthe_key_n_words(const fthe_key *k) { return k ? k->n_words : 0; }
+extern "C" int fthe_key_n_bits(const fthe_key *k) { return k ? k->n_bits : 0; }
+extern "C" int fthe_key_has_private(const fthe_key *k) { return k ? (int)k->priv : 0; }
+
+extern "C" int fthe_key_export(const fthe_key *k, uint32_t *n, uint32_t *lambda, uint32_t *mu, uint32_t *p, uint32_t *q) {
+    if (!k) return FTHE_ERR_ARG;
+    int w = k->n_words;
+    if (n) mpz_to_words(k->n, n, w);
+    if ((lambda || mu || p || q) && !k->priv) return FTHE_ERR_NOPRIV;
+    if (lambda) mpz_to_words(k->lambda, lambda, w);
+    if (mu) mpz_to_words(k->mu, mu, w);
+    if (p) mpz_to_words(k->p, p, (w + 1) / 2);
+    if (q) mpz_to_words(k->q, q, (w + 1) / 2);
+    return FTHE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Launch helpers
+namespace {
+
+struct Launch {
+    fthe_ctx *c; const fthe_key *k; int L; int S; double mm = 0; size_t live = 0;
+    uint32_t *slot(int s) const { return (uint32_t *)c->slots.p + (size_t)s * S * L; }
+    dim3 grid() const { return dim3((unsigned)(L / 256)); }
+    int prog(const fthe_key::PH &ph, const DevMod &mod) {
+        struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
+            c->slots.p, k->prog(ph), mod.d_ctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4)};
+        size_t sz = sizeof(args);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+        int vi = variant_index(S);
+        if (vi < 0) return FTHE_ERR_UNSUPPORTED;
+        if (hipModuleLaunchKernel(c->fn[vi], L / 256, 1, 1, 256, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
+            return FTHE_ERR_HIP;
+        mm += ph.mm * (double)live;
+        return FTHE_OK;
+    }
+    void fill(int s, int h) {
+        hipLaunchKernelGGL(k_fill_const, grid(), dim3(256), 0, c->stream, k->cst(h), slot(s), S, L);
+    }
+};
+
+int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots) {
+    if (!c || !k) return FTHE_ERR_ARG;
+    if (k->device != c->device) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    size_t ch = chunk_lanes();
+    size_t L = std::min(ch, (count + 255) / 256 * 256);
+    if (L == 0) L = 256;
+    Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = k->S;
+    int rc = c->slots.ensure((size_t)nslots * k->S * L * 4);
+    if (rc) return rc;
+    HIPOK(hipEventRecord(c->ev0, c->stream));
+    return FTHE_OK;
+}
+
+int end_call(fthe_ctx *c, Launch &Lc) {
+    HIPOK(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->last_mm = Lc.mm;
+    if (hipGetLastError() != hipSuccess) return FTHE_ERR_HIP;
+    return FTHE_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Encrypt
+extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count,
+                                    const uint32_t *r, int r_words, uint64_t rng_seed,
+                                    uint32_t *out, int flags) {
+    if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
+    if (r && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
+    bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
+    if (!crt && !k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    Launch Lc;
+    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    if (rc) return rc;
+    const int S = k->S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    // scratch: AoS r words for the device RNG
+    if (!r && (rc = c->scratch.ensure((size_t)L * nw * 4))) return rc;
+    RngKey rk{};
+    if (!r) {
+        uint64_t s = rng_seed ? rng_seed : urandom64();
+        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(s); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
+        rk.nonce = splitmix64(s);
+    }
+    if (crt) {
+        Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
+        Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_nRq);
+        Lc.fill(SL_T1, k->c_qinvRp2);
+    } else {
+        Lc.fill(SL_C0, k->c_R2n2); Lc.fill(SL_C1, k->c_nRn2);
+    }
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        if (r) {
+            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, r + off * r_words, r_words, cnt, 0,
+                               Lc.slot(SL_IN0), S, L);
+        } else {
+            hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_nwords, nw, k->n_bits, rk,
+                               (uint64_t)off, cnt, (uint32_t *)c->scratch.p);
+            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, (const uint32_t *)c->scratch.p, nw,
+                               cnt, 0, Lc.slot(SL_IN0), S, L);
+        }
+        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L);
+        if (crt) {
+            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;
+            if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
+            hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
+                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L);
+            if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L);
+            // c = cq + q^2 h   (< p^2 q^2 = n^2)
+            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
+                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr);
+        } else {
+            if ((rc = Lc.prog(k->pr_enc_pub, k->mn2))) return rc;
+            hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
+                               S, L, cnt, out + off * cw, cw);
+        }
+    }
+    return end_call(c, Lc);
+}
+
+// ---------------------------------------------------------------------------
+// Decrypt (CRT)
+extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count,
+                                uint64_t *m_low, uint32_t *m_full) {
+    if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
+    if (!k->priv) return FTHE_ERR_NOPRIV;
+    Launch Lc;
+    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    if (rc) return rc;
+    const int S = k->S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p);
+    Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_R3q);
+    Lc.fill(SL_T5, k->c_one);
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        const uint32_t *src = ct + off * cw;
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, RADIX_BITS * S,
+                           Lc.slot(SL_IN1), S, L);
+        if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
+        if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) return rc;
+        hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,
+                           k->cst(k->c_pinv), k->kp, Lc.slot(SL_T1), L);
+        hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2), S,
+                           k->cst(k->c_qinv2), k->kq, Lc.slot(SL_T2), L);
+        // slots C0/C1/C2 are reused for the mod-p / mod-q constants of the tail
+        Lc.fill(SL_C0, k->c_hRp); Lc.fill(SL_C1, k->c_hRq); Lc.fill(SL_C2, k->c_qinvRp);
+        if ((rc = Lc.prog(k->pr_dec_hp, k->mp))) return rc;
+        if ((rc = Lc.prog(k->pr_dec_hq, k->mq))) return rc;
+        hipLaunchKernelGGL(k_crt_dec_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
+                           k->cst(k->c_p), k->cst(k->c_q), k->cst(k->c_2p), Lc.slot(SL_T3), S, L);
+        if ((rc = Lc.prog(k->pr_dec_t, k->mp))) return rc;
+        hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T4), k->cst(k->c_p), S, L);
+        // m = mq + q t   (< n)
+        hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S, k->cst(k->c_q),
+                           k->kq, Lc.slot(SL_T4), k->kp, L, cnt, m_full ? m_full + off * nw : (uint32_t *)nullptr, nw,
+                           m_low ? m_low + off : (uint64_t *)nullptr);
+        if (off + L < count) {   // restore the exponentiation constants for the next chunk
+            Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p); Lc.fill(SL_C2, k->c_R2q);
+        }
+    }
+    return end_call(c, Lc);
+}
+
+// ---------------------------------------------------------------------------
+// Add / k-way product / scalar mul (mod n^2)
+extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    Launch Lc;
+    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    if (rc) return rc;
+    const int S = k->S, L = Lc.L, cw = 2 * k->n_words;
+    Lc.fill(SL_C0, k->c_R2n2);
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L);
+        if ((rc = Lc.prog(k->pr_add, k->mn2))) return rc;
+        hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+                           cnt, out + off * cw, cw);
+    }
+    return end_call(c, Lc);
+}
+
+// Programs built per call (k-way product, scalar exponent) go through a
+// per-context device buffer; the stream is drained before it is rewritten.
+static int upload_dyn_prog(fthe_ctx *c, const Prog &p, fthe_key::PH &ph, DevBuf &buf) {
+    HIPOK(hipStreamSynchronize(c->stream));
+    int rc = buf.ensure(p.w.size() * 4);
+    if (rc) return rc;
+    HIPOK(hipMemcpy(buf.p, p.w.data(), p.w.size() * 4, hipMemcpyHostToDevice));
+    ph.off = 0; ph.mm = p.montmuls;
+    return FTHE_OK;
+}
+
+namespace {
+// Launch with an explicit (dynamic) program pointer.
+int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod) {
+    struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
+        Lc.c->slots.p, prog, mod.d_ctx, (uint32_t)Lc.L * 4, (uint32_t)((size_t)Lc.S * Lc.L * 4)};
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    int vi = variant_index(Lc.S);
+    if (vi < 0) return FTHE_ERR_UNSUPPORTED;
+    if (hipModuleLaunchKernel(Lc.c->fn[vi], Lc.L / 256, 1, 1, 256, 1, 1, 0, Lc.c->stream, nullptr, cfg) != hipSuccess)
+        return FTHE_ERR_HIP;
+    Lc.mm += mm * (double)Lc.live;
+    return FTHE_OK;
+}
+}  // namespace
+
+// out[i] = prod_j x[j*count + i] mod n^2.
+// X = x_0;  X <- x_j X R^-1 (j = 1..k-1);  X <- X (R^k mod n^2) R^-1  = prod x_j.
+extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, int kk, size_t count, uint32_t *out) {
+    if (!k || !c || kk <= 0 || kk > 64 || ((!x || !out) && count)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    const int base = nslots_for(k);               // inputs live after the standard slots
+    Launch Lc;
+    int rc = begin_call(c, k, count, Lc, base + kk);
+    if (rc) return rc;
+    const int S = k->S, L = Lc.L, cw = 2 * k->n_words;
+    Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
+    std::vector<uint32_t> rl = to_limbs(Rk, S);
+    Prog p;
+    p.loadx(base);
+    for (int j = 1; j < kk; j++) p.mul(base + j);
+    p.mul(SL_C0);
+    p.storex(SL_OUTP); p.end();
+    std::vector<uint32_t> blob(p.w);
+    size_t prog_words = blob.size();
+    blob.insert(blob.end(), rl.begin(), rl.end());      // constant after the program
+    fthe_key::PH ph;
+    Prog tmp; tmp.w = blob; tmp.montmuls = p.montmuls;
+    if ((rc = upload_dyn_prog(c, tmp, ph, c->io[3]))) return rc;
+    HIPOK(hipEventRecord(c->ev0, c->stream));
+    const uint32_t *dconst = (const uint32_t *)c->io[3].p + prog_words;
+    hipLaunchKernelGGL(k_fill_const, Lc.grid(), dim3(256), 0, c->stream, dconst, Lc.slot(SL_C0), S, L);
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        for (int j = 0; j < kk; j++)
+            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + ((size_t)j * count + off) * cw, cw,
+                               cnt, 0, Lc.slot(base + j), S, L);
+        if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
+        hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+                           cnt, out + off * cw, cw);
+    }
+    return end_call(c, Lc);
+}
+
+// out[i] = x[i]^e mod n^2 (Paillier::mul, paillier.cpp:118), e uniform.
+extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, uint64_t e, size_t count, uint32_t *out) {
+    if (!k || !c || ((!x || !out) && count)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    Launch Lc;
+    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    if (rc) return rc;
+    const int S = k->S, L = Lc.L, cw = 2 * k->n_words;
+    Prog p;
+    if (e == 0) {
+        p.loadx(SL_C1);                 // x^0 = 1
+    } else {
+        Mpz ez; mpz_import(ez, 1, -1, 8, 0, 0, &e);
+        p.loadx(SL_IN0); p.mul(SL_C0);   // Montgomery form
+        p.pow(ez, SL_TAB, SL_SQ, std::min(best_window(ez.bits()), 5));
+        p.mul(SL_C1);                    // * 1 -> out of Montgomery
+    }
+    p.storex(SL_OUTP); p.end();
+    fthe_key::PH ph;
+    if ((rc = upload_dyn_prog(c, p, ph, c->io[3]))) return rc;
+    HIPOK(hipEventRecord(c->ev0, c->stream));
+    Lc.fill(SL_C0, k->c_R2n2); Lc.fill(SL_C1, k->c_one);
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L);
+        if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
+        hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+                           cnt, out + off * cw, cw);
+    }
+    return end_call(c, Lc);
+}
+
+// ---------------------------------------------------------------------------
+// Host-resident variants: stage through device buffers, synchronous.
+namespace {
+struct HostIO {
+    fthe_ctx *c;
+    int in(int i, const void *h, size_t bytes, void **d) {
+        int rc = c->io[i].ensure(bytes ? bytes : 4);
+        if (rc) return rc;
+        if (bytes) HIPOK(hipMemcpyAsync(c->io[i].p, h, bytes, hipMemcpyHostToDevice, c->stream));
+        *d = c->io[i].p;
+        return FTHE_OK;
+    }
+    int outbuf(int i, size_t bytes, void **d) {
+        int rc = c->io[i].ensure(bytes ? bytes : 4);
+        if (rc) return rc;
+        *d = c->io[i].p;
+        return FTHE_OK;
+    }
+    int back(void *h, const void *d, size_t bytes) {
+        if (bytes) HIPOK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPOK(hipStreamSynchronize(c->stream));
+        return FTHE_OK;
+    }
+};
+}  // namespace
+
+extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
+                                int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
+    if (!k || !c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HostIO io{c}; void *dm, *dr = nullptr, *dc; int rc;
+    size_t cw = 2 * (size_t)k->n_words;
+    if ((rc = io.in(0, m, count * 8, &dm))) return rc;
+    if (r && (rc = io.in(1, r, count * r_words * 4, &dr))) return rc;
+    if ((rc = io.outbuf(2, count * cw * 4, &dc))) return rc;
+    if ((rc = fthe_encrypt_u64_dev(k, c, (const uint64_t *)dm, count, (const uint32_t *)dr, r_words, rng_seed,
+                                   (uint32_t *)dc, flags))) return rc;
+    return io.back(out, dc, count * cw * 4);
+}
+
+extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full) {
+    if (!k || !c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HostIO io{c}; void *dc, *dl = nullptr, *df = nullptr; int rc;
+    size_t cw = 2 * (size_t)k->n_words;
+    if ((rc = io.in(0, ct, count * cw * 4, &dc))) return rc;
+    if (m_low && (rc = io.outbuf(1, count * 8, &dl))) return rc;
+    if (m_full && (rc = io.outbuf(2, count * k->n_words * 4, &df))) return rc;
+    if ((rc = fthe_decrypt_dev(k, c, (const uint32_t *)dc, count, (uint64_t *)dl, (uint32_t *)df))) return rc;
+    if (m_low && (rc = io.back(m_low, dl, count * 8))) return rc;
+    if (m_full && (rc = io.back(m_full, df, count * k->n_words * 4))) return rc;
+    return fthe_ctx_sync(c);
+}
+
+extern "C" int fthe_add(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    if (!k || !c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HostIO io{c}; void *da, *db, *dout; int rc;
+    size_t bytes = count * 2 * (size_t)k->n_words * 4;
+    if ((rc = io.in(0, a, bytes, &da))) return rc;
+    if ((rc = io.in(1, b, bytes, &db))) return rc;
+    if ((rc = io.outbuf(2, bytes, &dout))) return rc;
+    if ((rc = fthe_add_dev(k, c, (const uint32_t *)da, (const uint32_t *)db, count, (uint32_t *)dout))) return rc;
+    return io.back(out, dout, bytes);
+}
+
+extern "C" int fthe_reduce_kway(fthe_key *k, fthe_ctx *c, const uint32_t *x, int kk, size_t count, uint32_t *out) {
+    if (!k || !c || kk <= 0) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HostIO io{c}; void *dx, *dout; int rc;
+    size_t bytes = count * 2 * (size_t)k->n_words * 4;
+    if ((rc = io.in(0, x, bytes * kk, &dx))) return rc;
+    if ((rc = io.outbuf(2, bytes, &dout))) return rc;
+    if ((rc = fthe_reduce_kway_dev(k, c, (const uint32_t *)dx, kk, count, (uint32_t *)dout))) return rc;
+    return io.back(out, dout, bytes);
+}
+
+extern "C" int fthe_scalar_mul_u64(fthe_key *k, fthe_ctx *c, const uint32_t *x, uint64_t e, size_t count, uint32_t *out) {
+    if (!k || !c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HostIO io{c}; void *dx, *dout; int rc;
+    size_t bytes = count * 2 * (size_t)k->n_words * 4;
+    if ((rc = io.in(0, x, bytes, &dx))) return rc;
+    if ((rc = io.outbuf(2, bytes, &dout))) return rc;
+    if ((rc = fthe_scalar_mul_u64_dev(k, c, (const uint32_t *)dx, e, count, (uint32_t *)dout))) return rc;
+    return io.back(out, dout, bytes);
+}
+
+// ---------------------------------------------------------------------------
+// Codec
+extern "C" int fthe_encode_fixed_dev(fthe_ctx *c, const float *x, size_t count, uint64_t *m) {
+    if (!c) return FTHE_ERR_ARG;
+    if (!count) return FTHE_OK;
+    HIPOK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, c->stream, x, count, m);
+    return hipGetLastError() == hipSuccess ? FTHE_OK : FTHE_ERR_HIP;
+}
+extern "C" int fthe_decode_fixed_dev(fthe_ctx *c, const uint64_t *m, size_t count, float *x) {
+    if (!c) return FTHE_ERR_ARG;
+    if (!count) return FTHE_OK;
+    HIPOK(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, c->stream, m, count, x);
+    return hipGetLastError() == hipSuccess ? FTHE_OK : FTHE_ERR_HIP;
+}

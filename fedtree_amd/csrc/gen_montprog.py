@@ -131,10 +131,11 @@ def gen(S: int, B: int, U: int, name: str) -> str:
     e('  s_branch .Lend')
 
     def slot_addr():
-        # s[16:17] = slots + arg*slot_stride
+        # s[16:17] = slots + arg*slot_stride   (64-bit: slot regions exceed 4 GiB)
         e('  s_mul_i32 s16, s15, s11')
+        e('  s_mul_hi_u32 s17, s15, s11')
         e('  s_add_u32 s16, s4, s16')
-        e('  s_addc_u32 s17, s5, 0')
+        e('  s_addc_u32 s17, s5, s17')
 
     def step_addr():
         e('  s_add_u32 s16, s16, s10')

@@ -1,0 +1,152 @@
+/*
+ * fthe.h -- C ABI of the MI355X batch Paillier engine ("FedTree HE").
+ *
+ * Drop-in boundary for FedTree's homomorphic-encryption interface.  Every
+ * entry point below replaces a reference call (file:line relative to the
+ * FedTree source tree); INTEGRATION.md shows the C++ shim a FedTree build
+ * would compile (USE_HIP) and the ctypes binding used by the Python mirror.
+ *
+ * Conventions
+ *   - Big integers are little-endian arrays of uint32 words, the order of
+ *     mpz_import/mpz_export(order=-1, size=4) used by the reference GPU path
+ *     (paillier_gpu.cu:7,18).  A key of n_words words has ciphertexts of
+ *     2*n_words words.
+ *   - Plaintexts are the 64-bit fixed-point codec values of common.h:81-86 /
+ *     :127 ((uint64)(int64)((double)x*1e6)); decryption returns the low 64
+ *     bits, which is what the reference decodes (paillier_gpu.cu:485-488).
+ *   - "_dev" calls take device pointers and are asynchronous on the context's
+ *     stream; the plain calls take host pointers and are synchronous.
+ *   - All calls return FTHE_OK (0) or a negative status; nothing aborts.
+ *   - Thread safety: a context may be used by one host thread at a time;
+ *     create one context per host thread / device (callers enter the boundary
+ *     from OpenMP regions, FLtrainer.cpp:275-306).  Keys are immutable after
+ *     creation and may be shared between contexts on the same device.
+ *   - There is no CPU fallback: without a gfx950 device every compute call
+ *     fails with FTHE_ERR_HIP.
+ */
+#ifndef FTHE_H
+#define FTHE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FTHE_OK               0
+#define FTHE_ERR_ARG         -1   /* bad argument / size */
+#define FTHE_ERR_HIP         -2   /* HIP runtime failure, no device, kernel load */
+#define FTHE_ERR_NOPRIV      -3   /* private key required (decrypt, CRT) */
+#define FTHE_ERR_UNSUPPORTED -4   /* modulus size not built */
+#define FTHE_ERR_KEY         -5   /* invalid key material (mu not invertible, p==q, ...) */
+#define FTHE_ERR_NOMEM       -6
+
+/* fthe_encrypt flags */
+#define FTHE_ENC_DEFAULT      0   /* CRT when the private key is present */
+#define FTHE_ENC_PUBLIC       1   /* force the public-key (no CRT) formula */
+
+typedef struct fthe_ctx fthe_ctx;
+typedef struct fthe_key fthe_key;
+
+int         fthe_version(void);
+const char *fthe_strerror(int status);
+
+/* ---- device context (one HIP stream + workspace) ------------------------ */
+int   fthe_ctx_create(int device, fthe_ctx **out);
+void  fthe_ctx_destroy(fthe_ctx *ctx);
+int   fthe_ctx_sync(fthe_ctx *ctx);
+void *fthe_ctx_stream(fthe_ctx *ctx);       /* hipStream_t */
+int   fthe_ctx_device(fthe_ctx *ctx);
+
+/* ---- keys ----------------------------------------------------------------
+ * fthe_key_generate      Paillier::keygen(int keyLength), paillier.cpp:66-90:
+ *                        n has exactly n_bits bits (NTL semantics),
+ *                        g = n+1, lambda = lcm(p-1,q-1), mu = L(g^lambda)^-1.
+ *                        seed 0 draws primes from /dev/urandom; a nonzero seed
+ *                        is deterministic (tests, benchmarks).
+ * fthe_key_from_primes   same derivation from caller primes (injected keys).
+ * fthe_key_from_n        public key only: Paillier::operator=, paillier.h:12-18
+ *                        (copies modulus/generator/keyLength only).
+ */
+int  fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out);
+int  fthe_key_from_primes(fthe_ctx *ctx, const uint32_t *p, const uint32_t *q,
+                          int pq_words, fthe_key **out);
+int  fthe_key_from_n(fthe_ctx *ctx, const uint32_t *n, int n_words, fthe_key **out);
+void fthe_key_destroy(fthe_key *key);
+int  fthe_key_n_words(const fthe_key *key);
+int  fthe_key_n_bits(const fthe_key *key);
+int  fthe_key_has_private(const fthe_key *key);
+/* Each output (nullable) is n_words words; p and q are n_words/2 words. */
+int  fthe_key_export(const fthe_key *key, uint32_t *n, uint32_t *lambda,
+                     uint32_t *mu, uint32_t *p, uint32_t *q);
+
+/* ---- encrypt: c = g^m * r^n mod n^2 (paillier.cpp:134-137) ----------------
+ * Replaces Paillier::encrypt (paillier.cpp:122), Paillier_GMP::encrypt
+ * (paillier_gmp.cpp:37) and Paillier_GPU::encrypt (paillier_gpu.cu:211).
+ * r:       NULL -> a fresh uniform r in [1,n) per ciphertext from a device
+ *          ChaCha20 stream keyed by rng_seed (0 -> /dev/urandom);
+ *          else count*r_words words, r < n (injected randomness: parity,
+ *          reference-compat shared r of paillier_gpu.cu:262-272).
+ * c:       count * 2*n_words words. */
+int fthe_encrypt_u64_dev(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
+                         const uint32_t *r, int r_words, uint64_t rng_seed,
+                         uint32_t *c, int flags);
+int fthe_encrypt_u64(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
+                     const uint32_t *r, int r_words, uint64_t rng_seed,
+                     uint32_t *c, int flags);
+
+/* ---- decrypt: m = L(c^lambda mod n^2) * mu mod n (paillier.cpp:153-156) ---
+ * Computed with CRT over p^2, q^2 (identical canonical result).
+ * Replaces Paillier::decrypt (paillier.cpp:141), Paillier_GMP::decrypt
+ * (paillier_gmp.cpp:75), Paillier_GPU::decrypt (paillier_gpu.cu:448,497).
+ * m_low:   count uint64 (low 64 bits of the plaintext), nullable.
+ * m_full:  count * n_words words (full plaintext), nullable. */
+int fthe_decrypt_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t count,
+                     uint64_t *m_low, uint32_t *m_full);
+int fthe_decrypt(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t count,
+                 uint64_t *m_low, uint32_t *m_full);
+
+/* ---- homomorphic add: x*y mod n^2 (paillier.cpp:103) ------------------------
+ * Replaces Paillier::add / Paillier_GMP::add (paillier_gmp.cpp:16) and
+ * Paillier_GPU::add (paillier_gpu.cu:58).  Alias-safe: out may equal a or b
+ * (fixes SURVEY Q11, where add(s,s,c) zeroes s). */
+int fthe_add_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
+                 size_t count, uint32_t *out);
+int fthe_add(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
+             size_t count, uint32_t *out);
+
+/* ---- scalar mul: x^k mod n^2 (paillier.cpp:118), one k for the batch ------
+ * The reference only multiplies by (unsigned long)-1 (subtraction,
+ * common.h:264-267,311-317). */
+int fthe_scalar_mul_u64_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, uint64_t k,
+                            size_t count, uint32_t *out);
+int fthe_scalar_mul_u64(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, uint64_t k,
+                        size_t count, uint32_t *out);
+
+/* ---- k-way product (k-party histogram merge) ---------------------------
+ * out[i] = prod_{j<k} x[j*count + i] mod n^2.
+ * merge_histograms_server_propose, hist_tree_builder.cpp:1015-1058 (the
+ * reference's first add into an unencrypted zero is a fresh encrypt(0),
+ * pass that ciphertext as one of the k inputs to reproduce it). */
+int fthe_reduce_kway_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, int k,
+                         size_t count, uint32_t *out);
+int fthe_reduce_kway(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, int k,
+                     size_t count, uint32_t *out);
+
+/* ---- fixed-point codec (common.h:81-86,127-128,140-143) ------------------- */
+int fthe_encode_fixed_dev(fthe_ctx *ctx, const float *x, size_t count, uint64_t *m);
+int fthe_decode_fixed_dev(fthe_ctx *ctx, const uint64_t *m, size_t count, float *x);
+
+/* ---- profiling hooks: time of the last call's kernels on the stream ------ */
+double fthe_last_kernel_ms(fthe_ctx *ctx);
+/* Montgomery products executed by the last call (for roofline accounting). */
+double fthe_last_montmuls(fthe_ctx *ctx);
+/* limb count S of the radix-2^28 kernel used for a modulus of `bits` bits
+ * (0 if unsupported). */
+int    fthe_kernel_limbs(int bits);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FTHE_H */
