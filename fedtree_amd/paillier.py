@@ -1,0 +1,397 @@
+"""Host-side mirror of FedTree's homomorphic-encryption interface over libfthe.so.
+
+Reference interface (FedTree, file:line):
+  Paillier            include/FedTree/Encryption/paillier.h:6-41, src/.../paillier.cpp
+  Paillier_GPU        include/FedTree/Encryption/paillier_gpu.h:28-94, paillier_gpu.cu
+  GHPair HE codec     include/FedTree/common.h:65-412
+  Server HE methods   include/FedTree/FL/server.h:58-135
+  Party HE methods    include/FedTree/FL/party.h:118-142
+
+Every computation goes through the HIP engine (libfthe.so).  There is no CPU
+fallback: without the library or a gfx950 device the constructors raise.
+Ciphertexts are numpy uint32 arrays of shape (count, 2*n_words), the
+little-endian word order of mpz_export(order=-1) (paillier_gpu.cu:7,18); batch
+calls also accept torch tensors resident on the device (the *_dev paths).
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib
+
+MINUS_ONE = 2**64 - 1   # (unsigned long)-1, common.h:264-267 / :311
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _words(x, nw):
+    return np.array([(x >> (32 * i)) & 0xFFFFFFFF for i in range(nw)], dtype=np.uint32)
+
+
+def _int(w):
+    v = 0
+    for x in np.asarray(w, dtype=np.uint64)[::-1]:
+        v = (v << 32) | int(x)
+    return v
+
+
+# --------------------------------------------------------------------------
+# codec (common.h:81-86, 127-128, 140-143): host marshalling, as the reference
+# does it on the host (paillier_gpu.cu:240-251, 480-489).
+def encode_fixed(x):
+    """(uint64)(long)((double)x * 1e6), truncating toward zero."""
+    v = np.trunc(np.asarray(x, dtype=np.float32).astype(np.float64) * 1e6)
+    return v.astype(np.int64).view(np.uint64)
+
+
+def decode_fixed(m):
+    """(float)((float)(long)low64 / 1e6)."""
+    v = np.asarray(m, dtype=np.uint64).view(np.int64)
+    return (v.astype(np.float32).astype(np.float64) / 1e6).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
+class Device:
+    """One engine context (HIP stream + workspace) on one GPU.
+
+    The C ABI context is single-threaded; Device.current() hands each host
+    thread its own context, so callers may enter from OpenMP-style thread
+    pools as FedTree does (FLtrainer.cpp:275-306)."""
+
+    _tls = threading.local()
+
+    def __init__(self, device=0):
+        self.lib = _lib.load()
+        self.ctx = ctypes.c_void_p()
+        _lib.check(self.lib.fthe_ctx_create(int(device), ctypes.byref(self.ctx)), "fthe_ctx_create")
+        self.device = int(device)
+
+    @classmethod
+    def current(cls, device=0):
+        d = getattr(cls._tls, "devs", None)
+        if d is None:
+            d = cls._tls.devs = {}
+        if device not in d:
+            d[device] = cls(device)
+        return d[device]
+
+    def sync(self):
+        _lib.check(self.lib.fthe_ctx_sync(self.ctx), "sync")
+
+    def last_kernel_ms(self):
+        return self.lib.fthe_last_kernel_ms(self.ctx)
+
+    def last_montmuls(self):
+        return self.lib.fthe_last_montmuls(self.ctx)
+
+    def close(self):
+        if self.ctx:
+            self.lib.fthe_ctx_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Paillier:
+    """Paillier key + batch engine (mirror of Paillier / Paillier_GPU).
+
+    Public fields follow paillier.h: modulus, generator, keyLength, p, q,
+    lambda_ (lambda), u (mu).  `keyLength` is the bit length of n, as in the
+    NTL build (paillier.cpp:53-54)."""
+
+    def __init__(self, device=None):
+        self.dev = device if isinstance(device, Device) else Device.current(device or 0)
+        self.lib = self.dev.lib
+        self._key = None
+        self.modulus = self.generator = None
+        self.keyLength = 0
+        self.p = self.q = self.lambda_ = self.u = None
+
+    # ---- key management -------------------------------------------------
+    def _adopt(self, key):
+        if self._key:
+            self.lib.fthe_key_destroy(self._key)
+        self._key = key
+        self.n_words = self.lib.fthe_key_n_words(key)
+        nw = self.n_words
+        n = np.zeros(nw, np.uint32)
+        if self.lib.fthe_key_has_private(key):
+            lam, mu = np.zeros(nw, np.uint32), np.zeros(nw, np.uint32)
+            p, q = np.zeros((nw + 1) // 2, np.uint32), np.zeros((nw + 1) // 2, np.uint32)
+            _lib.check(self.lib.fthe_key_export(key, _ptr(n), _ptr(lam), _ptr(mu), _ptr(p), _ptr(q)), "export")
+            self.lambda_, self.u, self.p, self.q = _int(lam), _int(mu), _int(p), _int(q)
+        else:
+            _lib.check(self.lib.fthe_key_export(key, _ptr(n), None, None, None, None), "export")
+        self.modulus = _int(n)
+        self.generator = self.modulus + 1
+        self.keyLength = self.modulus.bit_length()
+        self.n2 = self.modulus * self.modulus
+        return self
+
+    def keygen(self, keyLength, seed=0):
+        """Paillier::keygen(int keyLength) (paillier.cpp:66-90)."""
+        key = ctypes.c_void_p()
+        _lib.check(self.lib.fthe_key_generate(self.dev.ctx, int(keyLength), int(seed), ctypes.byref(key)), "keygen")
+        return self._adopt(key)
+
+    @classmethod
+    def from_primes(cls, p, q, device=None):
+        self = cls(device)
+        hw = max((p.bit_length() + 31) // 32, (q.bit_length() + 31) // 32)
+        pw, qw = _words(p, hw), _words(q, hw)
+        key = ctypes.c_void_p()
+        _lib.check(self.lib.fthe_key_from_primes(self.dev.ctx, _ptr(pw), _ptr(qw), hw, ctypes.byref(key)),
+                   "key_from_primes")
+        return self._adopt(key)
+
+    @classmethod
+    def from_public(cls, n, device=None):
+        self = cls(device)
+        nw = (n.bit_length() + 31) // 32
+        w = _words(n, nw)
+        key = ctypes.c_void_p()
+        _lib.check(self.lib.fthe_key_from_n(self.dev.ctx, _ptr(w), nw, ctypes.byref(key)), "key_from_n")
+        return self._adopt(key)
+
+    def public(self):
+        """Paillier::operator= (paillier.h:12-18): copies modulus, generator, keyLength only."""
+        return Paillier.from_public(self.modulus, self.dev)
+
+    @property
+    def has_private(self):
+        return bool(self._key) and bool(self.lib.fthe_key_has_private(self._key))
+
+    def __del__(self):
+        try:
+            if self._key:
+                self.lib.fthe_key_destroy(self._key)
+        except Exception:
+            pass
+
+    # ---- batch API (host arrays) ---------------------------------------------
+    def _cw(self):
+        return 2 * self.n_words
+
+    def encrypt_u64(self, m, r=None, seed=0, public=False):
+        """c = g^m r^n mod n^2 for every m (paillier.cpp:134-137).
+        r: None -> fresh uniform r per ciphertext from the device CSPRNG;
+           else (count, n_words) uint32 words or a list of ints."""
+        m = np.ascontiguousarray(m, dtype=np.uint64).reshape(-1)
+        cnt = len(m)
+        out = np.zeros((cnt, self._cw()), dtype=np.uint32)
+        rw = None
+        if r is not None:
+            if not isinstance(r, np.ndarray):
+                r = np.stack([_words(int(x), self.n_words) for x in r]) if cnt else np.zeros((0, self.n_words), np.uint32)
+            rw = np.ascontiguousarray(r, dtype=np.uint32).reshape(cnt, -1)
+        flags = _lib.FTHE_ENC_PUBLIC if public else _lib.FTHE_ENC_DEFAULT
+        _lib.check(self.lib.fthe_encrypt_u64(self._key, self.dev.ctx, _ptr(m), cnt, _ptr(rw),
+                                             rw.shape[1] if rw is not None else 0, int(seed), _ptr(out), flags),
+                   "encrypt")
+        return out
+
+    def decrypt_u64(self, c, full=False):
+        """Low 64 bits of m = L(c^lambda mod n^2) mu mod n (paillier.cpp:153-156)."""
+        c = np.ascontiguousarray(c, dtype=np.uint32).reshape(-1, self._cw())
+        cnt = len(c)
+        low = np.zeros(cnt, dtype=np.uint64)
+        fullw = np.zeros((cnt, self.n_words), dtype=np.uint32) if full else None
+        _lib.check(self.lib.fthe_decrypt(self._key, self.dev.ctx, _ptr(c), cnt, _ptr(low), _ptr(fullw)), "decrypt")
+        return (low, fullw) if full else low
+
+    def add_batch(self, a, b):
+        """x*y mod n^2 (paillier.cpp:103), alias-safe."""
+        a = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self._cw())
+        b = np.ascontiguousarray(b, dtype=np.uint32).reshape(-1, self._cw())
+        out = np.zeros_like(a)
+        _lib.check(self.lib.fthe_add(self._key, self.dev.ctx, _ptr(a), _ptr(b), len(a), _ptr(out)), "add")
+        return out
+
+    def reduce_kway(self, x):
+        """x: (k, count, 2nw) -> prod over k (hist_tree_builder.cpp:1015-1058 merge)."""
+        x = np.ascontiguousarray(x, dtype=np.uint32)
+        k, cnt = x.shape[0], x.shape[1]
+        out = np.zeros((cnt, self._cw()), dtype=np.uint32)
+        _lib.check(self.lib.fthe_reduce_kway(self._key, self.dev.ctx, _ptr(x), k, cnt, _ptr(out)), "reduce_kway")
+        return out
+
+    def scalar_mul(self, x, k):
+        """x^k mod n^2 (paillier.cpp:118), k < 2^64."""
+        x = np.ascontiguousarray(x, dtype=np.uint32).reshape(-1, self._cw())
+        out = np.zeros_like(x)
+        _lib.check(self.lib.fthe_scalar_mul_u64(self._key, self.dev.ctx, _ptr(x), int(k), len(x), _ptr(out)),
+                   "scalar_mul")
+        return out
+
+    # ---- device-resident batch API (torch tensors on this device) -------------
+    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False):
+        flags = _lib.FTHE_ENC_PUBLIC if public else _lib.FTHE_ENC_DEFAULT
+        rp = ctypes.c_void_p(r.data_ptr()) if r is not None else None
+        rw = r.shape[-1] if r is not None else 0
+        _lib.check(self.lib.fthe_encrypt_u64_dev(self._key, self.dev.ctx, ctypes.c_void_p(m.data_ptr()), m.numel(),
+                                                 rp, rw, int(seed), ctypes.c_void_p(out.data_ptr()), flags),
+                   "encrypt_dev")
+        return out
+
+    def decrypt_u64_dev(self, c, out_low):
+        cnt = c.numel() // self._cw()
+        _lib.check(self.lib.fthe_decrypt_dev(self._key, self.dev.ctx, ctypes.c_void_p(c.data_ptr()), cnt,
+                                             ctypes.c_void_p(out_low.data_ptr()), None), "decrypt_dev")
+        return out_low
+
+    def add_dev(self, a, b, out):
+        cnt = a.numel() // self._cw()
+        _lib.check(self.lib.fthe_add_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),
+                                         ctypes.c_void_p(b.data_ptr()), cnt, ctypes.c_void_p(out.data_ptr())),
+                   "add_dev")
+        return out
+
+    def reduce_kway_dev(self, x, k, out):
+        cnt = out.numel() // self._cw()
+        _lib.check(self.lib.fthe_reduce_kway_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), int(k),
+                                                 cnt, ctypes.c_void_p(out.data_ptr())), "reduce_kway_dev")
+        return out
+
+    # ---- reference single-value signatures (batch of one) ------------------
+    def encrypt(self, message, r=None):
+        """Paillier::encrypt(const ZZ&) (paillier.cpp:122).  message < 2^64."""
+        c = self.encrypt_u64(np.array([int(message) % 2**64], np.uint64), None if r is None else [int(r)])
+        return _int(c[0])
+
+    def decrypt(self, ciphertext):
+        """Paillier::decrypt(const ZZ&) (paillier.cpp:141): the full plaintext."""
+        c = _words(int(ciphertext), self._cw())[None]
+        _, full = self.decrypt_u64(c, full=True)
+        return _int(full[0])
+
+    def add(self, x, y):
+        """Paillier::add (paillier.cpp:92)."""
+        return _int(self.add_batch(_words(int(x), self._cw())[None], _words(int(y), self._cw())[None])[0])
+
+    def mul(self, x, y):
+        """Paillier::mul (paillier.cpp:107), exponent y < 2^64."""
+        if not 0 <= int(y) < 2**64:
+            raise ValueError("exponent must fit in 64 bits (the reference only uses (unsigned long)-1)")
+        return _int(self.scalar_mul(_words(int(x), self._cw())[None], int(y))[0])
+
+
+# --------------------------------------------------------------------------
+class GHPairs:
+    """A batch of GHPair (common.h:65-412): float g, h plus ciphertexts g_enc,
+    h_enc and the `encrypted` flag.  Arrays are numpy; ciphertexts are
+    (count, 2*n_words) uint32."""
+
+    def __init__(self, g, h=None, paillier=None):
+        self.g = np.ascontiguousarray(g, dtype=np.float32).copy()
+        self.h = np.ascontiguousarray(h if h is not None else g, dtype=np.float32).copy()
+        self.encrypted = False
+        self.g_enc = self.h_enc = None
+        self.paillier = paillier
+
+    def __len__(self):
+        return len(self.g)
+
+    def homo_encrypt(self, pl, r_g=None, r_h=None, seed=0):
+        """GHPair::homo_encrypt (common.h:125-134): encrypt g,h, zero them, set encrypted."""
+        if self.encrypted:
+            return self
+        m = np.concatenate([encode_fixed(self.g), encode_fixed(self.h)])
+        r = None
+        if r_g is not None:
+            r = np.concatenate([np.asarray(r_g, np.uint32).reshape(len(self), -1),
+                                np.asarray(r_h, np.uint32).reshape(len(self), -1)])
+        c = pl.encrypt_u64(m, r=r, seed=seed)
+        self.g_enc, self.h_enc = c[:len(self)], c[len(self):]
+        self.paillier = pl
+        self.g[:] = 0
+        self.h[:] = 0
+        self.encrypted = True
+        return self
+
+    def homo_decrypt(self, pl):
+        """GHPair::homo_decrypt (common.h:136-146): g = (float)(long)dec / 1e6."""
+        if not self.encrypted:
+            return self
+        low = pl.decrypt_u64(np.concatenate([self.g_enc, self.h_enc]))
+        self.g = decode_fixed(low[:len(self)])
+        self.h = decode_fixed(low[len(self):])
+        self.encrypted = False
+        return self
+
+    def _enc_side(self, pl):
+        t = GHPairs(self.g, self.h)
+        return t.homo_encrypt(pl)
+
+    def __add__(self, rhs):
+        """GHPair::operator+ (common.h:150-195).  An unencrypted side is first
+        encrypted with a fresh r."""
+        if not self.encrypted and not rhs.encrypted:
+            return GHPairs(self.g + rhs.g, self.h + rhs.h)
+        pl = rhs.paillier if not self.encrypted else self.paillier
+        lhs = self if self.encrypted else self._enc_side(pl)
+        r = rhs if rhs.encrypted else rhs._enc_side(pl)
+        res = GHPairs(np.zeros(len(self), np.float32), np.zeros(len(self), np.float32), pl)
+        both = pl.add_batch(np.concatenate([lhs.g_enc, lhs.h_enc]), np.concatenate([r.g_enc, r.h_enc]))
+        res.g_enc, res.h_enc = both[:len(self)], both[len(self):]
+        res.encrypted = True
+        return res
+
+    def __sub__(self, rhs):
+        """GHPair::operator- (common.h:253-337): rhs^(2^64-1) then add; an
+        unencrypted rhs is negated and encrypted."""
+        if not self.encrypted and not rhs.encrypted:
+            return GHPairs(self.g - rhs.g, self.h - rhs.h)
+        if not rhs.encrypted:
+            neg = GHPairs(-rhs.g, -rhs.h)
+            return self + neg._enc_side(self.paillier)
+        pl = rhs.paillier if not self.encrypted else self.paillier
+        negc = pl.scalar_mul(np.concatenate([rhs.g_enc, rhs.h_enc]), MINUS_ONE)
+        neg = GHPairs(np.zeros(len(rhs), np.float32), None, pl)
+        neg.g_enc, neg.h_enc = negc[:len(rhs)], negc[len(rhs):]
+        neg.encrypted = True
+        return (self if self.encrypted else self._enc_side(pl)) + neg
+
+
+class HEServer:
+    """Server HE members (server.h:47-135)."""
+
+    def __init__(self, device=None):
+        self.paillier = Paillier(device)
+
+    def homo_init(self, keylength, seed=0):
+        """server.h:58-67 (NTL build: keygen(keylength))."""
+        self.paillier.keygen(keylength, seed)
+
+    def send_key(self, party):
+        """server.h:53-55: party.paillier = paillier (public part only)."""
+        party.paillier = self.paillier.public()
+
+    def encrypt_gh_pairs(self, raw, seed=0):
+        """server.h:113-135."""
+        return raw.homo_encrypt(self.paillier, seed=seed)
+
+    def decrypt_gh_pairs(self, encrypted):
+        """server.h:80-111."""
+        return encrypted.homo_decrypt(self.paillier)
+
+    def decrypt_gh(self, gh):
+        """server.h:69-78 (single pair, as a batch of one)."""
+        return gh.homo_decrypt(self.paillier)
+
+
+class HEParty:
+    """Party HE members (party.h:118-142, 181-185)."""
+
+    def __init__(self, paillier=None):
+        self.paillier = paillier
+
+    def encrypt_histogram(self, hist, seed=0):
+        """party.h:118-142."""
+        return hist.homo_encrypt(self.paillier, seed=seed)

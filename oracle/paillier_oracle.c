@@ -235,3 +235,18 @@ int po_num_threads(void) {
     return 1;
 #endif
 }
+
+/* Fixed-point codec exactly as the reference writes it (float_type = float):
+ *   GMP/GPU build  common.h:81      long g_ul = (long)(g * 1e6);
+ *   NTL build      common.h:127     NTL::to_ZZ((unsigned long)(g * 1e6))
+ *   decode         common.h:142     g = (float_type)g_dec / 1e6;
+ *                  paillier_gpu.cu:487 (float_type)g_ul / 1e6          */
+void po_encode_fixed_gmp(const float *g, long n, uint64_t *out) {
+    for (long i = 0; i < n; i++) { long v = (long)(g[i] * 1e6); out[i] = (uint64_t)v; }
+}
+void po_encode_fixed_ntl(const float *g, long n, uint64_t *out) {
+    for (long i = 0; i < n; i++) out[i] = (unsigned long)(g[i] * 1e6);
+}
+void po_decode_fixed(const uint64_t *m, long n, float *out) {
+    for (long i = 0; i < n; i++) { long v = (long)m[i]; out[i] = (float)v / 1e6; }
+}

@@ -1,0 +1,292 @@
+"""Parity of the HIP engine (libfthe.so, through the C ABI) with the oracle.
+
+* golden vectors of the reference's own Paillier_GMP (tests/golden/), bit-exact;
+* seeded random keys / messages / r against the C oracle, bit-exact;
+* full-size properties (encrypt -> decrypt round trips across chunk
+  boundaries, homomorphic sums, scalar-multiplication linearity).
+Integer work: every comparison is exact.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import GOLDEN_KEYS, golden_key, load_golden
+from fedtree_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from fedtree_amd.paillier import Device
+    return Device(0)
+
+
+@pytest.fixture(scope="module", params=GOLDEN_KEYS)
+def gold(request):
+    return load_golden(request.param)
+
+
+def _pl(dev, p, q):
+    from fedtree_amd.paillier import Paillier
+    return Paillier.from_primes(p, q, dev)
+
+
+def _cts(gold):
+    return pyoracle.ints_to_words([int(c["c"], 16) for c in gold["cases"]], 2 * gold["n_words"])
+
+
+def _public_supported(pl):
+    return pl.lib.fthe_kernel_limbs(2 * pl.keyLength) != 0
+
+
+# ---------------------------------------------------------------- golden vectors
+def test_golden_key(dev, gold):
+    p, q = golden_key(gold)
+    pl = _pl(dev, p, q)
+    assert pl.modulus == int(gold["n"], 16)
+    assert pl.lambda_ == int(gold["lambda"], 16)
+    assert pl.u == int(gold["mu"], 16)
+    assert pl.n_words == gold["n_words"]
+
+
+def test_golden_encrypt_crt(dev, gold):
+    p, q = golden_key(gold)
+    pl = _pl(dev, p, q)
+    ms = np.array([c["m"] for c in gold["cases"]], dtype=np.uint64)
+    r = np.tile(pyoracle.to_words(int(gold["shared_r"], 16), pl.n_words), (len(ms), 1))
+    assert np.array_equal(pl.encrypt_u64(ms, r=r), _cts(gold))
+
+
+def test_golden_encrypt_public(dev, gold):
+    p, q = golden_key(gold)
+    pl = _pl(dev, p, q)
+    ms = np.array([c["m"] for c in gold["cases"]], dtype=np.uint64)
+    r = np.tile(pyoracle.to_words(int(gold["shared_r"], 16), pl.n_words), (len(ms), 1))
+    if not _public_supported(pl):
+        with pytest.raises(_lib.FtheError) as e:
+            pl.encrypt_u64(ms, r=r, public=True)
+        assert e.value.status == _lib.FTHE_ERR_UNSUPPORTED
+        return
+    assert np.array_equal(pl.encrypt_u64(ms, r=r, public=True), _cts(gold))
+    # a public-key-only copy (Paillier::operator=) encrypts identically
+    pub = pl.public()
+    assert not pub.has_private
+    assert np.array_equal(pub.encrypt_u64(ms, r=r), _cts(gold))
+
+
+def test_golden_decrypt(dev, gold):
+    p, q = golden_key(gold)
+    pl = _pl(dev, p, q)
+    low, full = pl.decrypt_u64(_cts(gold), full=True)
+    assert [int(x) for x in low] == [c["m"] % 2**64 for c in gold["cases"]]
+    assert [pyoracle.from_words(f) for f in full] == [int(c["dec"], 16) for c in gold["cases"]]
+    # decrypts of the reference's homomorphic results
+    adds = pyoracle.ints_to_words([int(a["c"], 16) for a in gold["adds"]], 2 * pl.n_words)
+    _, full = pl.decrypt_u64(adds, full=True)
+    assert [pyoracle.from_words(f) for f in full] == [int(a["dec"], 16) for a in gold["adds"]]
+
+
+def test_golden_add_mul(dev, gold):
+    p, q = golden_key(gold)
+    pl = _pl(dev, p, q)
+    cts = _cts(gold)
+    a_idx = [a["i"] for a in gold["adds"]]
+    b_idx = [a["j"] for a in gold["adds"]]
+    if not _public_supported(pl):
+        with pytest.raises(_lib.FtheError):
+            pl.add_batch(cts[a_idx], cts[b_idx])
+        return
+    out = pl.add_batch(cts[a_idx], cts[b_idx])
+    assert [pyoracle.from_words(x) for x in out] == [int(a["c"], 16) for a in gold["adds"]]
+    for m in gold["muls"]:
+        got = pl.scalar_mul(cts[m["i"]][None], m["k"])
+        assert pyoracle.from_words(got[0]) == int(m["c"], 16), m["k"]
+
+
+def test_golden_hist_merge(dev, gold):
+    """k-party merge with the reference's encrypt(0)-first semantics."""
+    p, q = golden_key(gold)
+    pl = _pl(dev, p, q)
+    h = gold["hist"]
+    cw = 2 * pl.n_words
+    if not _public_supported(pl):
+        pytest.skip("mod n^2 products at 4096 bits: round-2 kernel")
+    stack = [np.tile(pyoracle.to_words(int(h["enc_zero"], 16), cw), (h["bins"], 1))]
+    for pi in range(h["parties"]):
+        stack.append(pyoracle.ints_to_words([int(x, 16) for x in h["ct"][pi]], cw))
+    out = pl.reduce_kway(np.stack(stack))
+    assert [pyoracle.from_words(x) for x in out] == [int(x, 16) for x in h["merged"]]
+    low = pl.decrypt_u64(out)
+    assert [int(x) for x in low] == [sum(h["m"][pi][b] for pi in range(h["parties"])) % 2**64
+                                     for b in range(h["bins"])]
+
+
+# ---------------------------------------------------------------- seeded random vs C oracle
+def _det_primes(coracle, nbits, seed):
+    rng = np.random.default_rng(seed)
+    hw = nbits // 64
+    return [coracle.next_prime(rng.integers(0, 2**32, hw, dtype=np.uint64).astype(np.uint32)) for _ in range(2)]
+
+
+@pytest.mark.parametrize("nbits", [512, 1024, 2048])
+def test_random_vs_c_oracle(dev, coracle, nbits):
+    pw, qw = _det_primes(coracle, nbits, 20261015 + nbits)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    ok = coracle.key(pw, qw)
+    n = pl.modulus
+    rng = np.random.default_rng(nbits + 1)
+    cnt = 777
+    m = rng.integers(0, 2**64, cnt, dtype=np.uint64)
+    m[:5] = [0, 1, 2**64 - 1, 2**63 - 1, 2**63]
+    rs = [int.from_bytes(rng.bytes(pl.n_words * 4), "little") % (n - 1) + 1 for _ in range(cnt)]
+    rs[0], rs[1] = 1, n - 1
+    r = pyoracle.ints_to_words(rs, pl.n_words)
+    want = ok.encrypt_batch(m, r)
+    assert np.array_equal(pl.encrypt_u64(m, r=r), want)
+    if _public_supported(pl):
+        assert np.array_equal(pl.encrypt_u64(m, r=r, public=True), want)
+    low, full = pl.decrypt_u64(want, full=True)
+    assert np.array_equal(low, m)
+    assert np.array_equal(full, ok.decrypt_batch(want))
+
+
+# ---------------------------------------------------------------- full-size properties
+def test_p2048_roundtrip_across_chunks(dev, coracle):
+    """Device CSPRNG r, count crossing the 262144-lane chunk boundary."""
+    pw, qw = _det_primes(coracle, 2048, 7)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    cnt = 262144 + 777
+    m = np.random.default_rng(3).integers(0, 2**64, cnt, dtype=np.uint64)
+    c = pl.encrypt_u64(m, seed=11)
+    assert np.array_equal(pl.decrypt_u64(c), m)
+    # ciphertexts are fresh (no shared r): no two equal
+    assert len({bytes(c[i]) for i in range(0, cnt, 997)}) == len(range(0, cnt, 997))
+    # independent check of a sample by the C oracle
+    ok = coracle.key(pw, qw)
+    idx = np.arange(0, cnt, cnt // 40)
+    dec = ok.decrypt_batch(c[idx])
+    assert [pyoracle.from_words(d) for d in dec] == [int(x) for x in m[idx]]
+    # same seed -> same ciphertexts; different seed -> different
+    c2 = pl.encrypt_u64(m[:1000], seed=11)
+    assert np.array_equal(c2, c[:1000])
+    c3 = pl.encrypt_u64(m[:1000], seed=12)
+    assert not np.array_equal(c3, c[:1000])
+
+
+def test_homomorphic_sum_and_scalar(dev, coracle):
+    pw, qw = _det_primes(coracle, 1024, 9)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    k, cnt = 8, 4099
+    m = np.random.default_rng(5).integers(0, 2**64, (k, cnt), dtype=np.uint64)
+    c = pl.encrypt_u64(m.reshape(-1), seed=1).reshape(k, cnt, -1)
+    s = pl.reduce_kway(c)
+    want = np.zeros(cnt, dtype=np.uint64)
+    for j in range(k):
+        want = want + m[j]            # wraps mod 2^64 == low 64 bits of the sum
+    assert np.array_equal(pl.decrypt_u64(s), want)
+    # subtraction through scalar mul by 2^64-1 (common.h:311-317)
+    neg = pl.scalar_mul(c[1], 2**64 - 1)
+    d = pl.add_batch(c[0], neg)
+    assert np.array_equal(pl.decrypt_u64(d), m[0] - m[1])
+    # linearity c^k -> k m
+    t = pl.scalar_mul(c[2], 12345)
+    assert np.array_equal(pl.decrypt_u64(t), m[2] * np.uint64(12345))
+    # alias safety: out == a through the device API
+    import torch
+    ta = torch.from_numpy(c[0].copy()).cuda()
+    tb = torch.from_numpy(c[1].copy()).cuda()
+    pl.add_dev(ta, tb, ta)
+    pl.dev.sync()
+    assert np.array_equal(pl.decrypt_u64(ta.cpu().numpy()), m[0] + m[1])
+
+
+@pytest.mark.parametrize("cnt", [0, 1, 255, 257])
+def test_edge_counts(dev, coracle, cnt):
+    pw, qw = _det_primes(coracle, 1024, 13)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    m = np.arange(cnt, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    c = pl.encrypt_u64(m, seed=3)
+    assert c.shape == (cnt, 2 * pl.n_words)
+    assert np.array_equal(pl.decrypt_u64(c), m)
+    assert pl.add_batch(c, c).shape == c.shape
+
+
+def test_device_codec_and_dev_api(dev, coracle):
+    import torch
+    from fedtree_amd.paillier import decode_fixed, encode_fixed
+    g = load_golden("codec.json")
+    f = np.array(g["floats_f32_bits"], dtype=np.uint32).view(np.float32)
+    rng = np.random.default_rng(0)
+    f = np.concatenate([f, rng.normal(size=5000).astype(np.float32), rng.uniform(-1, 1, 5000).astype(np.float32)])
+    lib = dev.lib
+    tf = torch.from_numpy(f).cuda()
+    tm = torch.zeros(len(f), dtype=torch.int64, device="cuda")
+    _lib.check(lib.fthe_encode_fixed_dev(dev.ctx, ctypes.c_void_p(tf.data_ptr()), len(f),
+                                         ctypes.c_void_p(tm.data_ptr())))
+    dev.sync()
+    m = tm.cpu().numpy().view(np.uint64)
+    assert np.array_equal(m, encode_fixed(f))
+    din = np.array(g["decode_in"], dtype=np.uint64)
+    allin = np.concatenate([din, m])
+    tin = torch.from_numpy(allin.view(np.int64)).cuda()
+    tout = torch.zeros(len(allin), dtype=torch.float32, device="cuda")
+    _lib.check(lib.fthe_decode_fixed_dev(dev.ctx, ctypes.c_void_p(tin.data_ptr()), len(allin),
+                                         ctypes.c_void_p(tout.data_ptr())))
+    dev.sync()
+    assert np.array_equal(tout.cpu().numpy().view(np.uint32), decode_fixed(allin).view(np.uint32))
+    # device-resident encrypt/decrypt through torch buffers
+    pw, qw = _det_primes(coracle, 2048, 21)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    tc = torch.zeros((len(m), 2 * pl.n_words), dtype=torch.int32, device="cuda")
+    pl.encrypt_u64_dev(tm, tc, seed=5)
+    tl = torch.zeros(len(m), dtype=torch.int64, device="cuda")
+    pl.decrypt_u64_dev(tc, tl)
+    dev.sync()
+    assert np.array_equal(tl.cpu().numpy().view(np.uint64), m)
+    host = pl.encrypt_u64(m, seed=5)
+    assert np.array_equal(tc.cpu().numpy().view(np.uint32), host)
+
+
+def test_keygen(dev):
+    from fedtree_amd.paillier import Paillier
+    a = Paillier(dev).keygen(2048, seed=42)
+    b = Paillier(dev).keygen(2048, seed=42)
+    c = Paillier(dev).keygen(2048, seed=43)
+    assert a.keyLength == 2048 and a.modulus == b.modulus != c.modulus
+    assert a.p * a.q == a.modulus
+    m = np.arange(1000, dtype=np.uint64) * np.uint64(2**40 + 7)
+    assert np.array_equal(a.decrypt_u64(a.encrypt_u64(m)), m)
+    # reference single-value signatures
+    x = a.encrypt(123456789)
+    assert a.decrypt(x) == 123456789
+    assert 0 < x < a.modulus ** 2
+
+
+def test_ghpair_server_party_flow(dev):
+    """Server/Party HE flow on the reference's histogram KAT values
+    (test_tree_builder.cpp:52-91): decrypt(sum of encrypted) == plaintext sum
+    within the 1e-6 fixed-point quantum."""
+    from fedtree_amd.paillier import GHPairs, HEParty, HEServer
+    srv = HEServer(dev)
+    srv.homo_init(1024, seed=1)
+    party = HEParty()
+    srv.send_key(party)
+    assert not party.paillier.has_private
+    g = np.array([0.4, 1.2, 0.1, 0.8, 0.7], np.float32)
+    h = np.array([0.6, 1.4, 0.2, 1.0, 0.8], np.float32)
+    a = srv.encrypt_gh_pairs(GHPairs(g, h))
+    assert a.encrypted and not a.g.any()
+    b = party.encrypt_histogram(GHPairs(g * 2, h * 2))
+    s = a + b                                   # homomorphic
+    z = GHPairs(np.zeros(5, np.float32)) + a    # unencrypted lhs: fresh encrypt(0) first (Q10)
+    d = s - a                                   # subtraction via x^(2^64-1)
+    srv.decrypt_gh_pairs(s)
+    srv.decrypt_gh_pairs(z)
+    srv.decrypt_gh_pairs(d)
+    np.testing.assert_allclose(s.g, 3 * g, atol=3e-6)
+    np.testing.assert_allclose(s.h, 3 * h, atol=3e-6)
+    np.testing.assert_allclose(z.g, g, atol=2e-6)
+    np.testing.assert_allclose(d.g, 2 * g, atol=3e-6)
