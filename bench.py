@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""bench.py -- Paillier-2048 encrypts/s, device-resident (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[4], per-GPU share; configs[2]'s encrypt half):
+one step = encrypt 10M synthetic logistic gradient pairs (20M ciphertexts) that
+already sit in HBM as float32 (g, h): device fixed-point codec + a fresh
+uniform r per ciphertext from the device ChaCha20 stream + c = g^m r^n mod n^2
+(CRT over p^2, q^2: the encrypting server holds the key, server.h:113-135),
+output 20M x 512 B ciphertexts left in HBM.
+
+Multi-GPU: one process per GPU (torchrun), each rank encrypts its own 10M
+pairs -- independent units, no collective on the data path (weak scaling);
+the barrier and the max-over-ranks elapsed time use torch.distributed.
+
+Printed by rank 0: one JSON line with the driver's contract fields plus
+`roofline` (montprog kernel: algorithmic integer MACs per second vs the
+half-rate v_mad_u64_u32 peak, per-launch HIP events on the engine stream) and
+`cpu_baseline` (the reference's own Paillier_GMP::encrypt, OpenMP over a
+bounded sample on this host's cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Paillier-2048 encrypts/s device-resident; ciphertext adds/s; 1/2/4/8 GPU"
+SEED = 20261015
+KEY_BITS = 2048
+# Roofline (MI355X_MICROARCH.md: 256 CUs, 2.4 GHz, SIMD32).  v_mad_u64_u32 is
+# half-rate on gfx950 (measured, profiles/r01_microbench_valu.txt): 64 lanes per
+# 4 cycles per SIMD -> 16 MACs/clk/SIMD.
+PEAK_MAC_S = 256 * 4 * 16 * 2.4e9          # 3.93e13 32x32->64 MACs/s
+MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves/CU
+# W(s) = 2 s^2 + s MACs per Montgomery product on s u32 limbs,
+# 1.2 e products per e-bit exponent; CRT encrypt = 2 modexps of 2048-bit exponent
+# over 2048-bit moduli (s = 64).
+W64 = 2 * 64 * 64 + 64
+ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pairs", type=int, default=10_000_000, help="gradient pairs per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=32768, help="ciphertexts in the CPU baseline sample (about 10-20 s of 16 host threads)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(sample, threads):
+    """The reference's Paillier_GMP::encrypt (full PowerMod(g,m,n^2)*PowerMod(r,n,n^2),
+    paillier_gmp.cpp:37-73), OpenMP over elements as server.h:129-133.  Falls back to
+    our C/GMP port of paillier.cpp if the reference build is absent."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from fedtree_amd.synth import logistic_gradients
+    from fedtree_amd.paillier import encode_fixed
+    g, h = logistic_gradients(sample // 2, SEED)
+    m = np.ascontiguousarray(np.concatenate([encode_fixed(g), encode_fixed(h)]))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    try:
+        ref = pyoracle.RefGMP()
+        hk = ref.lib.ref_keygen(2 * KEY_BITS)          # GMP keyGen(L) -> L/2-bit n
+        nw = ref.lib.ref_n_words(hk)
+        out = np.zeros((len(m), 2 * nw), dtype=np.uint32)
+        t0 = time.perf_counter()
+        ref.lib.ref_encrypt_batch(hk, nw, m.ctypes.data, len(m), out.ctypes.data, threads)
+        dt = time.perf_counter() - t0
+        ref.lib.ref_free(hk)
+        kind, what = "reference", "FedTree Paillier_GMP::encrypt compiled from the reference sources"
+    except OSError:
+        o = pyoracle.COracle()
+        rng = np.random.default_rng(SEED)
+        hw = KEY_BITS // 64
+        pw = o.next_prime(rng.integers(0, 2**32, hw, dtype=np.uint64).astype(np.uint32))
+        qw = o.next_prime(rng.integers(0, 2**32, hw, dtype=np.uint64).astype(np.uint32))
+        key = o.key(pw, qw)
+        r = rng.integers(0, 2**32, (len(m), 2 * hw), dtype=np.uint64).astype(np.uint32)
+        r[:, -1] &= 0x3FFFFFFF
+        t0 = time.perf_counter()
+        key.encrypt_batch(m, r, threads)
+        dt = time.perf_counter() - t0
+        kind, what = "port", "C/GMP restatement of paillier.cpp:122-139 (oracle/paillier_oracle.c)"
+    return {"value": len(m) / dt, "unit": "encrypts/s", "cores": threads, "kind": kind,
+            "sample": f"{len(m)} Paillier-2048 encrypts of synthetic gradients ({what}, full PowerMod, "
+                      f"no CRT, OpenMP {threads} threads), {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from fedtree_amd.paillier import Device, Paillier
+    from fedtree_amd.synth import logistic_gradients
+    from fedtree_amd import _lib
+    import ctypes
+
+    dev = Device(local)
+    lib = dev.lib
+    pl = Paillier(dev).keygen(KEY_BITS, seed=SEED)            # the server's key (same on every rank)
+    P = a.pairs
+    g, h = logistic_gradients(P, SEED + rank)
+    gh = torch.from_numpy(np.concatenate([g, h])).to(f"cuda:{local}")    # resident before timing
+    m = torch.empty(2 * P, dtype=torch.int64, device=f"cuda:{local}")
+    c = torch.empty((2 * P, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    def step(i):
+        _lib.check(lib.fthe_encode_fixed_dev(dev.ctx, ctypes.c_void_p(gh.data_ptr()), 2 * P,
+                                             ctypes.c_void_p(m.data_ptr())), "encode")
+        pl.encrypt_u64_dev(m, c, seed=SEED * 1000 + rank * 100 + i + 1)
+
+    for i in range(a.warmup):
+        step(i)
+    dev.sync()
+    lib.fthe_prof_enable(dev.ctx, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dev.sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    dev.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kms, launches, lane_mm, lanes = (ctypes.c_double() for _ in range(4))
+    _lib.check(lib.fthe_prof_read(dev.ctx, ctypes.byref(kms), ctypes.byref(launches), ctypes.byref(lane_mm),
+                                  ctypes.byref(lanes)))
+    lib.fthe_prof_enable(dev.ctx, 0)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    enc_total = world * 2 * P * a.steps
+    value = enc_total / elapsed
+
+    # -- roofline of the dominant kernel (montprog, per-launch HIP events, this rank)
+    enc_rank = 2 * P * a.steps
+    alg_macs = enc_rank * ALG_MACS_PER_CRT_ENC
+    k_s = kms.value * 1e-3
+    S = lib.fthe_kernel_limbs(KEY_BITS)
+    achieved = alg_macs / k_s / 1e12
+    issued = lane_mm.value * 2 * S * S / k_s / 1e12
+    roof = {"bound": "valu", "kernel": "fthe_montprog_s74", "achieved": round(achieved, 3),
+            "peak": round(PEAK_MAC_S / 1e12, 3), "unit": "TMAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_S, 4),
+            "traffic": None,
+            "launches": int(launches.value), "avg_launch_ms": round(kms.value / max(1, launches.value), 3),
+            "alg_macs_per_encrypt": ALG_MACS_PER_CRT_ENC,
+            "issued_v_mad_u64_u32_tmac_s": round(issued, 3),
+            "issued_frac_of_measured_mad_peak": round(issued * 1e12 / MEASURED_MAD_S, 4),
+            "kernel_share_of_step": round(k_s / elapsed, 4)}
+    prof_hbm = os.path.join(ROOT, "profiles", "r01_montprog_pmc.json")
+    if os.path.exists(prof_hbm):
+        try:
+            roof["traffic"] = json.load(open(prof_hbm)).get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    secondary = {}
+    if rank == 0 and not a.no_secondary:
+        # CRT decrypt of 1M ciphertexts (config 3's decrypt half), device-resident
+        nd = min(2 * P, 1 << 20)
+        low = torch.empty(nd, dtype=torch.int64, device=f"cuda:{local}")
+        pl.decrypt_u64_dev(c[:nd], low)
+        dev.sync()
+        secondary["crt_decrypt_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        ok = torch.equal(low, m[:nd])
+        secondary["decrypt_roundtrip_ok"] = bool(ok)
+        # ciphertext adds: P-1024 (n^2 = 2048-bit) on the same kernel; P-2048 adds
+        # need the 4096-bit modulus kernel (not built in round 1)
+        p1 = Paillier(dev).keygen(1024, seed=SEED)
+        na = 1 << 20
+        x = torch.randint(0, 2**31, (na, 2 * p1.n_words), dtype=torch.int32, device=f"cuda:{local}")
+        x[:, -1] = 0
+        y = x.flip(0).contiguous()
+        o = torch.empty_like(x)
+        p1.add_dev(x, y, o)
+        p1.add_dev(x, y, o)
+        dev.sync()
+        secondary["p1024_add_per_s"] = round(na / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        secondary["p2048_add_per_s"] = None
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(a.cpu_sample, a.cpu_threads)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "encrypts/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic logistic gradients (splitmix64 seed 20261015+rank), fresh device-CSPRNG r per ciphertext",
+            "config": {"workload": "Paillier-2048 encrypt of gradient pairs, device-resident, CRT (key holder)",
+                       "pairs_per_gpu": P, "ciphertexts_per_gpu_per_step": 2 * P, "key_bits": KEY_BITS,
+                       "parallelism": f"independent shards x{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "secondary": secondary,
+        }
+        if cpu:
+            line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -100,6 +100,12 @@ struct fthe_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_mm = 0;
     bool timed = false;
+    // optional per-launch timing of the montprog kernel (bench roofline)
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
+    size_t prof_used = 0;
+    double prof_lane_mm = 0;      // sum over launches of live lanes x products
+    double prof_launch_lanes = 0; // sum over launches of live lanes
 };
 
 // Device copy of one Montgomery modulus.
@@ -212,6 +218,7 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) hipModuleUnload(c->mod[i]);
+    for (auto &e : c->prof_ev) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -235,6 +242,31 @@ extern "C" double fthe_last_kernel_ms(fthe_ctx *c) {
     return ms;
 }
 extern "C" double fthe_last_montmuls(fthe_ctx *c) { return c ? c->last_mm : 0.0; }
+
+extern "C" int fthe_prof_enable(fthe_ctx *c, int on) {
+    if (!c) return FTHE_ERR_ARG;
+    c->prof = on != 0;
+    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0;
+    return FTHE_OK;
+}
+
+extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, double *lane_montmuls, double *lanes) {
+    if (!c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipStreamSynchronize(c->stream));
+    double tot = 0;
+    for (size_t i = 0; i < c->prof_used; i++) {
+        float ms = 0;
+        HIPOK(hipEventElapsedTime(&ms, c->prof_ev[i].first, c->prof_ev[i].second));
+        tot += ms;
+    }
+    if (kernel_ms) *kernel_ms = tot;
+    if (launches) *launches = (double)c->prof_used;
+    if (lane_montmuls) *lane_montmuls = c->prof_lane_mm;
+    if (lanes) *lanes = c->prof_launch_lanes;
+    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0;
+    return FTHE_OK;
+}
 
 // ---------------------------------------------------------------------------
 // Key set-up
@@ -482,19 +514,42 @@ extern "C" int fthe_key_export(const fthe_key *k, uint32_t *n, uint32_t *lambda,
 // Launch helpers
 namespace {
 
+// Launch the montprog kernel, bracketed by profiling events when enabled.
+int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *modctx, double lane_mm, size_t live) {
+    struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
+        c->slots.p, prog, modctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4)};
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    int vi = variant_index(S);
+    if (vi < 0) return FTHE_ERR_UNSUPPORTED;
+    std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
+    if (c->prof) {
+        if (c->prof_used == c->prof_ev.size()) {
+            std::pair<hipEvent_t, hipEvent_t> e;
+            HIPOK(hipEventCreate(&e.first));
+            HIPOK(hipEventCreate(&e.second));
+            c->prof_ev.push_back(e);
+        }
+        ev = &c->prof_ev[c->prof_used++];
+        HIPOK(hipEventRecord(ev->first, c->stream));
+    }
+    if (hipModuleLaunchKernel(c->fn[vi], L / 256, 1, 1, 256, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
+        return FTHE_ERR_HIP;
+    if (ev) {
+        HIPOK(hipEventRecord(ev->second, c->stream));
+        c->prof_lane_mm += lane_mm * (double)live;
+        c->prof_launch_lanes += (double)live;
+    }
+    return FTHE_OK;
+}
+
 struct Launch {
     fthe_ctx *c; const fthe_key *k; int L; int S; double mm = 0; size_t live = 0;
     uint32_t *slot(int s) const { return (uint32_t *)c->slots.p + (size_t)s * S * L; }
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
     int prog(const fthe_key::PH &ph, const DevMod &mod) {
-        struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
-            c->slots.p, k->prog(ph), mod.d_ctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4)};
-        size_t sz = sizeof(args);
-        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-        int vi = variant_index(S);
-        if (vi < 0) return FTHE_ERR_UNSUPPORTED;
-        if (hipModuleLaunchKernel(c->fn[vi], L / 256, 1, 1, 256, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
-            return FTHE_ERR_HIP;
+        int rc = launch_montprog(c, S, L, k->prog(ph), mod.d_ctx, ph.mm, live);
+        if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;
     }
@@ -668,14 +723,8 @@ static int upload_dyn_prog(fthe_ctx *c, const Prog &p, fthe_key::PH &ph, DevBuf 
 namespace {
 // Launch with an explicit (dynamic) program pointer.
 int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod) {
-    struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
-        Lc.c->slots.p, prog, mod.d_ctx, (uint32_t)Lc.L * 4, (uint32_t)((size_t)Lc.S * Lc.L * 4)};
-    size_t sz = sizeof(args);
-    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    int vi = variant_index(Lc.S);
-    if (vi < 0) return FTHE_ERR_UNSUPPORTED;
-    if (hipModuleLaunchKernel(Lc.c->fn[vi], Lc.L / 256, 1, 1, 256, 1, 1, 0, Lc.c->stream, nullptr, cfg) != hipSuccess)
-        return FTHE_ERR_HIP;
+    int rc = launch_montprog(Lc.c, Lc.S, Lc.L, prog, mod.d_ctx, mm, Lc.live);
+    if (rc) return rc;
     Lc.mm += mm * (double)Lc.live;
     return FTHE_OK;
 }

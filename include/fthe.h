@@ -142,6 +142,16 @@ int fthe_decode_fixed_dev(fthe_ctx *ctx, const uint64_t *m, size_t count, float 
 double fthe_last_kernel_ms(fthe_ctx *ctx);
 /* Montgomery products executed by the last call (for roofline accounting). */
 double fthe_last_montmuls(fthe_ctx *ctx);
+/* Per-launch timing of the Montgomery program kernel (HIP events on the
+ * context stream, bracketing each launch).  fthe_prof_read drains the stream,
+ * returns totals since the last read/enable and resets them:
+ *   kernel_ms      summed launch durations
+ *   launches       number of launches
+ *   lane_montmuls  sum over launches of (live lanes x Montgomery products)
+ *   lanes          sum over launches of live lanes */
+int    fthe_prof_enable(fthe_ctx *ctx, int on);
+int    fthe_prof_read(fthe_ctx *ctx, double *kernel_ms, double *launches,
+                      double *lane_montmuls, double *lanes);
 /* limb count S of the radix-2^28 kernel used for a modulus of `bits` bits
  * (0 if unsupported). */
 int    fthe_kernel_limbs(int bits);

@@ -199,4 +199,6 @@ class RefGMP:
         lib.ref_add_aliased.argtypes = [P, ctypes.c_int, P, P]
         lib.ref_mul.argtypes = [P, ctypes.c_int, P, ctypes.c_uint64, P]
         lib.ref_shared_r.argtypes = [P, ctypes.c_int, P]
+        lib.ref_encrypt_batch.argtypes = [P, ctypes.c_int, P, ctypes.c_long, P, ctypes.c_int]
+        lib.ref_num_threads.restype = ctypes.c_int
         self.lib = lib

@@ -7,6 +7,9 @@
 #include "FedTree/Encryption/paillier_gmp.h"   // /root/reference/include
 #include <cstring>
 #include <cstdint>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 static void exp_words(uint32_t *w, int nw, const mpz_t x) {
     size_t cnt = 0;
@@ -48,6 +51,32 @@ void ref_encrypt(void *h, int nw, uint64_t m, uint32_t *out) {
     exp_words(out, 2 * nw, c);
     mpz_clear(mz); mpz_clear(c);
 }
+// Batch form for the CPU baseline: OpenMP over elements exactly as
+// Server::encrypt_gh_pairs does (server.h:129-133), each element one call of
+// the reference's Paillier_GMP::encrypt (full PowerMod formula).
+void ref_encrypt_batch(void *h, int nw, const uint64_t *m, long count, uint32_t *out, int threads) {
+    Paillier_GMP *k = (Paillier_GMP *)h;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    #pragma omp parallel for schedule(dynamic, 4)
+    for (long i = 0; i < count; i++) {
+        mpz_t mz, c; mpz_init(mz);
+        uint64_t v = m[i];
+        mpz_import(mz, 1, -1, 8, 0, 0, &v);
+        k->encrypt(c, mz);
+        exp_words(out + (size_t)i * 2 * nw, 2 * nw, c);
+        mpz_clear(mz); mpz_clear(c);
+    }
+}
+int ref_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
 // Paillier_GMP::decrypt (paillier_gmp.cpp:75-85); out: nw words.
 void ref_decrypt(void *h, int nw, const uint32_t *c, uint32_t *out) {
     Paillier_GMP *k = (Paillier_GMP *)h;
