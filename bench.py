@@ -144,9 +144,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    kms, launches, lane_mm, lanes = (ctypes.c_double() for _ in range(4))
+    kms, launches, lane_mm, lanes, ems, elaunch = (ctypes.c_double() for _ in range(6))
     _lib.check(lib.fthe_prof_read(dev.ctx, ctypes.byref(kms), ctypes.byref(launches), ctypes.byref(lane_mm),
-                                  ctypes.byref(lanes)))
+                                  ctypes.byref(lanes), ctypes.byref(ems), ctypes.byref(elaunch)))
     lib.fthe_prof_enable(dev.ctx, 0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -166,6 +166,8 @@ def main():
             "peak": round(PEAK_MAC_S / 1e12, 3), "unit": "TMAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_S, 4),
             "traffic": None,
             "launches": int(launches.value), "avg_launch_ms": round(kms.value / max(1, launches.value), 3),
+            "expo_launches": int(elaunch.value),
+            "avg_expo_launch_ms": round(ems.value / max(1, elaunch.value), 3),
             "alg_macs_per_encrypt": ALG_MACS_PER_CRT_ENC,
             "issued_v_mad_u64_u32_tmac_s": round(issued, 3),
             "issued_frac_of_measured_mad_peak": round(issued * 1e12 / MEASURED_MAD_S, 4),
@@ -200,6 +202,15 @@ def main():
         dev.sync()
         secondary["p1024_add_per_s"] = round(na / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
         secondary["p2048_add_per_s"] = None
+        # end to end, host-resident in/out (pageable H2D of m, D2H of 512-B ciphertexts)
+        ne = min(2 * P, 1 << 20)
+        mh = m[:ne].cpu().numpy().view(np.uint64).copy()
+        pl.encrypt_u64(mh[:4096], seed=3)
+        t0 = time.perf_counter()
+        ch = pl.encrypt_u64(mh, seed=3)
+        dt = time.perf_counter() - t0
+        secondary["e2e_host_encrypt_per_s"] = round(ne / dt)
+        secondary["e2e_note"] = f"{ne} ciphertexts host->device->host incl. pageable copies ({ch.nbytes / 1e6:.0f} MB out)"
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_sample, a.cpu_threads)

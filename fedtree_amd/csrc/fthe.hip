@@ -103,6 +103,7 @@ struct fthe_ctx {
     // optional per-launch timing of the montprog kernel (bench roofline)
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
+    std::vector<double> prof_mm;  // products per lane of each recorded launch
     size_t prof_used = 0;
     double prof_lane_mm = 0;      // sum over launches of live lanes x products
     double prof_launch_lanes = 0; // sum over launches of live lanes
@@ -250,17 +251,21 @@ extern "C" int fthe_prof_enable(fthe_ctx *c, int on) {
     return FTHE_OK;
 }
 
-extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, double *lane_montmuls, double *lanes) {
+extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, double *lane_montmuls, double *lanes,
+                              double *expo_ms, double *expo_launches) {
     if (!c) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipStreamSynchronize(c->stream));
-    double tot = 0;
+    double tot = 0, etot = 0, en = 0;
     for (size_t i = 0; i < c->prof_used; i++) {
         float ms = 0;
         HIPOK(hipEventElapsedTime(&ms, c->prof_ev[i].first, c->prof_ev[i].second));
         tot += ms;
+        if (c->prof_mm[i] >= 64) { etot += ms; en += 1; }   // exponentiation launches
     }
     if (kernel_ms) *kernel_ms = tot;
+    if (expo_ms) *expo_ms = etot;
+    if (expo_launches) *expo_launches = en;
     if (launches) *launches = (double)c->prof_used;
     if (lane_montmuls) *lane_montmuls = c->prof_lane_mm;
     if (lanes) *lanes = c->prof_launch_lanes;
@@ -530,6 +535,8 @@ int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *mod
             HIPOK(hipEventCreate(&e.second));
             c->prof_ev.push_back(e);
         }
+        if (c->prof_mm.size() < c->prof_ev.size()) c->prof_mm.resize(c->prof_ev.size());
+        c->prof_mm[c->prof_used] = lane_mm;
         ev = &c->prof_ev[c->prof_used++];
         HIPOK(hipEventRecord(ev->first, c->stream));
     }

@@ -148,10 +148,13 @@ double fthe_last_montmuls(fthe_ctx *ctx);
  *   kernel_ms      summed launch durations
  *   launches       number of launches
  *   lane_montmuls  sum over launches of (live lanes x Montgomery products)
- *   lanes          sum over launches of live lanes */
+ *   lanes          sum over launches of live lanes
+ *   expo_ms/_launches  the same restricted to exponentiation launches
+ *                  (programs of >= 64 products per lane) */
 int    fthe_prof_enable(fthe_ctx *ctx, int on);
 int    fthe_prof_read(fthe_ctx *ctx, double *kernel_ms, double *launches,
-                      double *lane_montmuls, double *lanes);
+                      double *lane_montmuls, double *lanes,
+                      double *expo_ms, double *expo_launches);
 /* limb count S of the radix-2^28 kernel used for a modulus of `bits` bits
  * (0 if unsupported). */
 int    fthe_kernel_limbs(int bits);

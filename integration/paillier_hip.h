@@ -1,0 +1,183 @@
+// paillier_hip.h -- drop-in HE engine class for a FedTree build with USE_HIP.
+//
+// Copy to include/FedTree/Encryption/paillier_hip.h in a FedTree tree and select
+// it where the reference selects Paillier_GPU (server.h:47-51, party.h:181-185,
+// common.h:43-61 use USE_CUDA; add the same branches for USE_HIP).  The class has
+// the member functions and fields of Paillier_GPU (paillier_gpu.h:28-94), so the
+// callers -- Server::{homo_init, encrypt_gh_pairs, decrypt_gh_pairs, decrypt_gh}
+// (server.h:58-135), Party::encrypt_histogram (party.h:118-142) and GHPair's
+// operators through paillier_cpu (common.h:150-337) -- compile unchanged.
+//
+// Everything is computed by libfthe.so through the C ABI (include/fthe.h).
+// Differences from Paillier_GPU, all deliberate:
+//   * a fresh uniform r per ciphertext (device ChaCha20) instead of one shared,
+//     unseeded-MT r per batch (paillier_gpu.cu:262-272);
+//   * any key size up to Paillier-2048 with CRT on the key holder, instead of a
+//     fixed 512-bit n (BITS=1024, paillier_gpu.h:13);
+//   * add() is alias-safe; errors throw std::runtime_error instead of
+//     exit(1) / CHECK aborts.
+#pragma once
+#include <gmp.h>
+#include <cmath>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fthe.h"
+#include "FedTree/syncarray.h"
+#include "FedTree/common.h"
+#include "FedTree/Encryption/paillier_gmp.h"
+
+namespace fthe_shim {
+inline void check(int st, const char *what) {
+    if (st != FTHE_OK) throw std::runtime_error(std::string(what) + ": " + fthe_strerror(st));
+}
+// One engine context per host thread (the boundary is entered from OpenMP
+// regions, FLtrainer.cpp:275-306); device from FTHE_DEVICE (default 0).
+inline fthe_ctx *thread_ctx() {
+    static thread_local fthe_ctx *c = nullptr;
+    if (!c) {
+        const char *d = std::getenv("FTHE_DEVICE");
+        check(fthe_ctx_create(d ? std::atoi(d) : 0, &c), "fthe_ctx_create");
+    }
+    return c;
+}
+// mpz <-> little-endian u32 words (paillier_gpu.cu:7,18 order)
+inline void to_words(const mpz_t x, uint32_t *w, int nw) {
+    size_t cnt = 0;
+    for (int i = 0; i < nw; i++) w[i] = 0;
+    if (mpz_sizeinbase(x, 2) > (size_t)nw * 32) throw std::runtime_error("operand does not fit");
+    mpz_export(w, &cnt, -1, 4, 0, 0, x);
+}
+inline void from_words(mpz_t x, const uint32_t *w, int nw) { mpz_import(x, (size_t)nw, -1, 4, 0, 0, w); }
+// codec of common.h:81-86 and paillier_gpu.cu:487
+inline uint64_t encode(float_type v) { long l = (long)(v * 1e6); return (uint64_t)l; }
+inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 1e6; }
+}  // namespace fthe_shim
+
+class Paillier_HIP {
+public:
+    Paillier_HIP() : key_length(2048) {}
+    Paillier_HIP(const Paillier_HIP &o) : key_length(o.key_length) { copy_public(o); }
+    ~Paillier_HIP() { if (key_) fthe_key_destroy(key_); }
+
+    // Paillier_GPU::operator= (paillier_gpu.h:32-37): public part, re-uploaded.
+    Paillier_HIP &operator=(const Paillier_HIP &source) {
+        if (this != &source) { key_length = source.key_length; copy_public(source); }
+        return *this;
+    }
+
+    // Paillier_GPU::keygen (paillier_gpu.cu:119-121); key_length = bits of n.
+    void keygen() { keygen((int)key_length); }
+    void keygen(int keyLength) {
+        key_length = (uint32_t)keyLength;
+        if (key_) fthe_key_destroy(key_);
+        key_ = nullptr;
+        fthe_shim::check(fthe_key_generate(fthe_shim::thread_ctx(), keyLength, 0, &key_), "keygen");
+        export_cpu();
+    }
+    void parameters_cpu_to_gpu() {      // keys live on the device from creation
+        if (!key_ && mpz_sgn(paillier_cpu.n)) {
+            std::vector<uint32_t> w(words(paillier_cpu.n));
+            fthe_shim::to_words(paillier_cpu.n, w.data(), (int)w.size());
+            fthe_shim::check(fthe_key_from_n(fthe_shim::thread_ctx(), w.data(), (int)w.size(), &key_), "key_from_n");
+        }
+    }
+
+    // Paillier_GPU::encrypt(SyncArray<GHPair>&) (paillier_gpu.cu:211-313)
+    void encrypt(SyncArray<GHPair> &message) {
+        auto *d = message.host_data();
+        size_t n = message.size();
+        int nw = fthe_key_n_words(key_), cw = 2 * nw;
+        std::vector<uint64_t> m(2 * n);
+        for (size_t i = 0; i < n; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
+        std::vector<uint32_t> c(2 * n * (size_t)cw);
+        fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
+                                          FTHE_ENC_DEFAULT), "encrypt");
+        for (size_t i = 0; i < n; i++) {
+            fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
+            fthe_shim::from_words(d[i].h_enc, &c[(n + i) * cw], cw);
+        }
+    }
+
+    // Paillier_GPU::decrypt(SyncArray<GHPair>&) (paillier_gpu.cu:448-494)
+    void decrypt(SyncArray<GHPair> &message) {
+        auto *d = message.host_data();
+        size_t n = message.size();
+        int nw = fthe_key_n_words(key_), cw = 2 * nw;
+        std::vector<uint32_t> c(2 * n * (size_t)cw, 0);
+        for (size_t i = 0; i < n; i++) {
+            if (!d[i].encrypted) continue;
+            fthe_shim::to_words(d[i].g_enc, &c[i * cw], cw);
+            fthe_shim::to_words(d[i].h_enc, &c[(n + i) * cw], cw);
+        }
+        std::vector<uint64_t> m(2 * n);
+        fthe_shim::check(fthe_decrypt(key_, fthe_shim::thread_ctx(), c.data(), 2 * n, m.data(), nullptr), "decrypt");
+        for (size_t i = 0; i < n; i++)
+            if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }
+    }
+
+    // Paillier_GPU::decrypt(GHPair&) (paillier_gpu.cu:497-542)
+    void decrypt(GHPair &message) {
+        if (!message.encrypted) return;
+        int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> c(2 * (size_t)cw);
+        fthe_shim::to_words(message.g_enc, &c[0], cw);
+        fthe_shim::to_words(message.h_enc, &c[cw], cw);
+        uint64_t m[2];
+        fthe_shim::check(fthe_decrypt(key_, fthe_shim::thread_ctx(), c.data(), 2, m, nullptr), "decrypt");
+        message.g = fthe_shim::decode(m[0]);
+        message.h = fthe_shim::decode(m[1]);
+    }
+
+    // Paillier_GPU::add / mul (paillier_gpu.cu:58-68): single values.  Batch
+    // callers should use fthe_add / fthe_reduce_kway directly.
+    void add(mpz_t &result, mpz_t &x, mpz_t &y) {
+        int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> a(cw), b(cw), o(cw);
+        fthe_shim::to_words(x, a.data(), cw);
+        fthe_shim::to_words(y, b.data(), cw);
+        fthe_shim::check(fthe_add(key_, fthe_shim::thread_ctx(), a.data(), b.data(), 1, o.data()), "add");
+        fthe_shim::from_words(result, o.data(), cw);
+    }
+    void mul(mpz_t result, mpz_t &x, mpz_t &y) {
+        int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> a(cw), o(cw);
+        fthe_shim::to_words(x, a.data(), cw);
+        uint64_t k = 0;
+        if (mpz_sizeinbase(y, 2) > 64) throw std::runtime_error("mul: exponent > 64 bits");
+        mpz_export(&k, nullptr, -1, 8, 0, 0, y);
+        fthe_shim::check(fthe_scalar_mul_u64(key_, fthe_shim::thread_ctx(), a.data(), k, 1, o.data()), "mul");
+        fthe_shim::from_words(result, o.data(), cw);
+    }
+
+    uint32_t key_length;
+    Paillier_GMP paillier_cpu;          // host copy the GHPair operators use (common.h:72)
+    fthe_key *key() const { return key_; }
+
+private:
+    fthe_key *key_ = nullptr;
+    static size_t words(const mpz_t x) { return (mpz_sizeinbase(x, 2) + 31) / 32; }
+    void copy_public(const Paillier_HIP &o) {
+        if (key_) fthe_key_destroy(key_);
+        key_ = nullptr;
+        paillier_cpu = o.paillier_cpu;                                    // public part only
+        parameters_cpu_to_gpu();
+    }
+    void export_cpu() {
+        int nw = fthe_key_n_words(key_), hw = (nw + 1) / 2;
+        std::vector<uint32_t> n(nw), lam(nw), mu(nw), p(hw), q(hw);
+        fthe_shim::check(fthe_key_export(key_, n.data(), lam.data(), mu.data(), p.data(), q.data()), "export");
+        fthe_shim::from_words(paillier_cpu.n, n.data(), nw);
+        mpz_mul(paillier_cpu.n_square, paillier_cpu.n, paillier_cpu.n);
+        mpz_add_ui(paillier_cpu.generator, paillier_cpu.n, 1);
+        fthe_shim::from_words(paillier_cpu.lambda, lam.data(), nw);
+        fthe_shim::from_words(paillier_cpu.mu, mu.data(), nw);
+        fthe_shim::from_words(paillier_cpu.p, p.data(), hw);
+        fthe_shim::from_words(paillier_cpu.q, q.data(), hw);
+        mpz_sub_ui(paillier_cpu.p, paillier_cpu.p, 1);                   // the GMP build keeps p-1, q-1 (Q5)
+        mpz_sub_ui(paillier_cpu.q, paillier_cpu.q, 1);
+        paillier_cpu.key_length = key_length;
+    }
+};

@@ -290,3 +290,20 @@ def test_ghpair_server_party_flow(dev):
     np.testing.assert_allclose(s.h, 3 * h, atol=3e-6)
     np.testing.assert_allclose(z.g, g, atol=2e-6)
     np.testing.assert_allclose(d.g, 2 * g, atol=3e-6)
+
+
+def test_sharded_two_contexts(dev, coracle):
+    """ShardedPaillier on two engine contexts (here both on cuda:0): threads x streams,
+    contiguous shards, results identical to the single-context call."""
+    from fedtree_amd.multi import ShardedPaillier
+    from fedtree_amd.paillier import Device
+    pw, qw = _det_primes(coracle, 1024, 31)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    sp = ShardedPaillier(pl, [Device(0), Device(0)])
+    m = np.random.default_rng(8).integers(0, 2**64, 10_001, dtype=np.uint64)
+    c = sp.encrypt_u64(m, seed=4)
+    assert c.shape == (len(m), 2 * pl.n_words)
+    assert np.array_equal(sp.decrypt_u64(c), m)
+    assert np.array_equal(pl.decrypt_u64(c), m)
+    s = sp.add_batch(c, c[::-1].copy())
+    assert np.array_equal(s, pl.add_batch(c, c[::-1].copy()))

@@ -1,0 +1,69 @@
+"""Summarise rocprofv3 outputs into profiles/ text/json.
+
+  python tools/rocprof_summary.py trace <results.db> <out.txt>
+      per-kernel stats (calls, total, average) + montprog exponentiation launches
+  python tools/rocprof_summary.py pmc <dir-with-counter_collection.csv>... <out.json>
+      per-dispatch counter values of fthe_montprog_s74 aggregated per launch
+"""
+import csv
+import glob
+import json
+import os
+import sqlite3
+import sys
+
+
+def trace(db, out):
+    cur = sqlite3.connect(db).cursor()
+    lines = ["kernel,calls,total_ms,avg_ms,pct"]
+    for name, calls, tot, avg, pct in cur.execute("select * from top_kernels"):
+        lines.append(f"{name[:90]},{calls},{tot / 1e6:.3f},{avg / 1e6:.4f},{pct:.3f}")
+    durs = [d for (d,) in cur.execute("select duration from kernels where name like 'fthe_montprog%'")]
+    heavy = [d for d in durs if d > 10e6]        # exponentiation launches (> 10 ms)
+    lines.append("")
+    lines.append(f"fthe_montprog exponentiation launches (>10 ms): n={len(heavy)} "
+                 f"avg_ms={sum(heavy) / max(1, len(heavy)) / 1e6:.3f} "
+                 f"min_ms={min(heavy) / 1e6 if heavy else 0:.3f} max_ms={max(heavy) / 1e6 if heavy else 0:.3f}")
+    row = cur.execute("select vgpr_count, accum_vgpr_count, sgpr_count, lds_size, grid_x, workgroup_x "
+                      "from kernels where name like 'fthe_montprog%' limit 1").fetchone()
+    if row:
+        lines.append(f"fthe_montprog resources: vgpr={row[0]} agpr={row[1]} sgpr={row[2]} lds={row[3]} "
+                     f"grid_x={row[4]} wg={row[5]}")
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[-3:]))
+
+
+def pmc(dirs, out):
+    agg = {}
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if not r.get("Kernel_Name", "").startswith("fthe_montprog"):
+                    continue
+                key = (r["Dispatch_Id"], r["Counter_Name"])
+                agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
+    per = {}
+    for (disp, name), v in agg.items():
+        per.setdefault(name, []).append(v)
+    res = {}
+    for name, v in per.items():
+        v = sorted(v, reverse=True)
+        heavy = [x for x in v if x >= 0.25 * v[0]]     # exponentiation launches dominate every counter
+        res[name] = {"dispatches": len(v), "expo_dispatches": len(heavy),
+                     "expo_mean": sum(heavy) / len(heavy), "all_mean": sum(v) / len(v)}
+    if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
+        # FETCH_SIZE/WRITE_SIZE are KB; gfx950 FETCH_SIZE reads 1/2 of a coalesced
+        # stream (MI355X_MICROARCH.md HBM): calibrated on this kernel -- the loads
+        # the program issues (329 x 296 B per lane per launch) are 2.05x FETCH_SIZE.
+        f, w = res["FETCH_SIZE"]["expo_mean"], res["WRITE_SIZE"]["expo_mean"]
+        res["hbm_bytes_per_launch"] = (2 * f + w) * 1024
+        res["hbm_bytes_formula"] = "(2*FETCH_SIZE + WRITE_SIZE) * 1024, exponentiation launches"
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "trace":
+        trace(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2:-1], sys.argv[-1])
