@@ -39,56 +39,59 @@ inline void mpz_to_words(const mpz_t x, uint32_t *w, int n) {
     if (mpz_sizeinbase(x, 2) > (size_t)n * 32) return;
     mpz_export(w, &cnt, -1, 4, 0, 0, x);
 }
-// radix-2^28 limbs (S of them)
-inline std::vector<uint32_t> to_limbs(const mpz_t x, int S) {
+// radix-2^B limbs (S of them)
+inline std::vector<uint32_t> to_limbs(const mpz_t x, int S, int B = RADIX_BITS) {
     std::vector<uint32_t> l(S, 0);
     Mpz t; mpz_set(t, x);
+    const uint32_t mask = (1u << B) - 1;
     for (int k = 0; k < S; k++) {
-        l[k] = (uint32_t)(mpz_get_ui(t) & RADIX_MASK);
-        mpz_fdiv_q_2exp(t, t, RADIX_BITS);
+        l[k] = (uint32_t)(mpz_get_ui(t) & mask);
+        mpz_fdiv_q_2exp(t, t, B);
     }
     return l;
 }
 
+// Kernel variants: limbs S of radix 2^B, lanes per ciphertext.  A modulus of
+// `bits` bits needs R = 2^(B S) >= 2^8 N (almost-Montgomery headroom) and
+// 2 S (2^B)^2 < 2^63 (64-bit column accumulators never overflow).
+struct Shape { int S, B, lanes; };
+inline Shape kernel_shape_for_bits(int bits) {
+    static const Shape avail[] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}};
+    for (const Shape &s : avail)
+        if (bits + 8 <= s.B * s.S) return s;
+    return Shape{0, 0, 0};
+}
+
 // Montgomery modulus for the radix-2^28 program kernel with S limbs.
 struct MontMod {
-    int S = 0;
+    Shape sh{0, 0, 0};
+    int S = 0, B = RADIX_BITS;
     Mpz N, R, R2, R3;
     uint32_t nprime = 0;
     std::vector<uint32_t> ctx;   // N limbs (S) + nprime: the kernel's ctx buffer
-    void init(const mpz_t modulus, int limbs) {
-        S = limbs;
+    void init(const mpz_t modulus, Shape shape) {
+        sh = shape; S = shape.S; B = shape.B;
         mpz_set(N, modulus);
-        mpz_set_ui(R, 1); mpz_mul_2exp(R, R, (mp_bitcnt_t)RADIX_BITS * S);
+        mpz_set_ui(R, 1); mpz_mul_2exp(R, R, (mp_bitcnt_t)B * S);
         mpz_powm_ui(R2, R, 2, N);
         mpz_powm_ui(R3, R, 3, N);
         Mpz m2b, inv;
-        mpz_set_ui(m2b, 1); mpz_mul_2exp(m2b, m2b, RADIX_BITS);
+        mpz_set_ui(m2b, 1); mpz_mul_2exp(m2b, m2b, B);
         mpz_invert(inv, N, m2b);
         mpz_sub(inv, m2b, inv);
         nprime = (uint32_t)mpz_get_ui(inv);
-        ctx = to_limbs(N, S);
+        ctx = to_limbs(N, S, B);
         ctx.push_back(nprime);
     }
+    std::vector<uint32_t> limbs(const mpz_t x) const { return to_limbs(x, S, B); }
     // x * R mod N (Montgomery form of x), as limbs
     std::vector<uint32_t> mont(const mpz_t x) const {
         Mpz t; mpz_mul(t, x, R); mpz_mod(t, t, N);
-        return to_limbs(t, S);
-    }
-    std::vector<uint32_t> plain(const mpz_t x) const {
-        Mpz t; mpz_mod(t, x, N);
-        return to_limbs(t, S);
+        return to_limbs(t, S, B);
     }
 };
 
-// Smallest kernel limb count whose R = 2^(28 S) exceeds 4N with margin
-// (the kernel keeps every intermediate < 2N without final subtractions).
-inline int kernel_limbs_for_bits(int bits) {
-    static const int avail[] = {37, 74};
-    for (int s : avail)
-        if (bits + 8 <= RADIX_BITS * s) return s;
-    return 0;
-}
+inline int kernel_limbs_for_bits(int bits) { return kernel_shape_for_bits(bits).S; }
 
 // ---- uniform op program for the montprog kernel ---------------------------
 enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL = 4,

@@ -31,11 +31,11 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 2;
-const int kVariantS[MAX_VARIANTS] = {37, 74};
+constexpr int MAX_VARIANTS = 3;
+const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}};
 
 int variant_index(int S) {
-    for (int i = 0; i < MAX_VARIANTS; i++) if (kVariantS[i] == S) return i;
+    for (int i = 0; i < MAX_VARIANTS; i++) if (kVariants[i].S == S) return i;
     return -1;
 }
 
@@ -118,14 +118,15 @@ struct DevMod {
 // A named constant (S limbs) on the device.
 struct fthe_key {
     int device = 0;
-    int S = 0;                      // kernel limbs for this key
+    Shape spq{0, 0, 0}, sn2{0, 0, 0};   // kernel shapes: mod p^2/q^2/p/q and mod n^2
     int n_bits = 0, n_words = 0;
     bool priv = false, pub_ok = false;
     Mpz n, n2, g, p, q, lambda, mu;
     DevMod mn2, mp2, mq2, mp, mq;
     int kp = 0, kq = 0;             // limbs of p, q
-    // device constants: one allocation, S limbs each
+    // device constants: one allocation, each its modulus' limb count
     std::vector<std::vector<uint32_t>> host_consts;
+    std::vector<size_t> const_off;
     uint32_t *d_consts = nullptr;
     // programs: one allocation
     std::vector<uint32_t> host_progs;
@@ -140,11 +141,12 @@ struct fthe_key {
     }
     // constant handles
     int add_const(const std::vector<uint32_t> &limbs) {
-        std::vector<uint32_t> v(limbs); v.resize(S, 0);
-        host_consts.push_back(v);
+        size_t off = const_off.empty() ? 0 : const_off.back() + host_consts.back().size();
+        host_consts.push_back(limbs);
+        const_off.push_back(off);
         return (int)host_consts.size() - 1;
     }
-    uint32_t *cst(int h) const { return d_consts + (size_t)h * S; }
+    uint32_t *cst(int h) const { return d_consts + const_off[h]; }
     // programs
     struct PH { size_t off = 0; double mm = 0; };
     PH add_prog(const Prog &p) {
@@ -157,7 +159,7 @@ struct fthe_key {
     // ---- slot maps and programs --------------------------------------------
     int w_pub = 5, w_crt = 5, w_dec = 5, tabn_max = 16;
     // consts
-    int c_one = -1, c_R2n2 = -1, c_nRn2 = -1, c_n2 = -1;
+    int c_one = -1, c_one_n2 = -1, c_R2n2 = -1, c_nRn2 = -1, c_n2 = -1;
     int c_R2p = -1, c_R3p = -1, c_nRp = -1, c_R2q = -1, c_R3q = -1, c_nRq = -1;
     int c_p2 = -1, c_q2 = -1, c_2p2 = -1, c_qinvRp2 = -1;
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
@@ -201,11 +203,11 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
     c->device = device;
     HIPOK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < MAX_VARIANTS; i++) {
-        const unsigned char *blob = fthe_montprog_blob(kVariantS[i]);
+        const unsigned char *blob = fthe_montprog_blob(kVariants[i].S);
         if (!blob) return FTHE_ERR_HIP;
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
-        snprintf(name, sizeof name, "fthe_montprog_s%d", kVariantS[i]);
+        snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
     }
     HIPOK(hipEventCreate(&c->ev0));
@@ -275,37 +277,34 @@ extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, 
 
 // ---------------------------------------------------------------------------
 // Key set-up
-static int upload_mod(DevMod &d, const mpz_t N, int S) {
-    d.m.init(N, S);
+static int upload_mod(DevMod &d, const mpz_t N, Shape sh) {
+    d.m.init(N, sh);
     if (hipMalloc(&d.d_ctx, d.m.ctx.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(d.d_ctx, d.m.ctx.data(), d.m.ctx.size() * 4, hipMemcpyHostToDevice));
     return FTHE_OK;
 }
 
 static int key_finish(fthe_key *k) {
-    // choose kernel variant
-    int sp = 0;
+    // choose kernel variants: CRT moduli (p^2, q^2, p, q) and n^2
     if (k->priv) {
         Mpz p2; mpz_mul(p2, k->p, k->p);
         Mpz q2; mpz_mul(q2, k->q, k->q);
         size_t b = std::max(p2.bits(), q2.bits());
-        sp = kernel_limbs_for_bits((int)b);
-        if (!sp) return FTHE_ERR_UNSUPPORTED;
+        k->spq = kernel_shape_for_bits((int)b);
+        if (!k->spq.S) return FTHE_ERR_UNSUPPORTED;
     }
-    int sn = kernel_limbs_for_bits((int)k->n2.bits());
-    k->pub_ok = sn != 0;
+    k->sn2 = kernel_shape_for_bits((int)k->n2.bits());
+    k->pub_ok = k->sn2.S != 0;
     if (!k->pub_ok && !k->priv) return FTHE_ERR_UNSUPPORTED;
-    k->S = std::max(sp, sn);
-    if (!k->pub_ok) k->S = sp;
-    const int S = k->S;
     Mpz one(1);
-    k->c_one = k->add_const(to_limbs(one, S));
 
     if (k->pub_ok) {
-        int rc = upload_mod(k->mn2, k->n2, S); if (rc) return rc;
-        k->c_R2n2 = k->add_const(to_limbs(k->mn2.m.R2, S));
-        k->c_nRn2 = k->add_const(k->mn2.m.mont(k->n));
-        k->c_n2 = k->add_const(to_limbs(k->n2, S));
+        int rc = upload_mod(k->mn2, k->n2, k->sn2); if (rc) return rc;
+        const MontMod &M = k->mn2.m;
+        k->c_one_n2 = k->add_const(M.limbs(one));
+        k->c_R2n2 = k->add_const(M.limbs(M.R2));
+        k->c_nRn2 = k->add_const(M.mont(k->n));
+        k->c_n2 = k->add_const(M.limbs(k->n2));
         // encrypt: X = r R; X^n; (1 + m n) X  (paillier.cpp:135-137 with g^m = 1 + m n)
         Prog e;
         k->w_pub = best_window(k->n.bits());
@@ -324,28 +323,32 @@ static int key_finish(fthe_key *k) {
     if (k->priv) {
         int rc;
         Mpz p2, q2; mpz_mul(p2, k->p, k->p); mpz_mul(q2, k->q, k->q);
-        if ((rc = upload_mod(k->mp2, p2, S))) return rc;
-        if ((rc = upload_mod(k->mq2, q2, S))) return rc;
-        if ((rc = upload_mod(k->mp, k->p, S))) return rc;
-        if ((rc = upload_mod(k->mq, k->q, S))) return rc;
-        k->kp = (int)((k->p.bits() + RADIX_BITS - 1) / RADIX_BITS);
-        k->kq = (int)((k->q.bits() + RADIX_BITS - 1) / RADIX_BITS);
+        const Shape sh = k->spq;
+        const int S = sh.S, RB = sh.B;
+        if ((rc = upload_mod(k->mp2, p2, sh))) return rc;
+        if ((rc = upload_mod(k->mq2, q2, sh))) return rc;
+        if ((rc = upload_mod(k->mp, k->p, sh))) return rc;
+        if ((rc = upload_mod(k->mq, k->q, sh))) return rc;
+        auto L_ = [&](const mpz_t x) { return to_limbs(x, S, RB); };
+        k->c_one = k->add_const(L_(one));
+        k->kp = (int)((k->p.bits() + RB - 1) / RB);
+        k->kq = (int)((k->q.bits() + RB - 1) / RB);
         // --- CRT encrypt constants
         Mpz np, nq, ep, eq, t;
         mpz_mod(np, k->n, p2); mpz_mod(nq, k->n, q2);
         Mpz pm1, qm1; mpz_sub_ui(pm1, k->p, 1); mpz_sub_ui(qm1, k->q, 1);
         mpz_mul(t, k->p, pm1); mpz_mod(ep, k->n, t);     // n mod p(p-1): order of (Z/p^2)^*
         mpz_mul(t, k->q, qm1); mpz_mod(eq, k->n, t);
-        k->c_R2p = k->add_const(to_limbs(k->mp2.m.R2, S));
+        k->c_R2p = k->add_const(L_(k->mp2.m.R2));
         k->c_nRp = k->add_const(k->mp2.m.mont(np));
-        k->c_R2q = k->add_const(to_limbs(k->mq2.m.R2, S));
+        k->c_R2q = k->add_const(L_(k->mq2.m.R2));
         k->c_nRq = k->add_const(k->mq2.m.mont(nq));
-        k->c_R3p = k->add_const(to_limbs(k->mp2.m.R3, S));
-        k->c_R3q = k->add_const(to_limbs(k->mq2.m.R3, S));
-        k->c_p2 = k->add_const(to_limbs(p2, S));
-        k->c_q2 = k->add_const(to_limbs(q2, S));
+        k->c_R3p = k->add_const(L_(k->mp2.m.R3));
+        k->c_R3q = k->add_const(L_(k->mq2.m.R3));
+        k->c_p2 = k->add_const(L_(p2));
+        k->c_q2 = k->add_const(L_(q2));
         mpz_mul_2exp(t, p2, 1);
-        k->c_2p2 = k->add_const(to_limbs(t, S));
+        k->c_2p2 = k->add_const(L_(t));
         Mpz qi; if (!mpz_invert(qi, q2, p2)) return FTHE_ERR_KEY;
         k->c_qinvRp2 = k->add_const(k->mp2.m.mont(qi));
         k->w_crt = best_window(std::max(ep.bits(), eq.bits()));
@@ -365,17 +368,17 @@ static int key_finish(fthe_key *k) {
             k->pr_crt_h = k->add_prog(h);
         }
         // --- CRT decrypt constants
-        k->c_p = k->add_const(to_limbs(k->p, S));
-        k->c_q = k->add_const(to_limbs(k->q, S));
+        k->c_p = k->add_const(L_(k->p));
+        k->c_q = k->add_const(L_(k->q));
         mpz_mul_2exp(t, k->p, 1);
-        k->c_2p = k->add_const(to_limbs(t, S));
+        k->c_2p = k->add_const(L_(t));
         Mpz m2k, pinv, qinv;
-        mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RADIX_BITS * k->kp);
+        mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RB * k->kp);
         mpz_invert(pinv, k->p, m2k);
-        k->c_pinv = k->add_const(to_limbs(pinv, S));
-        mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RADIX_BITS * k->kq);
+        k->c_pinv = k->add_const(L_(pinv));
+        mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RB * k->kq);
         mpz_invert(qinv, k->q, m2k);
-        k->c_qinv2 = k->add_const(to_limbs(qinv, S));
+        k->c_qinv2 = k->add_const(L_(qinv));
         // h_P = L_P(g^(P-1) mod P^2)^-1 mod P
         for (int side = 0; side < 2; side++) {
             const Mpz &P = side ? k->q : k->p;
@@ -413,10 +416,9 @@ static int key_finish(fthe_key *k) {
         }
     }
     // upload constants and programs
-    size_t nc = k->host_consts.size();
-    if (hipMalloc(&k->d_consts, nc * S * 4) != hipSuccess) return FTHE_ERR_NOMEM;
-    std::vector<uint32_t> flat; flat.reserve(nc * S);
+    std::vector<uint32_t> flat;
     for (auto &v : k->host_consts) flat.insert(flat.end(), v.begin(), v.end());
+    if (hipMalloc(&k->d_consts, flat.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(k->d_consts, flat.data(), flat.size() * 4, hipMemcpyHostToDevice));
     if (hipMalloc(&k->d_progs, k->host_progs.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(k->d_progs, k->host_progs.data(), k->host_progs.size() * 4, hipMemcpyHostToDevice));
@@ -527,6 +529,7 @@ int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *mod
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     int vi = variant_index(S);
     if (vi < 0) return FTHE_ERR_UNSUPPORTED;
+    const unsigned blocks = (unsigned)((size_t)L * kVariants[vi].lanes / 256);
     std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
     if (c->prof) {
         if (c->prof_used == c->prof_ev.size()) {
@@ -540,7 +543,7 @@ int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *mod
         ev = &c->prof_ev[c->prof_used++];
         HIPOK(hipEventRecord(ev->first, c->stream));
     }
-    if (hipModuleLaunchKernel(c->fn[vi], L / 256, 1, 1, 256, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
+    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, 256, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
         return FTHE_ERR_HIP;
     if (ev) {
         HIPOK(hipEventRecord(ev->second, c->stream));
@@ -551,10 +554,11 @@ int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *mod
 }
 
 struct Launch {
-    fthe_ctx *c; const fthe_key *k; int L; int S; double mm = 0; size_t live = 0;
+    fthe_ctx *c; const fthe_key *k; int L; int S; int B; double mm = 0; size_t live = 0;
     uint32_t *slot(int s) const { return (uint32_t *)c->slots.p + (size_t)s * S * L; }
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
     int prog(const fthe_key::PH &ph, const DevMod &mod) {
+        if (mod.m.S != S) return FTHE_ERR_ARG;
         int rc = launch_montprog(c, S, L, k->prog(ph), mod.d_ctx, ph.mm, live);
         if (rc) return rc;
         mm += ph.mm * (double)live;
@@ -565,15 +569,17 @@ struct Launch {
     }
 };
 
-int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots) {
+int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots, Shape sh) {
     if (!c || !k) return FTHE_ERR_ARG;
     if (k->device != c->device) return FTHE_ERR_ARG;
+    if (!sh.S) return FTHE_ERR_UNSUPPORTED;
     HIPOK(hipSetDevice(c->device));
-    size_t ch = chunk_lanes();
+    size_t ch = chunk_lanes() / (size_t)sh.lanes;          // same slot footprint per chunk
+    ch = (ch + 255) / 256 * 256;
     size_t L = std::min(ch, (count + 255) / 256 * 256);
     if (L == 0) L = 256;
-    Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = k->S;
-    int rc = c->slots.ensure((size_t)nslots * k->S * L * 4);
+    Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = sh.S; Lc.B = sh.B;
+    int rc = c->slots.ensure((size_t)nslots * sh.S * L * 4);
     if (rc) return rc;
     HIPOK(hipEventRecord(c->ev0, c->stream));
     return FTHE_OK;
@@ -599,9 +605,9 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
     bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
     if (!crt && !k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    int rc = begin_call(c, k, count, Lc, nslots_for(k), crt ? k->spq : k->sn2);
     if (rc) return rc;
-    const int S = k->S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     // scratch: AoS r words for the device RNG
     if (!r && (rc = c->scratch.ensure((size_t)L * nw * 4))) return rc;
     RngKey rk{};
@@ -622,28 +628,28 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
         Lc.live = cnt;
         if (r) {
             hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, r + off * r_words, r_words, cnt, 0,
-                               Lc.slot(SL_IN0), S, L);
+                               Lc.slot(SL_IN0), S, L, Lc.B);
         } else {
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_nwords, nw, k->n_bits, rk,
                                (uint64_t)off, cnt, (uint32_t *)c->scratch.p);
             hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, (const uint32_t *)c->scratch.p, nw,
-                               cnt, 0, Lc.slot(SL_IN0), S, L);
+                               cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         }
-        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L);
+        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (crt) {
             if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;
             if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
             hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
-                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L);
+                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
             if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
-            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L);
+            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
             hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
-                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr);
+                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else {
             if ((rc = Lc.prog(k->pr_enc_pub, k->mn2))) return rc;
             hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
-                               S, L, cnt, out + off * cw, cw);
+                               S, L, cnt, out + off * cw, cw, Lc.B);
         }
     }
     return end_call(c, Lc);
@@ -656,9 +662,9 @@ extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, si
     if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
     if (!k->priv) return FTHE_ERR_NOPRIV;
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    int rc = begin_call(c, k, count, Lc, nslots_for(k), k->spq);
     if (rc) return rc;
-    const int S = k->S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p);
     Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_R3q);
     Lc.fill(SL_T5, k->c_one);
@@ -666,27 +672,27 @@ extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, si
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
         const uint32_t *src = ct + off * cw;
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L);
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, RADIX_BITS * S,
-                           Lc.slot(SL_IN1), S, L);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, Lc.B * S,
+                           Lc.slot(SL_IN1), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
         if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) return rc;
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,
-                           k->cst(k->c_pinv), k->kp, Lc.slot(SL_T1), L);
+                           k->cst(k->c_pinv), k->kp, Lc.slot(SL_T1), L, Lc.B);
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2), S,
-                           k->cst(k->c_qinv2), k->kq, Lc.slot(SL_T2), L);
+                           k->cst(k->c_qinv2), k->kq, Lc.slot(SL_T2), L, Lc.B);
         // slots C0/C1/C2 are reused for the mod-p / mod-q constants of the tail
         Lc.fill(SL_C0, k->c_hRp); Lc.fill(SL_C1, k->c_hRq); Lc.fill(SL_C2, k->c_qinvRp);
         if ((rc = Lc.prog(k->pr_dec_hp, k->mp))) return rc;
         if ((rc = Lc.prog(k->pr_dec_hq, k->mq))) return rc;
         hipLaunchKernelGGL(k_crt_dec_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
-                           k->cst(k->c_p), k->cst(k->c_q), k->cst(k->c_2p), Lc.slot(SL_T3), S, L);
+                           k->cst(k->c_p), k->cst(k->c_q), k->cst(k->c_2p), Lc.slot(SL_T3), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_dec_t, k->mp))) return rc;
-        hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T4), k->cst(k->c_p), S, L);
+        hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T4), k->cst(k->c_p), S, L, Lc.B);
         // m = mq + q t   (< n)
         hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S, k->cst(k->c_q),
                            k->kq, Lc.slot(SL_T4), k->kp, L, cnt, m_full ? m_full + off * nw : (uint32_t *)nullptr, nw,
-                           m_low ? m_low + off : (uint64_t *)nullptr);
+                           m_low ? m_low + off : (uint64_t *)nullptr, Lc.B);
         if (off + L < count) {   // restore the exponentiation constants for the next chunk
             Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p); Lc.fill(SL_C2, k->c_R2q);
         }
@@ -700,18 +706,18 @@ extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const u
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    int rc = begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
     if (rc) return rc;
-    const int S = k->S, L = Lc.L, cw = 2 * k->n_words;
+    const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     Lc.fill(SL_C0, k->c_R2n2);
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L);
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_add, k->mn2))) return rc;
         hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
-                           cnt, out + off * cw, cw);
+                           cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
 }
@@ -730,6 +736,7 @@ static int upload_dyn_prog(fthe_ctx *c, const Prog &p, fthe_key::PH &ph, DevBuf 
 namespace {
 // Launch with an explicit (dynamic) program pointer.
 int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod) {
+    if (mod.m.S != Lc.S) return FTHE_ERR_ARG;
     int rc = launch_montprog(Lc.c, Lc.S, Lc.L, prog, mod.d_ctx, mm, Lc.live);
     if (rc) return rc;
     Lc.mm += mm * (double)Lc.live;
@@ -744,11 +751,11 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     const int base = nslots_for(k);               // inputs live after the standard slots
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, base + kk);
+    int rc = begin_call(c, k, count, Lc, base + kk, k->sn2);
     if (rc) return rc;
-    const int S = k->S, L = Lc.L, cw = 2 * k->n_words;
+    const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
-    std::vector<uint32_t> rl = to_limbs(Rk, S);
+    std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
     Prog p;
     p.loadx(base);
     for (int j = 1; j < kk; j++) p.mul(base + j);
@@ -768,10 +775,10 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
         Lc.live = cnt;
         for (int j = 0; j < kk; j++)
             hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + ((size_t)j * count + off) * cw, cw,
-                               cnt, 0, Lc.slot(base + j), S, L);
+                               cnt, 0, Lc.slot(base + j), S, L, Lc.B);
         if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
         hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
-                           cnt, out + off * cw, cw);
+                           cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
 }
@@ -781,9 +788,9 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     if (!k || !c || ((!x || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k));
+    int rc = begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
     if (rc) return rc;
-    const int S = k->S, L = Lc.L, cw = 2 * k->n_words;
+    const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     Prog p;
     if (e == 0) {
         p.loadx(SL_C1);                 // x^0 = 1
@@ -797,14 +804,14 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     fthe_key::PH ph;
     if ((rc = upload_dyn_prog(c, p, ph, c->io[3]))) return rc;
     HIPOK(hipEventRecord(c->ev0, c->stream));
-    Lc.fill(SL_C0, k->c_R2n2); Lc.fill(SL_C1, k->c_one);
+    Lc.fill(SL_C0, k->c_R2n2); Lc.fill(SL_C1, k->c_one_n2);
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L);
+        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
         hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
-                           cnt, out + off * cw, cw);
+                           cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
 }

@@ -7,18 +7,18 @@
 namespace fthe {
 struct RngKey { uint32_t k[8]; uint64_t nonce; };
 
-__global__ void k_pack_words(const uint32_t *in, int win, size_t count, int bit0, uint32_t *slot, int S, int L);
-__global__ void k_pack_u64(const uint64_t *m, size_t count, uint32_t *slot, int S, int L);
+__global__ void k_pack_words(const uint32_t *in, int win, size_t count, int bit0, uint32_t *slot, int S, int L, int rb);
+__global__ void k_pack_u64(const uint64_t *m, size_t count, uint32_t *slot, int S, int L, int rb);
 __global__ void k_fill_const(const uint32_t *limbs, uint32_t *slot, int S, int L);
-__global__ void k_canon(uint32_t *x, const uint32_t *N, int S, int L);
-__global__ void k_unpack_canon(uint32_t *x, const uint32_t *N, int S, int L, size_t count, uint32_t *out, int wout);
+__global__ void k_canon(uint32_t *x, const uint32_t *N, int S, int L, int rb);
+__global__ void k_unpack_canon(uint32_t *x, const uint32_t *N, int S, int L, size_t count, uint32_t *out, int wout, int rb);
 __global__ void k_crt_enc_prep(uint32_t *cp, uint32_t *cq, const uint32_t *p2, const uint32_t *q2,
-                               const uint32_t *two_p2, uint32_t *u, int S, int L);
+                               const uint32_t *two_p2, uint32_t *u, int S, int L, int rb);
 __global__ void k_mul_add_out(const uint32_t *a, int na, const uint32_t *B, int nb, const uint32_t *h, int nh,
-                              int L, size_t count, uint32_t *out, int wout, uint64_t *out_low);
-__global__ void k_dec_lfunc(uint32_t *x, const uint32_t *P2, int S, const uint32_t *Pinv, int ky, uint32_t *y, int L);
+                              int L, size_t count, uint32_t *out, int wout, uint64_t *out_low, int rb);
+__global__ void k_dec_lfunc(uint32_t *x, const uint32_t *P2, int S, const uint32_t *Pinv, int ky, uint32_t *y, int L, int rb);
 __global__ void k_crt_dec_prep(uint32_t *mp, uint32_t *mq, const uint32_t *p, const uint32_t *q,
-                               const uint32_t *two_p, uint32_t *d, int S, int L);
+                               const uint32_t *two_p, uint32_t *d, int S, int L, int rb);
 __global__ void k_rng_r(const uint32_t *n_words, int nw, int nbits, RngKey key, uint64_t index0, size_t count, uint32_t *r);
 __global__ void k_encode_fixed(const float *x, size_t count, uint64_t *m);
 __global__ void k_decode_fixed(const uint64_t *m, size_t count, float *x);

@@ -294,6 +294,14 @@ def gen(S: int, B: int, U: int, name: str) -> str:
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
     e('')
+    o.extend(_descriptor(name, lds_bytes, NVGPR, NSGPR).splitlines())
+    return "\n".join(o) + "\n"
+
+
+
+def _descriptor(name, lds_bytes, NVGPR, NSGPR):
+    o = []
+    e = o.append
     # ---- kernel descriptor ------------------------------------------------
     e('.rodata')
     e('.p2align 6')
@@ -345,15 +353,289 @@ def gen(S: int, B: int, U: int, name: str) -> str:
     return "\n".join(o) + "\n"
 
 
+def gen_quad(S: int, B: int, U: int, name: str) -> str:
+    """Four lanes per ciphertext, for moduli up to B*S - 8 bits (n^2 of
+    Paillier-2048: S = 152 limbs of B = 27 bits; 2*152 products of < 2^54 keep
+    every 64-bit column below 2^63).  Lane k of a quad owns limbs [kQ, (k+1)Q)
+    of X, of the modulus N (held in VGPRs: it differs per lane) and of the
+    accumulator window.  Per outer iteration q is computed on lane 0 and
+    broadcast inside the quad (DPP quad_perm), the carry of the retired column
+    stays on lane 0, and every lane hands its lowest column to the lane below
+    (DPP) -- one 64-bit hand-off per lane per iteration.  16 ciphertexts per
+    wavefront, 168 VGPRs -> 3 waves/SIMD.
+
+    Slot layout is the limb-major [k][g] layout of gen(), g the ciphertext
+    index; kernarg limb_stride = L*4 for L ciphertexts."""
+    assert S % 4 == 0 and U % 2 == 0
+    Q = S // 4
+    MASK = (1 << B) - 1
+    NTRIPS, TAIL = S // U, S % U
+    # VGPRs: v0 tid (set-up) then the lane's A-write base, v1 lane offset in a
+    # slot row, v2 A read cursor (rests at the ciphertext's A column), v3/v4 a_i,
+    # v5 q, v[6:7] 64-bit temp, then X, N quarter, T window.
+    V_TID = V_LDSW = 0
+    V_GOFF, V_LDSI = 1, 2
+    V_AI = (3, 4)
+    V_Q = 5
+    V_TMP = 6
+    XB = 8
+    NB = XB + Q
+    TB = NB + Q
+    if TB % 2:
+        TB += 1
+    NT = Q + U
+    NVGPR = TB + 2 * NT
+    assert NVGPR <= 256, NVGPR
+    NSGPR = 32
+
+    def T(k):
+        return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
+
+    def Tlo(k):
+        return f"v{TB + 2 * k}"
+
+    def Thi(k):
+        return f"v{TB + 2 * k + 1}"
+
+    def X(k):
+        return f"v{XB + k}"
+
+    def NV(k):
+        return f"v{NB + k}"
+
+    o = []
+    e = o.append
+    lds_per_wave = S * 64          # A[i][c]: 16 ciphertexts x 4 B per row
+    lds_bytes = 4 * lds_per_wave
+    DPP = "row_mask:0xf bank_mask:0xf"
+    tmp = f"v[{V_TMP}:{V_TMP + 1}]"
+    e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
+    e('.amdhsa_code_object_version 5')
+    e('.text')
+    e(f'.globl {name}')
+    e('.p2align 8')
+    e(f'.type {name},@function')
+    e(f'{name}:')
+    e('  s_load_dwordx2 s[4:5], s[0:1], 0x0')
+    e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
+    e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
+    e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
+    # lane masks: k == 3 -> s[20:21], k == 0 -> s[22:23]
+    e('  s_mov_b32 s20, 0x88888888')
+    e('  s_mov_b32 s21, 0x88888888')
+    e('  s_mov_b32 s22, 0x11111111')
+    e('  s_mov_b32 s23, 0x11111111')
+    e('  s_waitcnt lgkmcnt(0)')
+    e(f'  s_load_dword s12, s[8:9], {hex(4 * S)}')
+    # g = wg*64 + tid>>2 ; k = tid & 3
+    e('  s_lshl_b32 s14, s2, 8')                                # wg*64*4 bytes
+    e(f'  v_lshrrev_b32_e32 v{V_GOFF}, 2, v{V_TID}')
+    e(f'  v_lshlrev_b32_e32 v{V_GOFF}, 2, v{V_GOFF}')
+    e(f'  v_add_u32_e32 v{V_GOFF}, s14, v{V_GOFF}')             # g*4
+    e(f'  v_and_b32_e32 v{V_TMP}, 3, v{V_TID}')                 # k
+    e(f'  v_mul_u32_u24_e32 v{V_TMP + 1}, {Q}, v{V_TMP}')       # k*Q
+    e(f'  v_mul_lo_u32 v{V_Q}, v{V_TMP + 1}, s10')               # k*Q*L*4
+    e(f'  v_add_u32_e32 v{V_GOFF}, v{V_GOFF}, v{V_Q}')
+    e(f'  v_lshlrev_b32_e32 v{V_Q}, 2, v{V_TMP + 1}')            # k*Q*4
+    for j in range(Q):
+        e(f'  global_load_dword {NV(j)}, v{V_Q}, s[8:9] offset:{4 * j}')
+    # A column of ciphertext c = (tid>>2)&15 in wave w = tid>>6
+    e(f'  v_lshrrev_b32_e32 v{V_LDSI}, 6, v{V_TID}')
+    e(f'  v_mul_u32_u24_e32 v{V_LDSI}, {hex(lds_per_wave)}, v{V_LDSI}')
+    e(f'  v_lshrrev_b32_e32 v{V_Q}, 2, v{V_TID}')
+    e(f'  v_and_b32_e32 v{V_Q}, 15, v{V_Q}')
+    e(f'  v_lshl_add_u32 v{V_LDSI}, v{V_Q}, 2, v{V_LDSI}')
+    e(f'  v_mul_u32_u24_e32 v{V_LDSW}, {Q * 64}, v{V_TMP}')        # k*Q*64 (tid dies here)
+    e(f'  v_add_u32_e32 v{V_LDSW}, v{V_LDSW}, v{V_LDSI}')
+    e('  s_waitcnt vmcnt(0) lgkmcnt(0)')
+
+    e('.Lprog:')
+    e('  s_load_dwordx2 s[14:15], s[6:7], 0x0')
+    e('  s_add_u32 s6, s6, 8')
+    e('  s_addc_u32 s7, s7, 0')
+    e('  s_waitcnt lgkmcnt(0)')
+    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
+                      (5, '.Laddslot'), (6, '.Laddsmall')):
+        e(f'  s_cmp_eq_u32 s14, {code}')
+        e(f'  s_cbranch_scc1 {lab}')
+    e('  s_branch .Lend')
+
+    def slot_addr():
+        e('  s_mul_i32 s16, s15, s11')
+        e('  s_mul_hi_u32 s17, s15, s11')
+        e('  s_add_u32 s16, s4, s16')
+        e('  s_addc_u32 s17, s5, s17')
+
+    def step_addr():
+        e('  s_add_u32 s16, s16, s10')
+        e('  s_addc_u32 s17, s17, 0')
+
+    def load_quarter(dst):
+        slot_addr()
+        for k in range(Q):
+            e(f'  global_load_dword {dst(k)}, v{V_GOFF}, s[16:17]')
+            if k != Q - 1:
+                step_addr()
+        e('  s_waitcnt vmcnt(0)')
+
+    def ripple_quad():
+        """X limbs + a pending 64-bit carry-out in tmp (of this lane) -> carries
+        move to the next lane's limb 0 (DPP quad_perm [0,0,1,2]; lane 0 gets
+        none) and ripple until no lane has one (at most 3 passes)."""
+        lab = f'.Lrq{len(o)}'
+        e(f'{lab}_loop:')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{V_AI[0]}, v{V_TMP} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_mov_b32_dpp v{V_AI[1]}, v{V_TMP + 1} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 v{V_TMP}, v{V_AI[0]}, 0, s[22:23]')     # lane 0: no carry in
+        e(f'  v_cndmask_b32_e64 v{V_TMP + 1}, v{V_AI[1]}, 0, s[22:23]')
+        e(f'  v_or_b32_e32 v{V_Q}, v{V_TMP}, v{V_TMP + 1}')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{V_Q}')
+        e('  s_nop 4')                                           # VALU vcc -> vccz read
+        e(f'  s_cbranch_vccz {lab}_done')
+        for k in range(Q):
+            e(f'  v_mad_u64_u32 {tmp}, vcc, {X(k)}, 1, {tmp}')
+            e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+            e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+        e(f'  s_branch {lab}_loop')
+        e(f'{lab}_done:')
+
+    def normalise_quad32():
+        """X limbs (small sums) -> radix 2^B, across the quad."""
+        e(f'  v_mov_b64_e32 {tmp}, 0')
+        for k in range(Q):
+            e(f'  v_mad_u64_u32 {tmp}, vcc, {X(k)}, 1, {tmp}')
+            e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+            e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+        ripple_quad()
+
+    e('.Lloadx:')
+    load_quarter(X)
+    e('  s_branch .Lprog')
+
+    e('.Lstorex:')
+    slot_addr()
+    for k in range(Q):
+        e(f'  global_store_dword v{V_GOFF}, {X(k)}, s[16:17]')
+        if k != Q - 1:
+            step_addr()
+    e('  s_waitcnt vmcnt(0)')
+    e('  s_branch .Lprog')
+
+    e('.Laddslot:')
+    load_quarter(lambda k: f"v{TB + k}")
+    for k in range(Q):
+        e(f'  v_add_u32_e32 {X(k)}, {X(k)}, v{TB + k}')
+    normalise_quad32()
+    e('  s_branch .Lprog')
+
+    e('.Laddsmall:')
+    e(f'  v_mov_b32_e32 v{V_TMP}, s15')
+    e(f'  v_cndmask_b32_e64 v{V_TMP}, 0, v{V_TMP}, s[22:23]')     # only lane 0 of the quad
+    e(f'  v_add_u32_e32 {X(0)}, {X(0)}, v{V_TMP}')
+    normalise_quad32()
+    e('  s_branch .Lprog')
+
+    def write_a(src):
+        for k in range(Q):
+            e(f'  ds_write_b32 v{V_LDSW}, {src(k)} offset:{k * 64}')
+            if k % 8 == 7:
+                e('  s_waitcnt lgkmcnt(0)')
+        e('  s_waitcnt lgkmcnt(0)')
+
+    e('.Lmul:')
+    load_quarter(lambda k: f"v{TB + k}")
+    write_a(lambda k: f"v{TB + k}")
+    e('  s_mov_b32 s19, 0')
+    e('  s_branch .Lmontmul')
+
+    e('.Lsqr:')
+    e('  s_mov_b32 s19, s15')
+    e('.Lsqr_loop:')
+    e('  s_cmp_eq_u32 s19, 0')
+    e('  s_cbranch_scc1 .Lprog')
+    write_a(X)
+    e('  s_branch .Lmontmul')
+
+    def iteration(u):
+        ai = f"v{V_AI[u % 2]}"
+        nai = f"v{V_AI[(u + 1) % 2]}"
+        q = f"v{V_Q}"
+        for j in range(Q):
+            e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {ai}, {X(j)}, {T(u + j)}')
+            if j == 3:
+                e(f'  v_mul_lo_u32 {q}, {Tlo(u)}, s12')
+            if j == 6:
+                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+            if j == 9:
+                e(f'  v_mov_b32_dpp {q}, {q} quad_perm:[0,0,0,0] {DPP}')
+            if j == 11:
+                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * 64}')
+        for j in range(Q):
+            e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {q}, {NV(j)}, {T(u + j)}')
+            if j == 3:
+                e(f'  v_lshrrev_b64 {tmp}, {B}, {T(u)}')
+            if j == 6:
+                e(f'  v_cndmask_b32_e64 v{V_TMP}, 0, v{V_TMP}, s[22:23]')
+                e(f'  v_cndmask_b32_e64 v{V_TMP + 1}, 0, v{V_TMP + 1}, s[22:23]')
+            if j == 9:
+                e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
+        # hand the lowest column to the lane below; lane 3 starts a fresh column
+        e(f'  v_mov_b32_dpp {Tlo(u + Q)}, {Tlo(u)} quad_perm:[1,2,3,3] {DPP}')
+        e(f'  v_mov_b32_dpp {Thi(u + Q)}, {Thi(u)} quad_perm:[1,2,3,3] {DPP}')
+        e(f'  v_cndmask_b32_e64 {Tlo(u + Q)}, {Tlo(u + Q)}, 0, s[20:21]')
+        e(f'  v_cndmask_b32_e64 {Thi(u + Q)}, {Thi(u + Q)}, 0, s[20:21]')
+        e('  s_waitcnt lgkmcnt(0)')
+
+    e('.Lmontmul:')
+    for k in range(Q):
+        e(f'  v_mov_b64_e32 {T(k)}, 0')
+    e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
+    e('  s_waitcnt lgkmcnt(0)')
+    if NTRIPS > 0:
+        e(f'  s_mov_b32 s18, {NTRIPS}')
+        e('.Ltrip:')
+        for u in range(U):
+            iteration(u)
+        for k in range(Q):
+            e(f'  v_mov_b64_e32 {T(k)}, {T(k + U)}')
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(U * 64)}, v{V_LDSI}')
+        e('  s_sub_u32 s18, s18, 1')
+        e('  s_cmp_lg_u32 s18, 0')
+        e('  s_cbranch_scc1 .Ltrip')
+    for u in range(TAIL):
+        iteration(u)
+    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIPS * U * 64)}, v{V_LDSI}')    # back to the column base
+    # normalise T[TAIL .. TAIL+Q-1] (64-bit columns) into X, then across lanes
+    e(f'  v_mov_b64_e32 {tmp}, 0')
+    for k in range(Q):
+        e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TAIL + k)}')
+        e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+        e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+    ripple_quad()
+    e('  s_cmp_eq_u32 s19, 0')
+    e('  s_cbranch_scc1 .Lprog')
+    e('  s_sub_u32 s19, s19, 1')
+    e('  s_branch .Lsqr_loop')
+    e('.Lend:')
+    e('  s_endpgm')
+    e(f'.Lfunc_end_{name}:')
+    e(f'  .size {name}, .Lfunc_end_{name}-{name}')
+    e('')
+    o.extend(_descriptor(name, lds_bytes, NVGPR, NSGPR).splitlines())
+    return "\n".join(o) + "\n"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--limbs', type=int, required=True)
     ap.add_argument('--bits', type=int, default=28)
     ap.add_argument('--unroll', type=int, default=12)
     ap.add_argument('--name', required=True)
+    ap.add_argument('--quad', action='store_true', help='four lanes per ciphertext')
     ap.add_argument('-o', '--out', required=True)
     a = ap.parse_args()
-    src = gen(a.limbs, a.bits, a.unroll, a.name)
+    src = (gen_quad if a.quad else gen)(a.limbs, a.bits, a.unroll, a.name)
     with open(a.out, 'w') as f:
         f.write(src)
 

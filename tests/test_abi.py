@@ -46,7 +46,8 @@ def test_kernel_limbs():
     lib = _lib.load()
     assert lib.fthe_kernel_limbs(1024) == 37
     assert lib.fthe_kernel_limbs(2048) == 74     # p^2 of Paillier-2048, n^2 of Paillier-1024
-    assert lib.fthe_kernel_limbs(4096) == 0      # n^2 of Paillier-2048: CRT path only in round 1
+    assert lib.fthe_kernel_limbs(4096) == 152    # n^2 of Paillier-2048: four lanes per ciphertext, radix 2^27
+    assert lib.fthe_kernel_limbs(4200) == 0
 
 
 def test_null_arguments_rejected():
