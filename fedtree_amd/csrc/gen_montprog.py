@@ -42,7 +42,7 @@ import argparse
 import sys
 
 
-def gen(S: int, B: int, U: int, name: str) -> str:
+def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
     assert U % 2 == 0 and U >= 2
     MASK = (1 << B) - 1
     NTRIPS = S // U
@@ -141,6 +141,59 @@ def gen(S: int, B: int, U: int, name: str) -> str:
         e('  s_add_u32 s16, s16, s10')
         e('  s_addc_u32 s17, s17, 0')
 
+    def emit_square():
+        """X <- X^2 R^-1 mod N, fully unrolled (S(S+1)/2 + S^2 v_mad_u64_u32)."""
+        touched = set()
+
+        def R(c):                       # register pair of column c
+            k = c % S
+            return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
+
+        def Rlo(c):
+            return f"v{TB + 2 * (c % S)}"
+
+        def mad(c, a, b):
+            src2 = R(c) if c in touched else "0"
+            touched.add(c)
+            e(f'  v_mad_u64_u32 {R(c)}, vcc, {a}, {b}, {src2}')
+
+        q = f"v{V_Q}"
+        d = f"v{V_AI[0]}"
+        tmp = f"v[{V_TMP}:{V_TMP + 1}]"
+        for i in range(S):
+            if i == 0:
+                mad(0, X(0), X(0))
+            e(f'  v_mul_lo_u32 {q}, {Rlo(i)}, s12')
+            e(f'  v_lshlrev_b32_e32 {d}, 1, {X(i)}')
+            cnt = 0
+            if i > 0:
+                mad(2 * i, X(i), X(i))
+                cnt += 1
+            for j in range(i + 1, S):
+                mad(i + j, d, X(j))
+                cnt += 1
+                if cnt == 2:
+                    e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+            if cnt < 2:
+                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+            for j in range(S):
+                mad(i + j, q, f"s{SN + j}")
+                if j == 3:
+                    e(f'  v_lshrrev_b64 {tmp}, {B}, {R(i)}')
+                if j == 7 or (j == S - 1 and S <= 7):
+                    pass
+                if j == 7:
+                    e(f'  v_lshl_add_u64 {R(i + 1)}, {tmp}, 0, {R(i + 1)}')
+            touched.discard(i)          # column i retired: its pair is reused for column i + S
+        # result columns S .. 2S-1 -> X
+        e(f'  v_and_b32_e32 {X(0)}, {hex(MASK)}, {Rlo(S)}')
+        e(f'  v_lshrrev_b64 {tmp}, {B}, {R(S)}')
+        for k in range(1, S):
+            e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {R(S + k)}')
+            e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+            if k != S - 1:
+                e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+
     # LOADX
     e('.Lloadx:')
     slot_addr()
@@ -215,18 +268,26 @@ def gen(S: int, B: int, U: int, name: str) -> str:
     e('  s_mov_b32 s19, 0')      # after the product: back to the dispatcher
     e('  s_branch .Lmontmul')
 
-    # SQR: count in s15
+    # SQR: count in s15.  Fully unrolled Montgomery squaring: a = X is in
+    # registers (no LDS), only the j >= i half of the a*X products is formed
+    # (2 a_i folded into one operand), columns live in S register pairs used
+    # as a ring (column c -> pair c mod S), so there is no window move.
     e('.Lsqr:')
     e('  s_mov_b32 s19, s15')
     e('.Lsqr_loop:')
     e('  s_cmp_eq_u32 s19, 0')
     e('  s_cbranch_scc1 .Lprog')
-    for k in range(S):
-        e(f'  ds_write_b32 v{V_LDSA}, {X(k)} offset:{k * 256}')
-        if k % 8 == 7:
-            e('  s_waitcnt lgkmcnt(0)')
-    e('  s_waitcnt lgkmcnt(0)')
-    e('  s_branch .Lmontmul')
+    if sqr_unrolled:
+        emit_square()
+        e('  s_sub_u32 s19, s19, 1')
+        e('  s_branch .Lsqr_loop')
+    else:
+        for k in range(S):
+            e(f'  ds_write_b32 v{V_LDSA}, {X(k)} offset:{k * 256}')
+            if k % 8 == 7:
+                e('  s_waitcnt lgkmcnt(0)')
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_branch .Lmontmul')
 
     # ---------------- Montgomery product ---------------------------------
     def iteration(u, last_in_block):
