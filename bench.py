@@ -144,9 +144,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    kms, launches, lane_mm, lanes, ems, elaunch = (ctypes.c_double() for _ in range(6))
+    kms, launches, lane_mm, lanes, ems, elaunch, amacs = (ctypes.c_double() for _ in range(7))
     _lib.check(lib.fthe_prof_read(dev.ctx, ctypes.byref(kms), ctypes.byref(launches), ctypes.byref(lane_mm),
-                                  ctypes.byref(lanes), ctypes.byref(ems), ctypes.byref(elaunch)))
+                                  ctypes.byref(lanes), ctypes.byref(ems), ctypes.byref(elaunch),
+                                  ctypes.byref(amacs)))
     lib.fthe_prof_enable(dev.ctx, 0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -155,22 +156,23 @@ def main():
     enc_total = world * 2 * P * a.steps
     value = enc_total / elapsed
 
-    # -- roofline of the dominant kernel (montprog, per-launch HIP events, this rank)
+    # -- roofline of the dominant kernel family (montprog s37 + s74, per-launch HIP
+    # events on the engine stream, this rank).  Algorithmic work = the Montgomery
+    # products the programs perform x W(s) = 2 s^2 + s MACs on s = 32-bit words of
+    # the modulus (SURVEY.md 8(d) unit), accumulated per launch by the engine.
     enc_rank = 2 * P * a.steps
-    alg_macs = enc_rank * ALG_MACS_PER_CRT_ENC
+    alg_macs = amacs.value
     k_s = kms.value * 1e-3
-    S = lib.fthe_kernel_limbs(KEY_BITS)
     achieved = alg_macs / k_s / 1e12
-    issued = lane_mm.value * 2 * S * S / k_s / 1e12
-    roof = {"bound": "valu", "kernel": "fthe_montprog_s74", "achieved": round(achieved, 3),
+    roof = {"bound": "valu", "kernel": "fthe_montprog_s37 + fthe_montprog_s74", "achieved": round(achieved, 3),
             "peak": round(PEAK_MAC_S / 1e12, 3), "unit": "TMAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_S, 4),
             "traffic": None,
             "launches": int(launches.value), "avg_launch_ms": round(kms.value / max(1, launches.value), 3),
             "expo_launches": int(elaunch.value),
             "avg_expo_launch_ms": round(ems.value / max(1, elaunch.value), 3),
-            "alg_macs_per_encrypt": ALG_MACS_PER_CRT_ENC,
-            "issued_v_mad_u64_u32_tmac_s": round(issued, 3),
-            "issued_frac_of_measured_mad_peak": round(issued * 1e12 / MEASURED_MAD_S, 4),
+            "alg_macs_per_encrypt": round(alg_macs / enc_rank),
+            "survey_alg_macs_per_crt_encrypt_direct": ALG_MACS_PER_CRT_ENC,
+            "montmuls_per_encrypt": round(lane_mm.value / enc_rank, 1),
             "kernel_share_of_step": round(k_s / elapsed, 4)}
     prof_hbm = os.path.join(ROOT, "profiles", "r01_montprog_pmc.json")
     if os.path.exists(prof_hbm):

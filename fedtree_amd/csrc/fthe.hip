@@ -96,7 +96,7 @@ struct fthe_ctx {
     hipStream_t stream = nullptr;
     hipModule_t mod[MAX_VARIANTS] = {};
     hipFunction_t fn[MAX_VARIANTS] = {};
-    DevBuf slots, scratch, io[4];
+    DevBuf slots, slots1, scratch, io[4];   // slots1: the small-modulus (mod p, q) programs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_mm = 0;
     bool timed = false;
@@ -106,6 +106,7 @@ struct fthe_ctx {
     std::vector<double> prof_mm;  // products per lane of each recorded launch
     size_t prof_used = 0;
     double prof_lane_mm = 0;      // sum over launches of live lanes x products
+    double prof_alg_macs = 0;     // sum over launches of live lanes x products x W(s), SURVEY 8(d)
     double prof_launch_lanes = 0; // sum over launches of live lanes
 };
 
@@ -113,6 +114,12 @@ struct fthe_ctx {
 struct DevMod {
     MontMod m;
     uint32_t *d_ctx = nullptr;     // N limbs (S) + nprime
+    // SURVEY 8(d) work unit: W(s) = 2 s^2 + s 32x32 MACs per Montgomery
+    // product on s = ceil(bits/32) u32 limbs (algorithmic, kernel-independent)
+    double w_alg() const {
+        double s = (double)((mpz_sizeinbase(m.N, 2) + 31) / 32);
+        return 2 * s * s + s;
+    }
 };
 
 // A named constant (S limbs) on the device.
@@ -122,7 +129,9 @@ struct fthe_key {
     int n_bits = 0, n_words = 0;
     bool priv = false, pub_ok = false;
     Mpz n, n2, g, p, q, lambda, mu;
-    DevMod mn2, mp2, mq2, mp, mq;
+    DevMod mn2, mp2, mq2, mp, mq, mp1, mq1;   // mp1/mq1: mod p, q on the small-limb kernel
+    Shape sp1{0, 0, 0};
+    int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
     int kp = 0, kq = 0;             // limbs of p, q
     // device constants: one allocation, each its modulus' limb count
     std::vector<std::vector<uint32_t>> host_consts;
@@ -134,7 +143,7 @@ struct fthe_key {
     size_t n_words_dev_off = 0;     // offset (in u32) of n words in d_consts
     uint32_t *d_nwords = nullptr;
     ~fthe_key() {
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq}) if (d->d_ctx) hipFree(d->d_ctx);
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1}) if (d->d_ctx) hipFree(d->d_ctx);
         if (d_consts) hipFree(d_consts);
         if (d_progs) hipFree(d_progs);
         if (d_nwords) hipFree(d_nwords);
@@ -164,6 +173,7 @@ struct fthe_key {
     int c_p2 = -1, c_q2 = -1, c_2p2 = -1, c_qinvRp2 = -1;
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_enc_pub, pr_add, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+    PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 };
 
 // slot numbering shared by all programs
@@ -249,12 +259,12 @@ extern "C" double fthe_last_montmuls(fthe_ctx *c) { return c ? c->last_mm : 0.0;
 extern "C" int fthe_prof_enable(fthe_ctx *c, int on) {
     if (!c) return FTHE_ERR_ARG;
     c->prof = on != 0;
-    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0;
+    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0; c->prof_alg_macs = 0;
     return FTHE_OK;
 }
 
 extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, double *lane_montmuls, double *lanes,
-                              double *expo_ms, double *expo_launches) {
+                              double *expo_ms, double *expo_launches, double *alg_macs) {
     if (!c) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipStreamSynchronize(c->stream));
@@ -271,7 +281,8 @@ extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, 
     if (launches) *launches = (double)c->prof_used;
     if (lane_montmuls) *lane_montmuls = c->prof_lane_mm;
     if (lanes) *lanes = c->prof_launch_lanes;
-    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0;
+    if (alg_macs) *alg_macs = c->prof_alg_macs;
+    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0; c->prof_alg_macs = 0; c->prof_alg_macs = 0;
     return FTHE_OK;
 }
 
@@ -351,17 +362,50 @@ static int key_finish(fthe_key *k) {
         k->c_2p2 = k->add_const(L_(t));
         Mpz qi; if (!mpz_invert(qi, q2, p2)) return FTHE_ERR_KEY;
         k->c_qinvRp2 = k->add_const(k->mp2.m.mont(qi));
-        k->w_crt = best_window(std::max(ep.bits(), eq.bits()));
-        k->tabn_max = std::max(k->tabn_max, 1 << (k->w_crt - 1));
-        for (int side = 0; side < 2; side++) {
-            Prog e;
-            e.loadx(SL_IN0); e.mul(side ? SL_C2 : SL_C0);       // r R mod P^2
-            e.pow(side ? eq : ep, SL_TAB, SL_SQ, k->w_crt);       // r^n R
-            e.storex(SL_SAVED);
-            e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);        // m (n mod P^2)
-            e.addsmall(1); e.mul(SL_SAVED);                      // (1 + m n) r^n mod P^2
-            e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
-            (side ? k->pr_enc_q : k->pr_enc_p) = k->add_prog(e);
+        (void)ep; (void)eq;
+        // Two-stage CRT encrypt.  r^n mod P^2 = (r^Q mod P)^P mod P^2 for n = P Q:
+        // x = y (mod P) implies x^P = y^P (mod P^2), and r^Q mod P = r^(Q mod (P-1)) mod P.
+        // Stage A (mod P, small-limb kernel): y = r^(Q mod (P-1)) mod P, 1024-bit exponent
+        // over a 1024-bit modulus; stage B (mod P^2): y^P (1024-bit exponent) then
+        // (1 + m n) y^P.  Same canonical residue as PowerMod(r, n, n^2) (paillier.cpp:136),
+        // 0.62x the products of the direct r^(n mod P(P-1)) mod P^2.
+        {
+            size_t pb = std::max(k->p.bits(), k->q.bits());
+            k->sp1 = kernel_shape_for_bits((int)pb);
+            if (!k->sp1.S) return FTHE_ERR_UNSUPPORTED;
+            if ((rc = upload_mod(k->mp1, k->p, k->sp1))) return rc;
+            if ((rc = upload_mod(k->mq1, k->q, k->sp1))) return rc;
+            const MontMod &A = k->mp1.m, &Bq = k->mq1.m;
+            k->c1_R2p = k->add_const(A.limbs(A.R2));
+            k->c1_R3p = k->add_const(A.limbs(A.R3));
+            k->c1_R2q = k->add_const(Bq.limbs(Bq.R2));
+            k->c1_R3q = k->add_const(Bq.limbs(Bq.R3));
+            k->c1_one = k->add_const(A.limbs(one));
+            Mpz ea, eb;
+            mpz_mod(ea, k->q, pm1);             // Q mod (P-1) for P = p
+            mpz_mod(eb, k->p, qm1);             // and for P = q
+            int wA = best_window(std::max(ea.bits(), eb.bits()));
+            int wB = best_window(std::max(k->p.bits(), k->q.bits()));
+            k->tabn_max = std::max(k->tabn_max, std::max(1 << (wA - 1), 1 << (wB - 1)));
+            for (int side = 0; side < 2; side++) {
+                Prog a;                                          // slots in the small region
+                a.loadx(SL_IN1); a.mul(side ? SL_C3 : SL_C1);    // r_hi R^2
+                a.storex(SL_T0);
+                a.loadx(SL_IN0); a.mul(side ? SL_C2 : SL_C0);    // r_lo R
+                a.addslot(SL_T0);                                // r R mod P
+                a.pow(side ? eb : ea, SL_TAB, SL_SQ, wA);         // r^Q R
+                a.mul(SL_T5);                                    // out of Montgomery (< 2P)
+                a.storex(side ? SL_OUTQ : SL_OUTP); a.end();
+                (side ? k->pr_encA_q : k->pr_encA_p) = k->add_prog(a);
+                Prog e;                                          // slots in the P^2 region
+                e.loadx(side ? SL_T4 : SL_T3); e.mul(side ? SL_C2 : SL_C0);   // y R mod P^2
+                e.pow(side ? k->q : k->p, SL_TAB, SL_SQ, wB);     // y^P R = r^n R
+                e.storex(SL_SAVED);
+                e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);    // m (n mod P^2)
+                e.addsmall(1); e.mul(SL_SAVED);                  // (1 + m n) r^n mod P^2
+                e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+                (side ? k->pr_enc_q : k->pr_enc_p) = k->add_prog(e);
+            }
         }
         {   // h = (cp - cq) (q^2)^-1 mod p^2
             Prog h; h.loadx(SL_T0); h.mul(SL_T1); h.storex(SL_T2); h.end();
@@ -522,9 +566,10 @@ extern "C" int fthe_key_export(const fthe_key *k, uint32_t *n, uint32_t *lambda,
 namespace {
 
 // Launch the montprog kernel, bracketed by profiling events when enabled.
-int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *modctx, double lane_mm, size_t live) {
+int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, const DevMod &mod, double lane_mm,
+                    size_t live) {
     struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
-        c->slots.p, prog, modctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4)};
+        slots, prog, mod.d_ctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4)};
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     int vi = variant_index(S);
@@ -548,6 +593,7 @@ int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *mod
     if (ev) {
         HIPOK(hipEventRecord(ev->second, c->stream));
         c->prof_lane_mm += lane_mm * (double)live;
+        c->prof_alg_macs += lane_mm * (double)live * mod.w_alg();
         c->prof_launch_lanes += (double)live;
     }
     return FTHE_OK;
@@ -555,11 +601,12 @@ int launch_montprog(fthe_ctx *c, int S, int L, const void *prog, const void *mod
 
 struct Launch {
     fthe_ctx *c; const fthe_key *k; int L; int S; int B; double mm = 0; size_t live = 0;
-    uint32_t *slot(int s) const { return (uint32_t *)c->slots.p + (size_t)s * S * L; }
+    void *base = nullptr;          // slot region (c->slots, or c->slots1 for small-modulus programs)
+    uint32_t *slot(int s) const { return (uint32_t *)base + (size_t)s * S * L; }
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
     int prog(const fthe_key::PH &ph, const DevMod &mod) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, S, L, k->prog(ph), mod.d_ctx, ph.mm, live);
+        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live);
         if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;
@@ -580,6 +627,7 @@ int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nsl
     if (L == 0) L = 256;
     Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = sh.S; Lc.B = sh.B;
     int rc = c->slots.ensure((size_t)nslots * sh.S * L * 4);
+    Lc.base = c->slots.p;
     if (rc) return rc;
     HIPOK(hipEventRecord(c->ev0, c->stream));
     return FTHE_OK;
@@ -616,7 +664,14 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
         for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(s); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
         rk.nonce = splitmix64(s);
     }
+    Launch L1 = Lc;                    // stage A: mod p, q on the small-limb kernel, own slot region
     if (crt) {
+        L1.S = k->sp1.S; L1.B = k->sp1.B;
+        if ((rc = c->slots1.ensure((size_t)nslots_for(k) * L1.S * L * 4))) return rc;
+        L1.base = c->slots1.p;
+        L1.fill(SL_C0, k->c1_R2p); L1.fill(SL_C1, k->c1_R3p);
+        L1.fill(SL_C2, k->c1_R2q); L1.fill(SL_C3, k->c1_R3q);
+        L1.fill(SL_T5, k->c1_one);
         Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
         Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_nRq);
         Lc.fill(SL_T1, k->c_qinvRp2);
@@ -625,18 +680,28 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
     }
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
-        Lc.live = cnt;
-        if (r) {
-            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, r + off * r_words, r_words, cnt, 0,
-                               Lc.slot(SL_IN0), S, L, Lc.B);
-        } else {
+        Lc.live = cnt; L1.live = cnt;
+        const uint32_t *rw = r + (r ? off * r_words : 0);
+        int rwn = r_words;
+        if (!r) {
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_nwords, nw, k->n_bits, rk,
                                (uint64_t)off, cnt, (uint32_t *)c->scratch.p);
-            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, (const uint32_t *)c->scratch.p, nw,
-                               cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+            rw = (const uint32_t *)c->scratch.p; rwn = nw;
         }
         hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (crt) {
+            // r (< n) -> low / high halves in the small layout
+            hipLaunchKernelGGL(k_pack_words, L1.grid(), dim3(256), 0, c->stream, rw, rwn, cnt, 0,
+                               L1.slot(SL_IN0), L1.S, L, L1.B);
+            hipLaunchKernelGGL(k_pack_words, L1.grid(), dim3(256), 0, c->stream, rw, rwn, cnt, L1.B * L1.S,
+                               L1.slot(SL_IN1), L1.S, L, L1.B);
+            if ((rc = L1.prog(k->pr_encA_p, k->mp1))) return rc;
+            if ((rc = L1.prog(k->pr_encA_q, k->mq1))) return rc;
+            if (L1.B != Lc.B) return FTHE_ERR_UNSUPPORTED;
+            hipLaunchKernelGGL(k_copy_limbs, Lc.grid(), dim3(256), 0, c->stream, L1.slot(SL_OUTP), L1.S,
+                               Lc.slot(SL_T3), S, L);
+            hipLaunchKernelGGL(k_copy_limbs, Lc.grid(), dim3(256), 0, c->stream, L1.slot(SL_OUTQ), L1.S,
+                               Lc.slot(SL_T4), S, L);
             if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;
             if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
             hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
@@ -647,10 +712,13 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
             hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
                                k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else {
+            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, rw, rwn, cnt, 0,
+                               Lc.slot(SL_IN0), S, L, Lc.B);
             if ((rc = Lc.prog(k->pr_enc_pub, k->mn2))) return rc;
             hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
                                S, L, cnt, out + off * cw, cw, Lc.B);
         }
+        Lc.mm += L1.mm; L1.mm = 0;
     }
     return end_call(c, Lc);
 }
@@ -737,7 +805,7 @@ namespace {
 // Launch with an explicit (dynamic) program pointer.
 int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod) {
     if (mod.m.S != Lc.S) return FTHE_ERR_ARG;
-    int rc = launch_montprog(Lc.c, Lc.S, Lc.L, prog, mod.d_ctx, mm, Lc.live);
+    int rc = launch_montprog(Lc.c, Lc.base, Lc.S, Lc.L, prog, mod, mm, Lc.live);
     if (rc) return rc;
     Lc.mm += mm * (double)Lc.live;
     return FTHE_OK;

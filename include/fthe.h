@@ -150,11 +150,14 @@ double fthe_last_montmuls(fthe_ctx *ctx);
  *   lane_montmuls  sum over launches of (live lanes x Montgomery products)
  *   lanes          sum over launches of live lanes
  *   expo_ms/_launches  the same restricted to exponentiation launches
- *                  (programs of >= 64 products per lane) */
+ *                  (programs of >= 64 products per lane)
+ *   alg_macs       algorithmic work of those launches: live lanes x products x
+ *                  W(s), W(s) = 2 s^2 + s with s = 32-bit words of the modulus
+ *                   -- independent of the kernel's radix */
 int    fthe_prof_enable(fthe_ctx *ctx, int on);
 int    fthe_prof_read(fthe_ctx *ctx, double *kernel_ms, double *launches,
                       double *lane_montmuls, double *lanes,
-                      double *expo_ms, double *expo_launches);
+                      double *expo_ms, double *expo_launches, double *alg_macs);
 /* limb count S of the radix-2^28 kernel used for a modulus of `bits` bits
  * (0 if unsupported). */
 int    fthe_kernel_limbs(int bits);
