@@ -191,19 +191,25 @@ def main():
         secondary["crt_decrypt_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
         ok = torch.equal(low, m[:nd])
         secondary["decrypt_roundtrip_ok"] = bool(ok)
-        # ciphertext adds: P-1024 (n^2 = 2048-bit) on the same kernel; P-2048 adds
-        # need the 4096-bit modulus kernel (not built in round 1)
-        p1 = Paillier(dev).keygen(1024, seed=SEED)
-        na = 1 << 20
-        x = torch.randint(0, 2**31, (na, 2 * p1.n_words), dtype=torch.int32, device=f"cuda:{local}")
-        x[:, -1] = 0
-        y = x.flip(0).contiguous()
-        o = torch.empty_like(x)
-        p1.add_dev(x, y, o)
-        p1.add_dev(x, y, o)
+        # ciphertext adds (x*y mod n^2, 4096-bit n^2 on the four-lane kernel), device-resident
+        na = min(2 * P, 1 << 20)
+        o = torch.empty((na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+        pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
+        pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
         dev.sync()
-        secondary["p1024_add_per_s"] = round(na / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
-        secondary["p2048_add_per_s"] = None
+        secondary["p2048_add_per_s"] = round(na / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        del o
+        # configs[3]: 8-party merge of 256 x 4096 bins x {g, h} (hist_tree_builder.cpp:1015-1058)
+        bins, parties = 2 * 256 * 4096, 8
+        if 2 * P >= bins:
+            x = c[:bins].unsqueeze(0).expand(parties, bins, 2 * pl.n_words).contiguous()
+            ho = torch.empty((bins, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+            pl.reduce_kway_dev(x, parties, ho)
+            dev.sync()
+            ms_h = lib.fthe_last_kernel_ms(dev.ctx)
+            secondary["hist_merge_8party_1M_bins"] = {"ms": round(ms_h, 2), "ciphertexts_out": bins,
+                                                      "adds_per_s": round(bins * (parties - 1) / (ms_h * 1e-3))}
+            del x, ho
         # end to end, host-resident in/out (pageable H2D of m, D2H of 512-B ciphertexts)
         ne = min(2 * P, 1 << 20)
         mh = m[:ne].cpu().numpy().view(np.uint64).copy()

@@ -34,30 +34,40 @@ def trace(db, out):
 
 
 def pmc(dirs, out):
+    """Per montprog variant: counters of its exponentiation dispatches (those whose
+    value is >= 25% of the variant's largest, i.e. not the 1-product launches)."""
     agg = {}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if not r.get("Kernel_Name", "").startswith("fthe_montprog"):
+                kn = r.get("Kernel_Name", "")
+                if not kn.startswith("fthe_montprog"):
                     continue
-                key = (r["Dispatch_Id"], r["Counter_Name"])
+                key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                 agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
     per = {}
-    for (disp, name), v in agg.items():
-        per.setdefault(name, []).append(v)
+    for (kn, disp, name), v in agg.items():
+        per.setdefault(kn, {}).setdefault(name, []).append(v)
     res = {}
-    for name, v in per.items():
-        v = sorted(v, reverse=True)
-        heavy = [x for x in v if x >= 0.25 * v[0]]     # exponentiation launches dominate every counter
-        res[name] = {"dispatches": len(v), "expo_dispatches": len(heavy),
-                     "expo_mean": sum(heavy) / len(heavy), "all_mean": sum(v) / len(v)}
-    if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
-        # FETCH_SIZE/WRITE_SIZE are KB; gfx950 FETCH_SIZE reads 1/2 of a coalesced
-        # stream (MI355X_MICROARCH.md HBM): calibrated on this kernel -- the loads
-        # the program issues (329 x 296 B per lane per launch) are 2.05x FETCH_SIZE.
-        f, w = res["FETCH_SIZE"]["expo_mean"], res["WRITE_SIZE"]["expo_mean"]
-        res["hbm_bytes_per_launch"] = (2 * f + w) * 1024
-        res["hbm_bytes_formula"] = "(2*FETCH_SIZE + WRITE_SIZE) * 1024, exponentiation launches"
+    for kn, counters in per.items():
+        rk = {}
+        for name, v in counters.items():
+            v = sorted(v, reverse=True)
+            heavy = [x for x in v if x >= 0.25 * v[0]] if v[0] > 0 else v
+            rk[name] = {"dispatches": len(v), "expo_dispatches": len(heavy),
+                        "expo_mean": sum(heavy) / len(heavy), "all_mean": sum(v) / len(v)}
+        if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
+            # FETCH_SIZE/WRITE_SIZE are KB; gfx950 FETCH_SIZE reads 1/2 of a coalesced
+            # stream (MI355X_MICROARCH.md HBM): calibrated on this kernel in round 1 --
+            # the 329 x 296-B slot loads per lane per launch it issues = 2.05 x FETCH_SIZE.
+            f, w = rk["FETCH_SIZE"]["expo_mean"], rk["WRITE_SIZE"]["expo_mean"]
+            rk["hbm_bytes_per_launch"] = (2 * f + w) * 1024
+            rk["hbm_bytes_formula"] = "(2*FETCH_SIZE + WRITE_SIZE) * 1024, exponentiation launches"
+        res[kn] = rk
+    dom = "fthe_montprog_s74"
+    if dom in res and "hbm_bytes_per_launch" in res[dom]:
+        res["hbm_bytes_per_launch"] = res[dom]["hbm_bytes_per_launch"]
+        res["dominant_kernel"] = dom
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
