@@ -170,10 +170,16 @@ def main():
             "launches": int(launches.value), "avg_launch_ms": round(kms.value / max(1, launches.value), 3),
             "expo_launches": int(elaunch.value),
             "avg_expo_launch_ms": round(ems.value / max(1, elaunch.value), 3),
+            "avg_expo_launch_ms_by_kernel": {},
             "alg_macs_per_encrypt": round(alg_macs / enc_rank),
             "survey_alg_macs_per_crt_encrypt_direct": ALG_MACS_PER_CRT_ENC,
             "montmuls_per_encrypt": round(lane_mm.value / enc_rank, 1),
             "kernel_share_of_step": round(k_s / elapsed, 4)}
+    for S in (37, 74, 152):
+        vms, vn = ctypes.c_double(), ctypes.c_double()
+        lib.fthe_prof_variant(dev.ctx, S, ctypes.byref(vms), ctypes.byref(vn))
+        if vn.value:
+            roof["avg_expo_launch_ms_by_kernel"][f"fthe_montprog_s{S}"] = round(vms.value / vn.value, 3)
     prof_hbm = os.path.join(ROOT, "profiles", "r01_montprog_pmc.json")
     if os.path.exists(prof_hbm):
         try:

@@ -69,6 +69,7 @@ _PROTOS = {
     "fthe_last_montmuls": (ctypes.c_double, [_P]),
     "fthe_kernel_limbs": (_I, [_I]),
     "fthe_prof_enable": (_I, [_P, _I]),
+    "fthe_prof_variant": (_I, [_P, _I, _P, _P]),
     "fthe_prof_read": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
 }
 

@@ -104,6 +104,8 @@ struct fthe_ctx {
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
     std::vector<double> prof_mm;  // products per lane of each recorded launch
+    std::vector<int> prof_vi;     // kernel variant of each recorded launch
+    double var_ms[MAX_VARIANTS] = {}, var_n[MAX_VARIANTS] = {};   // last read, exponentiation launches
     size_t prof_used = 0;
     double prof_lane_mm = 0;      // sum over launches of live lanes x products
     double prof_alg_macs = 0;     // sum over launches of live lanes x products x W(s), SURVEY 8(d)
@@ -256,6 +258,15 @@ extern "C" double fthe_last_kernel_ms(fthe_ctx *c) {
 }
 extern "C" double fthe_last_montmuls(fthe_ctx *c) { return c ? c->last_mm : 0.0; }
 
+extern "C" int fthe_prof_variant(fthe_ctx *c, int S, double *expo_ms, double *expo_launches) {
+    if (!c) return FTHE_ERR_ARG;
+    int vi = variant_index(S);
+    if (vi < 0) return FTHE_ERR_ARG;
+    if (expo_ms) *expo_ms = c->var_ms[vi];
+    if (expo_launches) *expo_launches = c->var_n[vi];
+    return FTHE_OK;
+}
+
 extern "C" int fthe_prof_enable(fthe_ctx *c, int on) {
     if (!c) return FTHE_ERR_ARG;
     c->prof = on != 0;
@@ -269,11 +280,15 @@ extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, 
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipStreamSynchronize(c->stream));
     double tot = 0, etot = 0, en = 0;
+    for (int v = 0; v < MAX_VARIANTS; v++) c->var_ms[v] = c->var_n[v] = 0;
     for (size_t i = 0; i < c->prof_used; i++) {
         float ms = 0;
         HIPOK(hipEventElapsedTime(&ms, c->prof_ev[i].first, c->prof_ev[i].second));
         tot += ms;
-        if (c->prof_mm[i] >= 64) { etot += ms; en += 1; }   // exponentiation launches
+        if (c->prof_mm[i] >= 64) {                            // exponentiation launches
+            etot += ms; en += 1;
+            c->var_ms[c->prof_vi[i]] += ms; c->var_n[c->prof_vi[i]] += 1;
+        }
     }
     if (kernel_ms) *kernel_ms = tot;
     if (expo_ms) *expo_ms = etot;
@@ -584,7 +599,9 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
             c->prof_ev.push_back(e);
         }
         if (c->prof_mm.size() < c->prof_ev.size()) c->prof_mm.resize(c->prof_ev.size());
+        if (c->prof_vi.size() < c->prof_ev.size()) c->prof_vi.resize(c->prof_ev.size());
         c->prof_mm[c->prof_used] = lane_mm;
+        c->prof_vi[c->prof_used] = vi;
         ev = &c->prof_ev[c->prof_used++];
         HIPOK(hipEventRecord(ev->first, c->stream));
     }

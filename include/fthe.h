@@ -158,6 +158,9 @@ int    fthe_prof_enable(fthe_ctx *ctx, int on);
 int    fthe_prof_read(fthe_ctx *ctx, double *kernel_ms, double *launches,
                       double *lane_montmuls, double *lanes,
                       double *expo_ms, double *expo_launches, double *alg_macs);
+/* Per kernel variant (limb count S: 37, 74, 152) exponentiation-launch time and
+ * count of the last fthe_prof_read window. */
+int    fthe_prof_variant(fthe_ctx *ctx, int S, double *expo_ms, double *expo_launches);
 /* limb count S of the radix-2^28 kernel used for a modulus of `bits` bits
  * (0 if unsupported). */
 int    fthe_kernel_limbs(int bits);

@@ -13,6 +13,32 @@ import sqlite3
 import sys
 
 
+def trace_csv(csvfile, out):
+    """kernel_trace.csv of rocprofv3 --output-format csv: per-kernel stats plus the
+    exponentiation launches (> 5 ms) of each montprog variant."""
+    rows = list(csv.DictReader(open(csvfile)))
+    per = {}
+    for r in rows:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        per.setdefault(r["Kernel_Name"], []).append(d)
+    lines = ["kernel,calls,total_ms,avg_ms"]
+    for name, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        lines.append(f"{name[:90]},{len(v)},{sum(v) / 1e6:.3f},{sum(v) / len(v) / 1e6:.4f}")
+    lines.append("")
+    for name, v in sorted(per.items()):
+        if name.startswith("fthe_montprog"):
+            heavy = [d for d in v if d > 5e6]
+            if heavy:
+                lines.append(f"{name} exponentiation launches (>5 ms): n={len(heavy)} "
+                             f"avg_ms={sum(heavy) / len(heavy) / 1e6:.3f} min_ms={min(heavy) / 1e6:.3f} "
+                             f"max_ms={max(heavy) / 1e6:.3f}")
+                top = [d for d in heavy if d >= 0.9 * max(heavy)]   # the dominant (encrypt) launch type
+                lines.append(f"{name} launches within 10% of the longest (encrypt programs): n={len(top)} "
+                             f"avg_ms={sum(top) / len(top) / 1e6:.3f}")
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[-4:]))
+
+
 def trace(db, out):
     cur = sqlite3.connect(db).cursor()
     lines = ["kernel,calls,total_ms,avg_ms,pct"]
@@ -74,6 +100,6 @@ def pmc(dirs, out):
 
 if __name__ == "__main__":
     if sys.argv[1] == "trace":
-        trace(sys.argv[2], sys.argv[3])
+        (trace_csv if sys.argv[2].endswith(".csv") else trace)(sys.argv[2], sys.argv[3])
     else:
         pmc(sys.argv[2:-1], sys.argv[-1])
