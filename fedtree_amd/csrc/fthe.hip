@@ -96,7 +96,7 @@ struct fthe_ctx {
     hipStream_t stream = nullptr;
     hipModule_t mod[MAX_VARIANTS] = {};
     hipFunction_t fn[MAX_VARIANTS] = {};
-    DevBuf slots, slots1, scratch, io[4];   // slots1: the small-modulus (mod p, q) programs
+    DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_mm = 0;
     bool timed = false;
@@ -866,6 +866,115 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
                            cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
+}
+
+// Segmented product: out[s] = prod_{t in [seg_ptr[s], seg_ptr[s+1])} x[idx ? idx[t] : t]
+// mod n^2 (an empty segment gives 1).  Histogram scatter by bin id
+// (hist_tree_builder.cpp:565-595: hist[bin] = hist[bin] + gh[iid]), root sums
+// (tree.cpp:20-34) and node sums.  Passes of K-way products over groups of <= K
+// consecutive members of a segment (gathered per lane), until one element per
+// segment remains.  seg_ptr / idx are host arrays; x and out device pointers.
+extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
+                                        const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out) {
+    if (!k || !c || !seg_ptr || (nseg && !out)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (seg_ptr[0] != 0) return FTHE_ERR_ARG;
+    for (size_t s = 0; s < nseg; s++) if (seg_ptr[s + 1] < seg_ptr[s]) return FTHE_ERR_ARG;
+    size_t total = (size_t)seg_ptr[nseg];
+    if (idx) for (size_t t = 0; t < total; t++) if (idx[t] < 0 || (size_t)idx[t] >= count) return FTHE_ERR_ARG;
+    if (!idx && total > count) return FTHE_ERR_ARG;
+    if (!nseg) return FTHE_OK;
+    const int K = 8;
+    const int base = nslots_for(k);
+    // pass plan on the host: members of every segment, groups of <= K
+    std::vector<std::vector<int64_t>> members(nseg);
+    for (size_t s = 0; s < nseg; s++)
+        for (int64_t t = seg_ptr[s]; t < seg_ptr[s + 1]; t++) members[s].push_back(idx ? idx[t] : t);
+    const int cw = 2 * k->n_words;
+    size_t maxg = 0;
+    for (auto &m : members) maxg += std::max<size_t>(1, (m.size() + K - 1) / K);
+    int rc;
+    if ((rc = c->io[2].ensure(maxg * cw * 4)) || (rc = c->io[1].ensure(maxg * cw * 4))) return rc;
+    Launch Lc;
+    if ((rc = begin_call(c, k, maxg, Lc, base + K, k->sn2))) return rc;
+    const int S = Lc.S, L = Lc.L;
+    // program: X = x0; X <- x_j X R^-1; X <- X (R^K) R^-1
+    Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)K, k->n2);
+    std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
+    Prog p;
+    p.loadx(base);
+    for (int j = 1; j < K; j++) p.mul(base + j);
+    p.mul(SL_C0);
+    p.storex(SL_OUTP); p.end();
+    std::vector<uint32_t> blob(p.w);
+    size_t prog_words = blob.size();
+    blob.insert(blob.end(), rl.begin(), rl.end());
+    fthe_key::PH ph;
+    Prog tmp; tmp.w = blob; tmp.montmuls = p.montmuls;
+    if ((rc = upload_dyn_prog(c, tmp, ph, c->io[3]))) return rc;
+    HIPOK(hipEventRecord(c->ev0, c->stream));
+    hipLaunchKernelGGL(k_fill_const, Lc.grid(), dim3(256), 0, c->stream,
+                       (const uint32_t *)c->io[3].p + prog_words, Lc.slot(SL_C0), S, L);
+    const uint32_t *src = x;
+    int bufsel = 1;
+    std::vector<int64_t> gidx;
+    while (true) {
+        // groups of this pass
+        size_t G = 0;
+        for (auto &m : members) G += std::max<size_t>(1, (m.size() + K - 1) / K);
+        gidx.assign((size_t)K * G, -1);
+        std::vector<std::vector<int64_t>> next(nseg);
+        size_t g = 0;
+        bool done_after = true;
+        for (size_t s = 0; s < nseg; s++) {
+            size_t ng = std::max<size_t>(1, (members[s].size() + K - 1) / K);
+            for (size_t q = 0; q < ng; q++, g++) {
+                for (int j = 0; j < K; j++) {
+                    size_t t = q * K + j;
+                    if (t < members[s].size()) gidx[(size_t)j * G + g] = members[s][t];
+                }
+                next[s].push_back((int64_t)g);
+            }
+            if (ng > 1) done_after = false;
+        }
+        HIPOK(hipStreamSynchronize(c->stream));          // previous pass done with scratch
+        if ((rc = c->scratch.ensure(gidx.size() * 8))) return rc;
+        HIPOK(hipMemcpy(c->scratch.p, gidx.data(), gidx.size() * 8, hipMemcpyHostToDevice));
+        uint32_t *dst = done_after ? out : (uint32_t *)c->io[bufsel].p;
+        for (size_t off = 0; off < G; off += L) {
+            size_t cnt = std::min((size_t)L, G - off);
+            Lc.live = cnt;
+            for (int j = 0; j < K; j++)
+                hipLaunchKernelGGL(k_pack_gather, Lc.grid(), dim3(256), 0, c->stream, src, cw,
+                                   (const int64_t *)c->scratch.p + (size_t)j * G + off, cnt, Lc.slot(base + j), S, L,
+                                   Lc.B);
+            if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
+            hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
+                               S, L, cnt, dst + off * cw, cw, Lc.B);
+        }
+        if (done_after) break;
+        members.swap(next);
+        src = dst;
+        bufsel = 3 - bufsel;       // ping-pong io[1] / io[2]
+    }
+    return end_call(c, Lc);
+}
+
+extern "C" int fthe_reduce_segments(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
+                                    const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out) {
+    if (!k || !c || !seg_ptr) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    size_t cw = 2 * (size_t)k->n_words;
+    int rc;
+    // x staged in io[0], out in io[4]; io[1] / io[2] are the pass buffers, io[3] the program
+    if ((rc = c->io[0].ensure(std::max<size_t>(1, count) * cw * 4))) return rc;
+    if (count) HIPOK(hipMemcpyAsync(c->io[0].p, x, count * cw * 4, hipMemcpyHostToDevice, c->stream));
+    if ((rc = c->io[4].ensure(std::max<size_t>(1, nseg) * cw * 4))) return rc;
+    if ((rc = fthe_reduce_segments_dev(k, c, (const uint32_t *)c->io[0].p, count, seg_ptr, idx, nseg,
+                                       (uint32_t *)c->io[4].p))) return rc;
+    if (nseg) HIPOK(hipMemcpyAsync(out, c->io[4].p, nseg * cw * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    return FTHE_OK;
 }
 
 // out[i] = x[i]^e mod n^2 (Paillier::mul, paillier.cpp:118), e uniform.

@@ -8,6 +8,7 @@ namespace fthe {
 struct RngKey { uint32_t k[8]; uint64_t nonce; };
 
 __global__ void k_pack_words(const uint32_t *in, int win, size_t count, int bit0, uint32_t *slot, int S, int L, int rb);
+__global__ void k_pack_gather(const uint32_t *in, int win, const int64_t *idx, size_t count, uint32_t *slot, int S, int L, int rb);
 __global__ void k_pack_u64(const uint64_t *m, size_t count, uint32_t *slot, int S, int L, int rb);
 __global__ void k_copy_limbs(const uint32_t *src, int Ssrc, uint32_t *dst, int Sdst, int L);
 __global__ void k_fill_const(const uint32_t *limbs, uint32_t *slot, int S, int L);

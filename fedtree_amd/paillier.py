@@ -222,6 +222,18 @@ class Paillier:
         _lib.check(self.lib.fthe_reduce_kway(self._key, self.dev.ctx, _ptr(x), k, cnt, _ptr(out)), "reduce_kway")
         return out
 
+    def reduce_segments(self, x, seg_ptr, idx=None):
+        """out[s] = prod x[idx[t]] over t in [seg_ptr[s], seg_ptr[s+1]) mod n^2
+        (histogram scatter hist_tree_builder.cpp:565-595, root sum tree.cpp:20-34).
+        Empty segments give 1."""
+        x = np.ascontiguousarray(x, dtype=np.uint32).reshape(-1, self._cw())
+        seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
+        ix = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        out = np.zeros((len(seg) - 1, self._cw()), dtype=np.uint32)
+        _lib.check(self.lib.fthe_reduce_segments(self._key, self.dev.ctx, _ptr(x), len(x), _ptr(seg), _ptr(ix),
+                                                 len(seg) - 1, _ptr(out)), "reduce_segments")
+        return out
+
     def scalar_mul(self, x, k):
         """x^k mod n^2 (paillier.cpp:118), k < 2^64."""
         x = np.ascontiguousarray(x, dtype=np.uint32).reshape(-1, self._cw())
@@ -257,6 +269,16 @@ class Paillier:
         cnt = out.numel() // self._cw()
         _lib.check(self.lib.fthe_reduce_kway_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), int(k),
                                                  cnt, ctypes.c_void_p(out.data_ptr())), "reduce_kway_dev")
+        return out
+
+    def reduce_segments_dev(self, x, seg_ptr, out, idx=None):
+        """Device tensors x (count, 2nw) and out (nseg, 2nw); host seg_ptr / idx."""
+        seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
+        ix = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        cnt = x.numel() // self._cw()
+        _lib.check(self.lib.fthe_reduce_segments_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), cnt,
+                                                     _ptr(seg), _ptr(ix), len(seg) - 1,
+                                                     ctypes.c_void_p(out.data_ptr())), "reduce_segments_dev")
         return out
 
     # ---- reference single-value signatures (batch of one) ------------------
@@ -359,6 +381,28 @@ class GHPairs:
         return (self if self.encrypted else self._enc_side(pl)) + neg
 
 
+def histogram_segments(bin_ids, cut_col_ptr, max_num_bin):
+    """CSR form of the histogram scatter of hist_tree_builder.cpp:574-595:
+    segment b (= cut_col_ptr[fid] + bid) lists, in the reference's accumulation
+    order (instance order), the instances whose feature fid falls in bin bid;
+    bid == max_num_bin (missing value) is skipped.
+    bin_ids: uint8 (n_instances * n_columns), row-major by instance."""
+    cut = np.asarray(cut_col_ptr, dtype=np.int64)
+    n_col = len(cut) - 1
+    b = np.asarray(bin_ids, dtype=np.int64).reshape(-1, n_col)
+    n_inst = b.shape[0]
+    valid = b != int(max_num_bin)
+    key = b + cut[None, :-1]
+    iid = np.broadcast_to(np.arange(n_inst, dtype=np.int64)[:, None], b.shape)
+    key, iid = key[valid], iid[valid]
+    order = np.argsort(key, kind="stable")      # stable: instance order inside a bin
+    n_bins = int(cut[-1])
+    counts = np.bincount(key, minlength=n_bins)[:n_bins]
+    seg_ptr = np.zeros(n_bins + 1, dtype=np.int64)
+    np.cumsum(counts, out=seg_ptr[1:])
+    return seg_ptr, iid[order]
+
+
 class HEServer:
     """Server HE members (server.h:47-135)."""
 
@@ -395,3 +439,33 @@ class HEParty:
     def encrypt_histogram(self, hist, seed=0):
         """party.h:118-142."""
         return hist.homo_encrypt(self.paillier, seed=seed)
+
+    def compute_histogram(self, gh, bin_ids, cut_col_ptr, max_num_bin):
+        """Histogram of one node (hist_tree_builder.cpp:565-595, n_nodes_in_level == 1):
+        hist[cut_col_ptr[fid] + bid] = sum of gh[iid] over the instances in that bin.
+
+        Encrypted gh: one segmented product on the device for g and h together.
+        Bins without instances stay unencrypted zero, as in the reference; a
+        populated bin is the product of its members (the reference's first add
+        also folds in a fresh Enc(0) from promoting the zero accumulator,
+        common.h:156-160 -- same plaintext, different randomness).
+        Plain gh: float32 accumulation in instance order (dest.g += src.g)."""
+        seg_ptr, idx = histogram_segments(bin_ids, cut_col_ptr, max_num_bin)
+        n_bins = len(seg_ptr) - 1
+        if not gh.encrypted:
+            key = np.repeat(np.arange(n_bins), np.diff(seg_ptr))
+            hist = GHPairs(np.zeros(n_bins, np.float32), np.zeros(n_bins, np.float32))
+            np.add.at(hist.g, key, gh.g[idx])
+            np.add.at(hist.h, key, gh.h[idx])
+            return hist
+        pl = gh.paillier
+        n = len(gh)
+        both = np.concatenate([gh.g_enc, gh.h_enc])
+        seg2 = np.concatenate([seg_ptr, seg_ptr[1:] + seg_ptr[-1]])
+        idx2 = np.concatenate([idx, idx + n])
+        prod = pl.reduce_segments(both, seg2, idx2)
+        hist = GHPairs(np.zeros(n_bins, np.float32), np.zeros(n_bins, np.float32), pl)
+        hist.g_enc, hist.h_enc = prod[:n_bins], prod[n_bins:]
+        hist.encrypted = True
+        hist.bin_encrypted = np.diff(seg_ptr) > 0
+        return hist

@@ -134,6 +134,18 @@ int fthe_reduce_kway_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, int k,
 int fthe_reduce_kway(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, int k,
                      size_t count, uint32_t *out);
 
+/* ---- segmented product ----------------------------------------------------
+ * out[s] = prod_{t in [seg_ptr[s], seg_ptr[s+1])} x[idx ? idx[t] : t] mod n^2.
+ * The histogram scatter of hist_tree_builder.cpp:565-595 (hist[bin] += gh[iid],
+ * segments = the instances of each (feature, bin)), root / node sums
+ * (tree.cpp:20-34, tree_builder.cpp:268-274).  An empty segment yields 1 (the
+ * reference keeps an unencrypted zero GHPair there).  seg_ptr (nseg+1 entries)
+ * and idx are HOST arrays; x / out are device (_dev) or host pointers. */
+int fthe_reduce_segments_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count,
+                             const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out);
+int fthe_reduce_segments(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count,
+                         const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out);
+
 /* ---- fixed-point codec (common.h:81-86,127-128,140-143) ------------------- */
 int fthe_encode_fixed_dev(fthe_ctx *ctx, const float *x, size_t count, uint64_t *m);
 int fthe_decode_fixed_dev(fthe_ctx *ctx, const uint64_t *m, size_t count, float *x);

@@ -58,6 +58,41 @@ def mul(key, x, y):
     return pow(x, y, key["n2"])
 
 
+def segment_product(key, cts, seg_ptr, idx=None):
+    """Products of ciphertext segments (the add of paillier.cpp:103 folded over
+    each segment, in member order).  An empty segment gives 1."""
+    out = []
+    for s in range(len(seg_ptr) - 1):
+        acc = 1
+        for t in range(seg_ptr[s], seg_ptr[s + 1]):
+            acc = add(key, acc, cts[idx[t] if idx is not None else t])
+        out.append(acc)
+    return out
+
+
+def histogram(key, gh_cts, bin_ids, cut_col_ptr, max_num_bin, enc_zero=None):
+    """hist_tree_builder.cpp:574-595 (single node in level): for each feature
+    fid and instance iid with bid = dense_bin_id[iid*n_col + fid] != max_num_bin,
+    hist[cut_col_ptr[fid] + bid] = hist[...] + gh[iid].  Ciphertexts only (one
+    of g or h); the first add promotes the unencrypted zero with
+    Enc(0) (common.h:156-160) -- `enc_zero` stands for that fresh encryption
+    (None: the multiplicative identity).  Untouched bins are None
+    (unencrypted zero)."""
+    n_col = len(cut_col_ptr) - 1
+    n_inst = len(bin_ids) // n_col
+    hist = [None] * cut_col_ptr[-1]
+    for fid in range(n_col):
+        for iid in range(n_inst):
+            bid = int(bin_ids[iid * n_col + fid])
+            if bid == max_num_bin:
+                continue
+            b = cut_col_ptr[fid] + bid
+            if hist[b] is None:
+                hist[b] = 1 if enc_zero is None else enc_zero
+            hist[b] = add(key, hist[b], gh_cts[iid])
+    return hist
+
+
 def encode_fixed(x):
     """common.h:81-86 / :127: (uint64)(int64)((double)x * 1e6), truncating."""
     v = np.trunc(np.asarray(x, dtype=np.float32).astype(np.float64) * 1e6).astype(np.int64)

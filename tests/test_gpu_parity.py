@@ -307,3 +307,84 @@ def test_sharded_two_contexts(dev, coracle):
     assert np.array_equal(pl.decrypt_u64(c), m)
     s = sp.add_batch(c, c[::-1].copy())
     assert np.array_equal(s, pl.add_batch(c, c[::-1].copy()))
+
+
+# ---------------------------------------------------------------- segmented product / histogram
+@pytest.mark.parametrize("nbits", [1024, 2048])
+def test_reduce_segments_vs_oracle(dev, coracle, nbits):
+    """Ragged segments (empty, singletons, one multi-pass segment of 700), a
+    gather index with repeats, bit-exact against the oracle's fold of add."""
+    pw, qw = _det_primes(coracle, nbits, 31 + nbits)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    key = pyoracle.keygen_from_primes(pl.p, pl.q)
+    rng = np.random.default_rng(nbits)
+    cnt = 1200
+    m = rng.integers(0, 2**50, cnt, dtype=np.uint64)
+    c = pl.encrypt_u64(m, seed=5)
+    lens = np.concatenate([[0, 1, 0, 700, 9, 8, 17, 64, 65, 1], rng.integers(0, 20, 50)])
+    seg_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    idx = rng.integers(0, cnt, seg_ptr[-1]).astype(np.int64)
+    got = pl.reduce_segments(c, seg_ptr, idx)
+    cts = pyoracle.words_to_ints(c)
+    want = pyoracle.segment_product(key, cts, list(seg_ptr), list(idx))
+    assert [pyoracle.from_words(x) for x in got] == want
+    sums = [int(m[idx[seg_ptr[s]:seg_ptr[s + 1]]].sum(dtype=np.uint64)) for s in range(len(lens))]
+    assert [int(x) for x in pl.decrypt_u64(got)] == sums
+    # contiguous form (idx = None) == the identity gather
+    seg_c = np.array([0, 3, 3, 600, cnt], np.int64)
+    got_c = pl.reduce_segments(c, seg_c)
+    assert [pyoracle.from_words(x) for x in got_c] == pyoracle.segment_product(key, cts, list(seg_c))
+
+
+def test_reduce_segments_root_sum_full_size(dev, coracle):
+    """Root sum of 300,000 ciphertexts (tree.cpp:20-34): one segment, several
+    passes and chunks; property check through decryption."""
+    pw, qw = _det_primes(coracle, 2048, 41)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    cnt = 300000
+    m = np.random.default_rng(7).integers(0, 2**62, cnt, dtype=np.uint64)
+    import torch
+    tm = torch.from_numpy(m.view(np.int64)).cuda()
+    c = torch.empty((cnt, 2 * pl.n_words), dtype=torch.int32, device="cuda")
+    pl.encrypt_u64_dev(tm, c, seed=9)
+    out = torch.empty((2, 2 * pl.n_words), dtype=torch.int32, device="cuda")
+    seg = np.array([0, cnt, cnt + 3], np.int64)
+    idx = np.concatenate([np.arange(cnt), [5, 5, 5]]).astype(np.int64)
+    pl.reduce_segments_dev(c, seg, out, idx=idx)
+    pl.dev.sync()
+    low = pl.decrypt_u64(out.cpu().numpy().view(np.uint32))
+    assert int(low[0]) == int(m.sum(dtype=np.uint64))
+    assert int(low[1]) == int(m[5] * np.uint64(3))
+
+
+def test_histogram_vs_reference_loop(dev, coracle):
+    """HEParty.compute_histogram against the oracle's restatement of
+    hist_tree_builder.cpp:574-595 (g and h), then decrypt."""
+    from fedtree_amd.paillier import GHPairs, HEParty
+    pw, qw = _det_primes(coracle, 1024, 51)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    key = pyoracle.keygen_from_primes(pl.p, pl.q)
+    rng = np.random.default_rng(3)
+    n_inst, n_col, max_bin = 500, 5, 32
+    per = rng.integers(1, max_bin + 1, n_col)
+    cut = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    bins = np.stack([np.where(rng.random(n_inst) < 0.05, max_bin, rng.integers(0, per[f], n_inst))
+                     for f in range(n_col)], 1).astype(np.uint8)
+    g0 = rng.standard_normal(n_inst).astype(np.float32)
+    h0 = rng.random(n_inst).astype(np.float32)
+    gh = GHPairs(g0, h0)
+    gh.homo_encrypt(pl, seed=4)
+    hist = HEParty(pl).compute_histogram(gh, bins.reshape(-1), cut, max_bin)
+    for enc, name in ((gh.g_enc, "g"), (gh.h_enc, "h")):
+        want = pyoracle.histogram(key, pyoracle.words_to_ints(enc), bins.reshape(-1), list(cut), max_bin)
+        got = hist.g_enc if name == "g" else hist.h_enc
+        assert [pyoracle.from_words(x) for x in got] == [1 if w is None else w for w in want]
+    assert np.array_equal(hist.bin_encrypted, [w is not None for w in want])
+    # decrypted bins == decode(sum mod 2^64 of the encoded members)
+    from fedtree_amd.paillier import decode_fixed, encode_fixed, histogram_segments
+    seg_ptr, idx = histogram_segments(bins.reshape(-1), cut, max_bin)
+    hist.homo_decrypt(pl)
+    for arr, x0 in ((hist.g, g0), (hist.h, h0)):
+        e = encode_fixed(x0)
+        want = [e[idx[seg_ptr[b]:seg_ptr[b + 1]]].sum(dtype=np.uint64) for b in range(cut[-1])]
+        assert np.array_equal(arr, decode_fixed(np.array(want, np.uint64)))

@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hist-bins", type=int, default=256 * 4096)
     ap.add_argument("--parties", type=int, default=8)
+    ap.add_argument("--hist-inst", type=int, default=100000)
+    ap.add_argument("--hist-cols", type=int, default=28)
     ap.add_argument("--n", type=int, default=1 << 20, help="ciphertexts for the single-op rates")
     a = ap.parse_args()
     import torch
@@ -77,6 +79,24 @@ def main():
                          "adds_per_s": round(bins * (P - 1) / (ms * 1e-3)),
                          "input_GB": round(x.numel() * 4 / 1e9, 2),
                          "hbm_GBps_boundary": round((x.numel() + out.numel()) * 4 / (ms * 1e-3) / 1e9, 1)}
+    # histogram scatter (hist_tree_builder.cpp:574-595): n_inst x n_col members into bins, g and h
+    from fedtree_amd.paillier import histogram_segments
+    n_inst, n_col, nb = a.hist_inst, a.hist_cols, 256
+    rng = np.random.default_rng(1)
+    bins_ = rng.integers(0, nb, (n_inst, n_col)).astype(np.uint8)
+    cut = np.arange(n_col + 1, dtype=np.int64) * nb
+    t0 = time.perf_counter()
+    seg_ptr, idx = histogram_segments(bins_.reshape(-1), cut, 255 + 1)
+    t_csr = time.perf_counter() - t0
+    gh = c[: 2 * n_inst] if 2 * n_inst <= n else c[:n].repeat((2 * n_inst + n - 1) // n, 1)[: 2 * n_inst]
+    seg2 = np.concatenate([seg_ptr, seg_ptr[1:] + seg_ptr[-1]])
+    idx2 = np.concatenate([idx, idx + n_inst])
+    hout = torch.empty((2 * len(seg_ptr) - 2, cw), dtype=torch.int32, device="cuda")
+    t0 = time.perf_counter()
+    rate, ms = timed(lambda: pl.reduce_segments_dev(gh, seg2, hout, idx=idx2), len(idx2), 1)
+    res["hist_build"] = {"instances": n_inst, "features": n_col, "bins": int(cut[-1]), "members": int(len(idx2)),
+                         "kernel_ms": round(ms, 2), "members_per_s": round(rate), "csr_host_s": round(t_csr, 3),
+                         "wall_s_2calls": round(time.perf_counter() - t0, 3)}
     for kk in list(res):
         if isinstance(res[kk], float):
             res[kk] = round(res[kk])
