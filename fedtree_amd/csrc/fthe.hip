@@ -58,7 +58,8 @@ uint64_t splitmix64(uint64_t &s) {
 size_t chunk_lanes() {
     static size_t v = [] {
         const char *e = getenv("FTHE_CHUNK");
-        size_t c = e ? (size_t)strtoull(e, nullptr, 10) : 262144;
+        // 393216 lanes = 6144 waves: whole rounds at 2 waves/SIMD (s74) and 3 (s37, s152) on 1024 SIMDs
+        size_t c = e ? (size_t)strtoull(e, nullptr, 10) : 393216;
         c = (c + 255) / 256 * 256;
         return c < 256 ? (size_t)256 : c;
     }();
@@ -589,7 +590,10 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     int vi = variant_index(S);
     if (vi < 0) return FTHE_ERR_UNSUPPORTED;
-    const unsigned blocks = (unsigned)((size_t)L * kVariants[vi].lanes / 256);
+    // only the workgroups that hold live elements (slot strides stay those of L)
+    if (live > (size_t)L) return FTHE_ERR_ARG;
+    if (live == 0) return FTHE_OK;
+    const unsigned blocks = (unsigned)((live * kVariants[vi].lanes + 255) / 256);
     std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
     if (c->prof) {
         if (c->prof_used == c->prof_ev.size()) {
@@ -614,6 +618,18 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
         c->prof_launch_lanes += (double)live;
     }
     return FTHE_OK;
+}
+
+// AoS rows <-> slot limbs through the LDS-tiled kernels (fthe_glue.hip).
+void pack_rows(hipStream_t st, const uint32_t *in, int win, size_t count, int bit0, uint32_t *slot, int S, int L,
+               int B, const int64_t *idx = nullptr) {
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((L + PACK_TILE - 1) / PACK_TILE)), dim3(256),
+                       (size_t)PACK_TILE * (win + 1) * 4, st, in, win, idx, count, bit0, slot, S, L, B);
+}
+void unpack_rows(hipStream_t st, uint32_t *x, const uint32_t *N, int S, int L, size_t count, uint32_t *out,
+                 int wout, int B) {
+    hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((L + PACK_TILE - 1) / PACK_TILE)), dim3(256),
+                       (size_t)PACK_TILE * (wout + 1) * 4, st, x, N, S, L, count, out, wout, B);
 }
 
 struct Launch {
@@ -708,9 +724,9 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
         hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (crt) {
             // r (< n) -> low / high halves in the small layout
-            hipLaunchKernelGGL(k_pack_words, L1.grid(), dim3(256), 0, c->stream, rw, rwn, cnt, 0,
+            pack_rows(c->stream, rw, rwn, cnt, 0,
                                L1.slot(SL_IN0), L1.S, L, L1.B);
-            hipLaunchKernelGGL(k_pack_words, L1.grid(), dim3(256), 0, c->stream, rw, rwn, cnt, L1.B * L1.S,
+            pack_rows(c->stream, rw, rwn, cnt, L1.B * L1.S,
                                L1.slot(SL_IN1), L1.S, L, L1.B);
             if ((rc = L1.prog(k->pr_encA_p, k->mp1))) return rc;
             if ((rc = L1.prog(k->pr_encA_q, k->mq1))) return rc;
@@ -729,10 +745,10 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
             hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
                                k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else {
-            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, rw, rwn, cnt, 0,
+            pack_rows(c->stream, rw, rwn, cnt, 0,
                                Lc.slot(SL_IN0), S, L, Lc.B);
             if ((rc = Lc.prog(k->pr_enc_pub, k->mn2))) return rc;
-            hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
                                S, L, cnt, out + off * cw, cw, Lc.B);
         }
         Lc.mm += L1.mm; L1.mm = 0;
@@ -757,8 +773,8 @@ extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, si
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
         const uint32_t *src = ct + off * cw;
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, src, cw, cnt, Lc.B * S,
+        pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+        pack_rows(c->stream, src, cw, cnt, Lc.B * S,
                            Lc.slot(SL_IN1), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
         if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) return rc;
@@ -798,10 +814,10 @@ extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const u
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
+        pack_rows(c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+        pack_rows(c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_add, k->mn2))) return rc;
-        hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+        unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
                            cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
@@ -859,10 +875,10 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
         for (int j = 0; j < kk; j++)
-            hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + ((size_t)j * count + off) * cw, cw,
+            pack_rows(c->stream, x + ((size_t)j * count + off) * cw, cw,
                                cnt, 0, Lc.slot(base + j), S, L, Lc.B);
         if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
-        hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+        unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
                            cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
@@ -945,11 +961,10 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
             size_t cnt = std::min((size_t)L, G - off);
             Lc.live = cnt;
             for (int j = 0; j < K; j++)
-                hipLaunchKernelGGL(k_pack_gather, Lc.grid(), dim3(256), 0, c->stream, src, cw,
-                                   (const int64_t *)c->scratch.p + (size_t)j * G + off, cnt, Lc.slot(base + j), S, L,
-                                   Lc.B);
+                pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(base + j), S, L, Lc.B,
+                          (const int64_t *)c->scratch.p + (size_t)j * G + off);
             if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
-            hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
                                S, L, cnt, dst + off * cw, cw, Lc.B);
         }
         if (done_after) break;
@@ -1002,9 +1017,9 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
-        hipLaunchKernelGGL(k_pack_words, Lc.grid(), dim3(256), 0, c->stream, x + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+        pack_rows(c->stream, x + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
-        hipLaunchKernelGGL(k_unpack_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+        unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
                            cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);

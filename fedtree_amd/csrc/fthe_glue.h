@@ -7,13 +7,15 @@
 namespace fthe {
 struct RngKey { uint32_t k[8]; uint64_t nonce; };
 
-__global__ void k_pack_words(const uint32_t *in, int win, size_t count, int bit0, uint32_t *slot, int S, int L, int rb);
-__global__ void k_pack_gather(const uint32_t *in, int win, const int64_t *idx, size_t count, uint32_t *slot, int S, int L, int rb);
+constexpr int PACK_TILE = 64;       // ciphertexts per block of the tiled layout kernels
+__global__ void k_pack_rows(const uint32_t *in, int win, const int64_t *idx, size_t count, int bit0, uint32_t *slot,
+                            int S, int L, int rb);
+__global__ void k_unpack_rows(uint32_t *x, const uint32_t *N, int S, int L, size_t count, uint32_t *out, int wout,
+                              int rb);
 __global__ void k_pack_u64(const uint64_t *m, size_t count, uint32_t *slot, int S, int L, int rb);
 __global__ void k_copy_limbs(const uint32_t *src, int Ssrc, uint32_t *dst, int Sdst, int L);
 __global__ void k_fill_const(const uint32_t *limbs, uint32_t *slot, int S, int L);
 __global__ void k_canon(uint32_t *x, const uint32_t *N, int S, int L, int rb);
-__global__ void k_unpack_canon(uint32_t *x, const uint32_t *N, int S, int L, size_t count, uint32_t *out, int wout, int rb);
 __global__ void k_crt_enc_prep(uint32_t *cp, uint32_t *cq, const uint32_t *p2, const uint32_t *q2,
                                const uint32_t *two_p2, uint32_t *u, int S, int L, int rb);
 __global__ void k_mul_add_out(const uint32_t *a, int na, const uint32_t *B, int nb, const uint32_t *h, int nh,

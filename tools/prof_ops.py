@@ -1,0 +1,53 @@
+"""Small driver for kernel traces / counters of the mod-n^2 (four-lane) kernel:
+one device-resident add, one 8-way reduce and one histogram scatter at Paillier-2048.
+
+  python tools/prof_ops.py [--n 262144]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=262144)
+    ap.add_argument("--ops", default="add,kway,hist")
+    a = ap.parse_args()
+    import torch
+    from fedtree_amd.paillier import Device, Paillier, histogram_segments
+    dev = Device(0)
+    pl = Paillier(dev).keygen(2048, seed=5)
+    cw = 2 * pl.n_words
+    n = a.n
+    m = torch.randint(0, 2**62, (n,), dtype=torch.int64, device="cuda")
+    c = torch.empty((n, cw), dtype=torch.int32, device="cuda")
+    pl.encrypt_u64_dev(m, c, seed=1)
+    o = torch.empty_like(c)
+    ops = a.ops.split(",")
+    if "add" in ops:
+        pl.add_dev(c, c, o)
+        dev.sync()
+        print("add", n, "ms", dev.last_kernel_ms())
+    if "kway" in ops:
+        x = torch.stack([c] * 8)
+        pl.reduce_kway_dev(x, 8, o)
+        dev.sync()
+        print("kway8", n, "ms", dev.last_kernel_ms())
+    if "hist" in ops:
+        rng = np.random.default_rng(1)
+        ni = n // 2
+        bins = rng.integers(0, 256, (ni, 8)).astype(np.uint8)
+        cut = np.arange(9, dtype=np.int64) * 256
+        seg, idx = histogram_segments(bins.reshape(-1), cut, 256)
+        out = torch.empty((len(seg) - 1, cw), dtype=torch.int32, device="cuda")
+        pl.reduce_segments_dev(c, seg, out, idx=idx)
+        dev.sync()
+        print("hist", len(idx), "ms", dev.last_kernel_ms())
+
+
+if __name__ == "__main__":
+    main()
