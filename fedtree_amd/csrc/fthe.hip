@@ -92,9 +92,26 @@ struct DevBuf {
     ~DevBuf() { if (p) hipFree(p); }
 };
 
+// Pinned host staging buffer (page-locked: truly asynchronous DMA).
+struct PinBuf {
+    void *p = nullptr; size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return FTHE_OK;
+        if (p) hipHostFree(p);
+        p = nullptr; n = 0;
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return FTHE_ERR_NOMEM;
+        n = bytes;
+        return FTHE_OK;
+    }
+    ~PinBuf() { if (p) hipHostFree(p); }
+};
+
 struct fthe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t copy = nullptr;               // host<->device staging copies, overlapped with compute
+    PinBuf stage_out[2], stage_in[2];
+    hipEvent_t ev_done[2] = {}, ev_copied[2] = {}, ev_in[2] = {};
     hipModule_t mod[MAX_VARIANTS] = {};
     hipFunction_t fn[MAX_VARIANTS] = {};
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
@@ -215,6 +232,12 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
     std::unique_ptr<fthe_ctx> c(new fthe_ctx);
     c->device = device;
     HIPOK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPOK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+        HIPOK(hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
+        HIPOK(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
+        HIPOK(hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming));
+    }
     for (int i = 0; i < MAX_VARIANTS; i++) {
         const unsigned char *blob = fthe_montprog_blob(kVariants[i].S);
         if (!blob) return FTHE_ERR_HIP;
@@ -233,11 +256,18 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->copy) hipStreamSynchronize(c->copy);
     for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) hipModuleUnload(c->mod[i]);
     for (auto &e : c->prof_ev) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->copy) hipStreamDestroy(c->copy);
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_done[i]) hipEventDestroy(c->ev_done[i]);
+        if (c->ev_copied[i]) hipEventDestroy(c->ev_copied[i]);
+        if (c->ev_in[i]) hipEventDestroy(c->ev_in[i]);
+    }
     delete c;
 }
 
@@ -629,7 +659,7 @@ void pack_rows(hipStream_t st, const uint32_t *in, int win, size_t count, int bi
 void unpack_rows(hipStream_t st, uint32_t *x, const uint32_t *N, int S, int L, size_t count, uint32_t *out,
                  int wout, int B) {
     hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((L + PACK_TILE - 1) / PACK_TILE)), dim3(256),
-                       (size_t)PACK_TILE * (wout + 1) * 4, st, x, N, S, L, count, out, wout, B);
+                       (size_t)(PACK_TILE + 1) * S * 4, st, x, N, S, L, count, out, wout, B);
 }
 
 struct Launch {
@@ -674,13 +704,119 @@ int end_call(fthe_ctx *c, Launch &Lc) {
     return FTHE_OK;
 }
 
+// Host-resident calls: chunked, double-buffered transfers through pinned
+// staging on the context's copy stream.  Chunk i+1's input is staged and
+// chunk i's output drained while the kernels of the neighbouring chunk run,
+// so a host-to-host call costs ~max(compute, PCIe + host memcpy) rather than
+// their sum.  Caller buffers that are already page-locked are DMA'd directly.
+struct HostPipe {
+    struct In { const uint8_t *h; uint8_t *d; size_t row; bool pinned; };
+    struct Out { uint8_t *h; const uint8_t *d; size_t row; bool pinned; };
+    fthe_ctx *c;
+    In in[2]; int nin = 0;
+    Out out[2]; int nout = 0;
+    size_t L = 0, count = 0;
+    bool pend = false; int pend_slot = 0; size_t pend_off = 0, pend_cnt = 0;
+    static bool is_pinned(const void *p) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+        return a.type == hipMemoryTypeHost;
+    }
+    void add_in(const void *h, void *d, size_t row) {
+        in[nin++] = In{(const uint8_t *)h, (uint8_t *)d, row, is_pinned(h)};
+    }
+    void add_out(void *h, const void *d, size_t row) {
+        out[nout++] = Out{(uint8_t *)h, (const uint8_t *)d, row, is_pinned(h)};
+    }
+    size_t in_row() const { size_t r = 0; for (int i = 0; i < nin; i++) r += in[i].row; return r; }
+    size_t out_row() const { size_t r = 0; for (int i = 0; i < nout; i++) r += out[i].row; return r; }
+    int stage(size_t off) {                     // input rows [off, off + L) -> device, slot (off / L) & 1
+        if (off >= count) return FTHE_OK;
+        const size_t cnt = std::min(L, count - off);
+        const int sl = (int)((off / L) & 1);
+        HIPOK(hipEventSynchronize(c->ev_in[sl]));   // the slot's previous H2D has drained
+        uint8_t *st = (uint8_t *)c->stage_in[sl].p;
+        for (int i = 0; i < nin; i++) {
+            const size_t b = cnt * in[i].row, o = off * in[i].row;
+            if (in[i].pinned) {
+                HIPOK(hipMemcpyAsync(in[i].d + o, in[i].h + o, b, hipMemcpyHostToDevice, c->copy));
+            } else {
+                memcpy(st, in[i].h + o, b);
+                HIPOK(hipMemcpyAsync(in[i].d + o, st, b, hipMemcpyHostToDevice, c->copy));
+                st += b;
+            }
+        }
+        HIPOK(hipEventRecord(c->ev_in[sl], c->copy));
+        return FTHE_OK;
+    }
+    int finish_pending() {
+        if (!pend) return FTHE_OK;
+        HIPOK(hipEventSynchronize(c->ev_copied[pend_slot]));
+        const uint8_t *st = (const uint8_t *)c->stage_out[pend_slot].p;
+        for (int i = 0; i < nout; i++) {
+            if (out[i].pinned) continue;
+            const size_t b = pend_cnt * out[i].row;
+            memcpy(out[i].h + pend_off * out[i].row, st, b);
+            st += b;
+        }
+        pend = false;
+        return FTHE_OK;
+    }
+    // before the kernels of chunk [off, off+cnt)
+    int before(size_t off, size_t Lc, size_t cnt_total) {
+        int rc;
+        if (off == 0) {
+            L = Lc; count = cnt_total;
+            for (int i = 0; i < 2; i++) {
+                if ((rc = c->stage_in[i].ensure(std::max<size_t>(1, L * in_row())))) return rc;
+                if ((rc = c->stage_out[i].ensure(std::max<size_t>(1, L * out_row())))) return rc;
+                HIPOK(hipEventRecord(c->ev_in[i], c->copy));
+                HIPOK(hipEventRecord(c->ev_copied[i], c->copy));
+            }
+            if ((rc = stage(0))) return rc;
+        }
+        if (nin) HIPOK(hipStreamWaitEvent(c->stream, c->ev_in[(off / L) & 1], 0));
+        return FTHE_OK;
+    }
+    // after the kernels of chunk [off, off+cnt) are enqueued
+    int after(size_t off, size_t cnt) {
+        int rc;
+        const int sl = (int)((off / L) & 1);
+        if (nout) {
+            HIPOK(hipEventRecord(c->ev_done[sl], c->stream));
+            HIPOK(hipStreamWaitEvent(c->copy, c->ev_done[sl], 0));
+            uint8_t *st = (uint8_t *)c->stage_out[sl].p;
+            for (int i = 0; i < nout; i++) {
+                const size_t b = cnt * out[i].row, o = off * out[i].row;
+                if (out[i].pinned) {
+                    HIPOK(hipMemcpyAsync(out[i].h + o, out[i].d + o, b, hipMemcpyDeviceToHost, c->copy));
+                } else {
+                    HIPOK(hipMemcpyAsync(st, out[i].d + o, b, hipMemcpyDeviceToHost, c->copy));
+                    st += b;
+                }
+            }
+            HIPOK(hipEventRecord(c->ev_copied[sl], c->copy));
+        }
+        if ((rc = stage(off + L))) return rc;       // next chunk's input, behind this chunk's compute
+        if ((rc = finish_pending())) return rc;      // previous chunk's output -> caller
+        if (nout) { pend = true; pend_slot = sl; pend_off = off; pend_cnt = cnt; }
+        return FTHE_OK;
+    }
+    int finish() {
+        int rc = finish_pending();
+        if (rc) return rc;
+        HIPOK(hipStreamSynchronize(c->copy));
+        HIPOK(hipStreamSynchronize(c->stream));
+        return FTHE_OK;
+    }
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // Encrypt
-extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count,
-                                    const uint32_t *r, int r_words, uint64_t rng_seed,
-                                    uint32_t *out, int flags) {
+static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r, int r_words,
+                        uint64_t rng_seed, uint32_t *out, int flags, HostPipe *pipe) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
     if (r && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
     bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
@@ -714,6 +850,7 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt; L1.live = cnt;
+        if (pipe && (rc = pipe->before(off, L, count))) return rc;
         const uint32_t *rw = r + (r ? off * r_words : 0);
         int rwn = r_words;
         if (!r) {
@@ -752,14 +889,21 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
                                S, L, cnt, out + off * cw, cw, Lc.B);
         }
         Lc.mm += L1.mm; L1.mm = 0;
+        if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);
 }
 
+extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count,
+                                    const uint32_t *r, int r_words, uint64_t rng_seed,
+                                    uint32_t *out, int flags) {
+    return encrypt_impl(k, c, m, count, r, r_words, rng_seed, out, flags, nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Decrypt (CRT)
-extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count,
-                                uint64_t *m_low, uint32_t *m_full) {
+static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low,
+                        uint32_t *m_full, HostPipe *pipe) {
     if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
     if (!k->priv) return FTHE_ERR_NOPRIV;
     Launch Lc;
@@ -772,6 +916,7 @@ extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, si
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
+        if (pipe && (rc = pipe->before(off, L, count))) return rc;
         const uint32_t *src = ct + off * cw;
         pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         pack_rows(c->stream, src, cw, cnt, Lc.B * S,
@@ -797,13 +942,20 @@ extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, si
         if (off + L < count) {   // restore the exponentiation constants for the next chunk
             Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p); Lc.fill(SL_C2, k->c_R2q);
         }
+        if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);
 }
 
+extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count,
+                                uint64_t *m_low, uint32_t *m_full) {
+    return decrypt_impl(k, c, ct, count, m_low, m_full, nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Add / k-way product / scalar mul (mod n^2)
-extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+static int add_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,
+                    HostPipe *pipe) {
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
@@ -814,13 +966,19 @@ extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const u
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
+        if (pipe && (rc = pipe->before(off, L, count))) return rc;
         pack_rows(c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         pack_rows(c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_add, k->mn2))) return rc;
         unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
                            cnt, out + off * cw, cw, Lc.B);
+        if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);
+}
+
+extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    return add_impl(k, c, a, b, count, out, nullptr);
 }
 
 // Programs built per call (k-way product, scalar exponent) go through a
@@ -1053,42 +1211,53 @@ struct HostIO {
 
 extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
                                 int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
-    if (!k || !c) return FTHE_ERR_ARG;
+    if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
+    if (r && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
-    HostIO io{c}; void *dm, *dr = nullptr, *dc; int rc;
     size_t cw = 2 * (size_t)k->n_words;
-    if ((rc = io.in(0, m, count * 8, &dm))) return rc;
-    if (r && (rc = io.in(1, r, count * r_words * 4, &dr))) return rc;
-    if ((rc = io.outbuf(2, count * cw * 4, &dc))) return rc;
-    if ((rc = fthe_encrypt_u64_dev(k, c, (const uint64_t *)dm, count, (const uint32_t *)dr, r_words, rng_seed,
-                                   (uint32_t *)dc, flags))) return rc;
-    return io.back(out, dc, count * cw * 4);
+    int rc;
+    if ((rc = c->io[0].ensure(std::max<size_t>(4, count * 8))) || (rc = c->io[2].ensure(std::max<size_t>(4, count * cw * 4))))
+        return rc;
+    if (r && (rc = c->io[1].ensure(std::max<size_t>(4, count * r_words * 4)))) return rc;
+    HostPipe pipe{c};
+    pipe.add_in(m, c->io[0].p, 8);
+    if (r) pipe.add_in(r, c->io[1].p, (size_t)r_words * 4);
+    pipe.add_out(out, c->io[2].p, cw * 4);
+    if ((rc = encrypt_impl(k, c, (const uint64_t *)c->io[0].p, count, r ? (const uint32_t *)c->io[1].p : nullptr, r_words,
+                           rng_seed, (uint32_t *)c->io[2].p, flags, count ? &pipe : nullptr))) return rc;
+    return pipe.finish();
 }
 
 extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full) {
-    if (!k || !c) return FTHE_ERR_ARG;
+    if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
-    HostIO io{c}; void *dc, *dl = nullptr, *df = nullptr; int rc;
-    size_t cw = 2 * (size_t)k->n_words;
-    if ((rc = io.in(0, ct, count * cw * 4, &dc))) return rc;
-    if (m_low && (rc = io.outbuf(1, count * 8, &dl))) return rc;
-    if (m_full && (rc = io.outbuf(2, count * k->n_words * 4, &df))) return rc;
-    if ((rc = fthe_decrypt_dev(k, c, (const uint32_t *)dc, count, (uint64_t *)dl, (uint32_t *)df))) return rc;
-    if (m_low && (rc = io.back(m_low, dl, count * 8))) return rc;
-    if (m_full && (rc = io.back(m_full, df, count * k->n_words * 4))) return rc;
-    return fthe_ctx_sync(c);
+    size_t cw = 2 * (size_t)k->n_words, nw = k->n_words;
+    int rc;
+    if ((rc = c->io[0].ensure(std::max<size_t>(4, count * cw * 4)))) return rc;
+    if (m_low && (rc = c->io[1].ensure(std::max<size_t>(4, count * 8)))) return rc;
+    if (m_full && (rc = c->io[2].ensure(std::max<size_t>(4, count * nw * 4)))) return rc;
+    HostPipe pipe{c};
+    pipe.add_in(ct, c->io[0].p, cw * 4);
+    if (m_low) pipe.add_out(m_low, c->io[1].p, 8);
+    if (m_full) pipe.add_out(m_full, c->io[2].p, nw * 4);
+    if ((rc = decrypt_impl(k, c, (const uint32_t *)c->io[0].p, count, m_low ? (uint64_t *)c->io[1].p : nullptr,
+                           m_full ? (uint32_t *)c->io[2].p : nullptr, count ? &pipe : nullptr))) return rc;
+    return pipe.finish();
 }
 
 extern "C" int fthe_add(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
-    if (!k || !c) return FTHE_ERR_ARG;
+    if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
-    HostIO io{c}; void *da, *db, *dout; int rc;
-    size_t bytes = count * 2 * (size_t)k->n_words * 4;
-    if ((rc = io.in(0, a, bytes, &da))) return rc;
-    if ((rc = io.in(1, b, bytes, &db))) return rc;
-    if ((rc = io.outbuf(2, bytes, &dout))) return rc;
-    if ((rc = fthe_add_dev(k, c, (const uint32_t *)da, (const uint32_t *)db, count, (uint32_t *)dout))) return rc;
-    return io.back(out, dout, bytes);
+    size_t row = 2 * (size_t)k->n_words * 4;
+    int rc;
+    for (int i = 0; i < 3; i++) if ((rc = c->io[i].ensure(std::max<size_t>(4, count * row)))) return rc;
+    HostPipe pipe{c};
+    pipe.add_in(a, c->io[0].p, row);
+    pipe.add_in(b, c->io[1].p, row);
+    pipe.add_out(out, c->io[2].p, row);
+    if ((rc = add_impl(k, c, (const uint32_t *)c->io[0].p, (const uint32_t *)c->io[1].p, count, (uint32_t *)c->io[2].p,
+                       count ? &pipe : nullptr))) return rc;
+    return pipe.finish();
 }
 
 extern "C" int fthe_reduce_kway(fthe_key *k, fthe_ctx *c, const uint32_t *x, int kk, size_t count, uint32_t *out) {
