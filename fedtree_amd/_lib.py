@@ -63,6 +63,10 @@ _PROTOS = {
     "fthe_scalar_mul_u64": (_I, [_P, _P, _P, _U64, _SZ, _P]),
     "fthe_reduce_kway_dev": (_I, [_P, _P, _P, _I, _SZ, _P]),
     "fthe_reduce_kway": (_I, [_P, _P, _P, _I, _SZ, _P]),
+    "fthe_sub_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
+    "fthe_sub": (_I, [_P, _P, _P, _P, _SZ, _P]),
+    "fthe_scan_segments_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
+    "fthe_scan_segments": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_reduce_segments_dev": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
     "fthe_reduce_segments": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
     "fthe_encode_fixed_dev": (_I, [_P, _P, _SZ, _P]),

@@ -109,12 +109,28 @@ struct Prog {
     void addsmall(uint32_t k) { op(OP_ADDSMALL, k); }
     void end() { op(OP_END, 0); }
 
+    // X <- X^(2^j - 1) (Montgomery domain) by the all-ones addition chain:
+    // 2^(2a)-1 = (2^a-1) 2^a + (2^a-1)  and  2^(a+1)-1 = 2 (2^a-1) + 1.
+    // j-1 + popcount(j)-1 ... about log2(j) + popcount(j) multiplications and
+    // j-1 squarings (the exponent 2^64-1 of GHPair::operator-: 63 + 6).
+    void pow_ones(unsigned j, int base_slot, int tmp_slot) {
+        if (j <= 1) return;
+        storex(base_slot);
+        int top = 31 - __builtin_clz(j);
+        unsigned a = 1;
+        for (int b = top - 1; b >= 0; b--) {
+            storex(tmp_slot); sqr((int)a); mul(tmp_slot); a *= 2;          // 2^(2a)-1
+            if ((j >> b) & 1) { sqr(1); mul(base_slot); a += 1; }         // 2^(a+1)-1
+        }
+    }
+
     // X <- X^e (Montgomery domain), left-to-right sliding window of width w.
     // Uses slots tbl0 .. tbl0 + 2^(w-1) - 1 and sq_slot.  e > 0.
     void pow(const mpz_t e, int tbl0, int sq_slot, int w) {
         size_t nb = mpz_sizeinbase(e, 2);
         if (mpz_sgn(e) == 0) return;   // caller never asks for e == 0
         if (nb == 1) return;           // e == 1
+        if (nb >= 8 && mpz_popcount(e) == nb) { pow_ones((unsigned)nb, tbl0, sq_slot); return; }
         // largest odd window value needed
         int ntab = 1 << (w - 1);
         storex(tbl0);

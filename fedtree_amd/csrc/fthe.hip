@@ -192,7 +192,7 @@ struct fthe_key {
     int c_R2p = -1, c_R3p = -1, c_nRp = -1, c_R2q = -1, c_R3q = -1, c_nRq = -1;
     int c_p2 = -1, c_q2 = -1, c_2p2 = -1, c_qinvRp2 = -1;
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
-    PH pr_enc_pub, pr_add, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 };
 
@@ -376,6 +376,12 @@ static int key_finish(fthe_key *k) {
         Prog a;
         a.loadx(SL_IN0); a.mul(SL_IN1); a.mul(SL_C0); a.storex(SL_OUTP); a.end();
         k->pr_add = k->add_prog(a);
+        // sub: a * b^(2^64-1) mod n^2 (GHPair::operator-, common.h:311-317): b R; (b R)^(2^64-1)
+        // in the Montgomery domain by the all-ones chain; times a (plain) leaves the plain product
+        Prog sb;
+        sb.loadx(SL_IN1); sb.mul(SL_C0); sb.pow_ones(64, SL_T0, SL_T1); sb.mul(SL_IN0);
+        sb.storex(SL_OUTP); sb.end();
+        k->pr_sub = k->add_prog(sb);
     }
     if (k->priv) {
         int rc;
@@ -954,8 +960,8 @@ extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, si
 
 // ---------------------------------------------------------------------------
 // Add / k-way product / scalar mul (mod n^2)
-static int add_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,
-                    HostPipe *pipe) {
+static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,
+                     HostPipe *pipe, bool sub) {
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
@@ -969,7 +975,7 @@ static int add_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t 
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         pack_rows(c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         pack_rows(c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
-        if ((rc = Lc.prog(k->pr_add, k->mn2))) return rc;
+        if ((rc = Lc.prog(sub ? k->pr_sub : k->pr_add, k->mn2))) return rc;
         unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
                            cnt, out + off * cw, cw, Lc.B);
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
@@ -978,7 +984,13 @@ static int add_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t 
 }
 
 extern "C" int fthe_add_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
-    return add_impl(k, c, a, b, count, out, nullptr);
+    return pair_impl(k, c, a, b, count, out, nullptr, false);
+}
+
+// out = a * b^(2^64-1) mod n^2: the homomorphic a - b of GHPair::operator- (common.h:253-337,
+// both operands encrypted), i.e. Paillier::add(a, Paillier::mul(b, (unsigned long)-1)).
+extern "C" int fthe_sub_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    return pair_impl(k, c, a, b, count, out, nullptr, true);
 }
 
 // Programs built per call (k-way product, scalar exponent) go through a
@@ -1042,12 +1054,63 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     return end_call(c, Lc);
 }
 
+// Gathered K-way products: out[g] = prod_{j<K} x[idx[j*G + g]] mod n^2 (idx < 0 -> 1),
+// the building block of the segmented product and the segmented scan.  One
+// launch per chunk: K gathered tile loads, then X = x_0; X <- x_j X R^-1;
+// X <- X (R^K) R^-1.  idx is a host array, uploaded per pass.
+namespace {
+struct GatherProd {
+    fthe_key *k; fthe_ctx *c;
+    static constexpr int K = 8;
+    Launch Lc; int base = 0; double mm = 0; size_t prog_words = 0;
+    int init(size_t maxG) {
+        base = nslots_for(k);
+        int rc = begin_call(c, k, maxG, Lc, base + K, k->sn2);
+        if (rc) return rc;
+        Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)K, k->n2);
+        std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
+        Prog p;
+        p.loadx(base);
+        for (int j = 1; j < K; j++) p.mul(base + j);
+        p.mul(SL_C0);
+        p.storex(SL_OUTP); p.end();
+        mm = p.montmuls;
+        prog_words = p.w.size();
+        Prog blob; blob.w = p.w; blob.w.insert(blob.w.end(), rl.begin(), rl.end());
+        fthe_key::PH ph;
+        if ((rc = upload_dyn_prog(c, blob, ph, c->io[3]))) return rc;
+        HIPOK(hipEventRecord(c->ev0, c->stream));
+        hipLaunchKernelGGL(k_fill_const, Lc.grid(), dim3(256), 0, c->stream,
+                           (const uint32_t *)c->io[3].p + prog_words, Lc.slot(SL_C0), Lc.S, Lc.L);
+        return FTHE_OK;
+    }
+    // idx: K x G host indices into src (rows of cw words)
+    int run(const uint32_t *src, const std::vector<int64_t> &idx, size_t G, uint32_t *dst) {
+        const int cw = 2 * k->n_words, S = Lc.S, L = Lc.L;
+        int rc;
+        HIPOK(hipStreamSynchronize(c->stream));          // previous pass done with scratch
+        if ((rc = c->scratch.ensure(std::max<size_t>(8, idx.size() * 8)))) return rc;
+        if (!idx.empty()) HIPOK(hipMemcpy(c->scratch.p, idx.data(), idx.size() * 8, hipMemcpyHostToDevice));
+        for (size_t off = 0; off < G; off += L) {
+            size_t cnt = std::min((size_t)L, G - off);
+            Lc.live = cnt;
+            for (int j = 0; j < K; j++)
+                pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(base + j), S, L, Lc.B,
+                          (const int64_t *)c->scratch.p + (size_t)j * G + off);
+            if ((rc = launch_dyn(Lc, c->io[3].p, mm, k->mn2))) return rc;
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L, cnt, dst + off * cw, cw, Lc.B);
+        }
+        return FTHE_OK;
+    }
+};
+}  // namespace
+
 // Segmented product: out[s] = prod_{t in [seg_ptr[s], seg_ptr[s+1])} x[idx ? idx[t] : t]
 // mod n^2 (an empty segment gives 1).  Histogram scatter by bin id
 // (hist_tree_builder.cpp:565-595: hist[bin] = hist[bin] + gh[iid]), root sums
 // (tree.cpp:20-34) and node sums.  Passes of K-way products over groups of <= K
-// consecutive members of a segment (gathered per lane), until one element per
-// segment remains.  seg_ptr / idx are host arrays; x and out device pointers.
+// consecutive members of a segment, until one element per segment remains.
+// seg_ptr / idx are host arrays; x and out device pointers.
 extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
                                         const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out) {
     if (!k || !c || !seg_ptr || (nseg && !out)) return FTHE_ERR_ARG;
@@ -1058,9 +1121,7 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
     if (idx) for (size_t t = 0; t < total; t++) if (idx[t] < 0 || (size_t)idx[t] >= count) return FTHE_ERR_ARG;
     if (!idx && total > count) return FTHE_ERR_ARG;
     if (!nseg) return FTHE_OK;
-    const int K = 8;
-    const int base = nslots_for(k);
-    // pass plan on the host: members of every segment, groups of <= K
+    const int K = GatherProd::K;
     std::vector<std::vector<int64_t>> members(nseg);
     for (size_t s = 0; s < nseg; s++)
         for (int64_t t = seg_ptr[s]; t < seg_ptr[s + 1]; t++) members[s].push_back(idx ? idx[t] : t);
@@ -1069,31 +1130,12 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
     for (auto &m : members) maxg += std::max<size_t>(1, (m.size() + K - 1) / K);
     int rc;
     if ((rc = c->io[2].ensure(maxg * cw * 4)) || (rc = c->io[1].ensure(maxg * cw * 4))) return rc;
-    Launch Lc;
-    if ((rc = begin_call(c, k, maxg, Lc, base + K, k->sn2))) return rc;
-    const int S = Lc.S, L = Lc.L;
-    // program: X = x0; X <- x_j X R^-1; X <- X (R^K) R^-1
-    Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)K, k->n2);
-    std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
-    Prog p;
-    p.loadx(base);
-    for (int j = 1; j < K; j++) p.mul(base + j);
-    p.mul(SL_C0);
-    p.storex(SL_OUTP); p.end();
-    std::vector<uint32_t> blob(p.w);
-    size_t prog_words = blob.size();
-    blob.insert(blob.end(), rl.begin(), rl.end());
-    fthe_key::PH ph;
-    Prog tmp; tmp.w = blob; tmp.montmuls = p.montmuls;
-    if ((rc = upload_dyn_prog(c, tmp, ph, c->io[3]))) return rc;
-    HIPOK(hipEventRecord(c->ev0, c->stream));
-    hipLaunchKernelGGL(k_fill_const, Lc.grid(), dim3(256), 0, c->stream,
-                       (const uint32_t *)c->io[3].p + prog_words, Lc.slot(SL_C0), S, L);
+    GatherProd gp{k, c};
+    if ((rc = gp.init(maxg))) return rc;
     const uint32_t *src = x;
     int bufsel = 1;
     std::vector<int64_t> gidx;
     while (true) {
-        // groups of this pass
         size_t G = 0;
         for (auto &m : members) G += std::max<size_t>(1, (m.size() + K - 1) / K);
         gidx.assign((size_t)K * G, -1);
@@ -1111,26 +1153,61 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
             }
             if (ng > 1) done_after = false;
         }
-        HIPOK(hipStreamSynchronize(c->stream));          // previous pass done with scratch
-        if ((rc = c->scratch.ensure(gidx.size() * 8))) return rc;
-        HIPOK(hipMemcpy(c->scratch.p, gidx.data(), gidx.size() * 8, hipMemcpyHostToDevice));
         uint32_t *dst = done_after ? out : (uint32_t *)c->io[bufsel].p;
-        for (size_t off = 0; off < G; off += L) {
-            size_t cnt = std::min((size_t)L, G - off);
-            Lc.live = cnt;
-            for (int j = 0; j < K; j++)
-                pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(base + j), S, L, Lc.B,
-                          (const int64_t *)c->scratch.p + (size_t)j * G + off);
-            if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
-            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2),
-                               S, L, cnt, dst + off * cw, cw, Lc.B);
-        }
+        if ((rc = gp.run(src, gidx, G, dst))) return rc;
         if (done_after) break;
         members.swap(next);
         src = dst;
         bufsel = 3 - bufsel;       // ping-pong io[1] / io[2]
     }
-    return end_call(c, Lc);
+    return end_call(c, gp.Lc);
+}
+
+// Segmented inclusive scan: out[t] = prod_{t' in [seg_start(t), t]} x[t'] mod n^2, the
+// inclusive_scan_by_key over (node, feature) of the histogram (hist_tree_builder.cpp:695-708;
+// GHPair::operator+ as the binary op).  Hillis-Steele in radix K: pass p multiplies the K
+// elements at stride K^p, so ceil(log_K(longest segment)) passes.  seg_ptr is a host
+// array over the elements x[0 .. seg_ptr[nseg]).
+extern "C" int fthe_scan_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64_t *seg_ptr,
+                                      size_t nseg, uint32_t *out) {
+    if (!k || !c || !seg_ptr) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (seg_ptr[0] != 0) return FTHE_ERR_ARG;
+    size_t longest = 0;
+    for (size_t s = 0; s < nseg; s++) {
+        if (seg_ptr[s + 1] < seg_ptr[s]) return FTHE_ERR_ARG;
+        longest = std::max(longest, (size_t)(seg_ptr[s + 1] - seg_ptr[s]));
+    }
+    const size_t N = (size_t)seg_ptr[nseg];
+    if (!N) return FTHE_OK;
+    if (!x || !out) return FTHE_ERR_ARG;
+    const int K = GatherProd::K;
+    const int cw = 2 * k->n_words;
+    std::vector<int64_t> start(N);
+    for (size_t s = 0; s < nseg; s++)
+        for (int64_t t = seg_ptr[s]; t < seg_ptr[s + 1]; t++) start[t] = seg_ptr[s];
+    int npass = 1;
+    for (size_t span = K; span < longest; span *= K) npass++;
+    int rc;
+    if ((rc = c->io[2].ensure(N * cw * 4)) || (rc = c->io[1].ensure(N * cw * 4))) return rc;
+    GatherProd gp{k, c};
+    if ((rc = gp.init(N))) return rc;
+    std::vector<int64_t> gidx((size_t)K * N);
+    const uint32_t *src = x;
+    int bufsel = 1;
+    size_t stride = 1;
+    for (int p = 0; p < npass; p++, stride *= K) {
+        for (int j = 0; j < K; j++)
+            for (size_t t = 0; t < N; t++) {
+                int64_t from = (int64_t)t - (int64_t)(j * stride);
+                gidx[(size_t)j * N + t] = from >= start[t] ? from : -1;
+            }
+        uint32_t *dst = p == npass - 1 ? out : (uint32_t *)c->io[bufsel].p;
+        if ((rc = gp.run(src, gidx, N, dst))) return rc;
+        src = dst;
+        bufsel = 3 - bufsel;
+    }
+    return end_call(c, gp.Lc);
 }
 
 extern "C" int fthe_reduce_segments(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
@@ -1146,6 +1223,22 @@ extern "C" int fthe_reduce_segments(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     if ((rc = fthe_reduce_segments_dev(k, c, (const uint32_t *)c->io[0].p, count, seg_ptr, idx, nseg,
                                        (uint32_t *)c->io[4].p))) return rc;
     if (nseg) HIPOK(hipMemcpyAsync(out, c->io[4].p, nseg * cw * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    return FTHE_OK;
+}
+
+extern "C" int fthe_scan_segments(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64_t *seg_ptr, size_t nseg,
+                                  uint32_t *out) {
+    if (!k || !c || !seg_ptr) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    const size_t N = (size_t)seg_ptr[nseg], bytes = N * 2 * (size_t)k->n_words * 4;
+    int rc;
+    if ((rc = c->io[0].ensure(std::max<size_t>(4, bytes))) || (rc = c->io[4].ensure(std::max<size_t>(4, bytes))))
+        return rc;
+    if (N) HIPOK(hipMemcpyAsync(c->io[0].p, x, bytes, hipMemcpyHostToDevice, c->stream));
+    if ((rc = fthe_scan_segments_dev(k, c, (const uint32_t *)c->io[0].p, seg_ptr, nseg, (uint32_t *)c->io[4].p)))
+        return rc;
+    if (N) HIPOK(hipMemcpyAsync(out, c->io[4].p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
     return FTHE_OK;
 }
@@ -1245,7 +1338,8 @@ extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t
     return pipe.finish();
 }
 
-extern "C" int fthe_add(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+static int pair_host(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,
+                     bool sub) {
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     size_t row = 2 * (size_t)k->n_words * 4;
@@ -1255,9 +1349,17 @@ extern "C" int fthe_add(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint3
     pipe.add_in(a, c->io[0].p, row);
     pipe.add_in(b, c->io[1].p, row);
     pipe.add_out(out, c->io[2].p, row);
-    if ((rc = add_impl(k, c, (const uint32_t *)c->io[0].p, (const uint32_t *)c->io[1].p, count, (uint32_t *)c->io[2].p,
-                       count ? &pipe : nullptr))) return rc;
+    if ((rc = pair_impl(k, c, (const uint32_t *)c->io[0].p, (const uint32_t *)c->io[1].p, count, (uint32_t *)c->io[2].p,
+                        count ? &pipe : nullptr, sub))) return rc;
     return pipe.finish();
+}
+
+extern "C" int fthe_add(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    return pair_host(k, c, a, b, count, out, false);
+}
+
+extern "C" int fthe_sub(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    return pair_host(k, c, a, b, count, out, true);
 }
 
 extern "C" int fthe_reduce_kway(fthe_key *k, fthe_ctx *c, const uint32_t *x, int kk, size_t count, uint32_t *out) {

@@ -214,6 +214,24 @@ class Paillier:
         _lib.check(self.lib.fthe_add(self._key, self.dev.ctx, _ptr(a), _ptr(b), len(a), _ptr(out)), "add")
         return out
 
+    def sub_batch(self, a, b):
+        """a * b^(2^64-1) mod n^2: GHPair::operator- with both sides encrypted
+        (common.h:311-317), one fused device program."""
+        a = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self._cw())
+        b = np.ascontiguousarray(b, dtype=np.uint32).reshape(-1, self._cw())
+        out = np.zeros_like(a)
+        _lib.check(self.lib.fthe_sub(self._key, self.dev.ctx, _ptr(a), _ptr(b), len(a), _ptr(out)), "sub")
+        return out
+
+    def scan_segments(self, x, seg_ptr):
+        """Inclusive prefix products inside each segment (hist_tree_builder.cpp:695-708)."""
+        x = np.ascontiguousarray(x, dtype=np.uint32).reshape(-1, self._cw())
+        seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
+        out = np.zeros((int(seg[-1]), self._cw()), dtype=np.uint32)
+        _lib.check(self.lib.fthe_scan_segments(self._key, self.dev.ctx, _ptr(x), _ptr(seg), len(seg) - 1, _ptr(out)),
+                   "scan_segments")
+        return out
+
     def reduce_kway(self, x):
         """x: (k, count, 2nw) -> prod over k (hist_tree_builder.cpp:1015-1058 merge)."""
         x = np.ascontiguousarray(x, dtype=np.uint32)
@@ -263,6 +281,19 @@ class Paillier:
         _lib.check(self.lib.fthe_add_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),
                                          ctypes.c_void_p(b.data_ptr()), cnt, ctypes.c_void_p(out.data_ptr())),
                    "add_dev")
+        return out
+
+    def sub_dev(self, a, b, out):
+        cnt = a.numel() // self._cw()
+        _lib.check(self.lib.fthe_sub_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),
+                                         ctypes.c_void_p(b.data_ptr()), cnt, ctypes.c_void_p(out.data_ptr())),
+                   "sub_dev")
+        return out
+
+    def scan_segments_dev(self, x, seg_ptr, out):
+        seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
+        _lib.check(self.lib.fthe_scan_segments_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), _ptr(seg),
+                                                   len(seg) - 1, ctypes.c_void_p(out.data_ptr())), "scan_segments_dev")
         return out
 
     def reduce_kway_dev(self, x, k, out):
@@ -374,11 +405,12 @@ class GHPairs:
             neg = GHPairs(-rhs.g, -rhs.h)
             return self + neg._enc_side(self.paillier)
         pl = rhs.paillier if not self.encrypted else self.paillier
-        negc = pl.scalar_mul(np.concatenate([rhs.g_enc, rhs.h_enc]), MINUS_ONE)
-        neg = GHPairs(np.zeros(len(rhs), np.float32), None, pl)
-        neg.g_enc, neg.h_enc = negc[:len(rhs)], negc[len(rhs):]
-        neg.encrypted = True
-        return (self if self.encrypted else self._enc_side(pl)) + neg
+        lhs = self if self.encrypted else self._enc_side(pl)
+        both = pl.sub_batch(np.concatenate([lhs.g_enc, lhs.h_enc]), np.concatenate([rhs.g_enc, rhs.h_enc]))
+        res = GHPairs(np.zeros(len(rhs), np.float32), np.zeros(len(rhs), np.float32), pl)
+        res.g_enc, res.h_enc = both[:len(rhs)], both[len(rhs):]
+        res.encrypted = True
+        return res
 
 
 def histogram_segments(bin_ids, cut_col_ptr, max_num_bin):
@@ -469,3 +501,31 @@ class HEParty:
         hist.encrypted = True
         hist.bin_encrypted = np.diff(seg_ptr) > 0
         return hist
+
+    def prefix_histogram(self, hist, cut_col_ptr):
+        """inclusive_scan_by_key over features (hist_tree_builder.cpp:695-708):
+        bin b of feature f becomes the sum of bins cut_col_ptr[f] .. b.  One
+        segmented scan on the device for g and h together.  (An untouched bin
+        enters as the ciphertext 1; the reference would promote its zero with a
+        fresh Enc(0) -- same plaintexts.)"""
+        cut = np.asarray(cut_col_ptr, dtype=np.int64)
+        n_bins = int(cut[-1])
+        if not hist.encrypted:
+            out = GHPairs(hist.g.copy(), hist.h.copy())
+            for f in range(len(cut) - 1):
+                out.g[cut[f]:cut[f + 1]] = np.cumsum(hist.g[cut[f]:cut[f + 1]], dtype=np.float32)
+                out.h[cut[f]:cut[f + 1]] = np.cumsum(hist.h[cut[f]:cut[f + 1]], dtype=np.float32)
+            return out
+        pl = hist.paillier
+        seg2 = np.concatenate([cut, cut[1:] + n_bins])
+        sc = pl.scan_segments(np.concatenate([hist.g_enc, hist.h_enc]), seg2)
+        out = GHPairs(np.zeros(n_bins, np.float32), np.zeros(n_bins, np.float32), pl)
+        out.g_enc, out.h_enc = sc[:n_bins], sc[n_bins:]
+        out.encrypted = True
+        return out
+
+    @staticmethod
+    def sibling_histogram(father, computed):
+        """hist_tree_builder.cpp:670-680: the larger child's histogram as
+        father - computed (GHPair::operator-, one fused device op per bin)."""
+        return father - computed

@@ -116,6 +116,16 @@ int fthe_add_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t
 int fthe_add(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
              size_t count, uint32_t *out);
 
+/* out[i] = a[i] * b[i]^(2^64-1) mod n^2: GHPair::operator- with both sides
+ * encrypted (common.h:253-337 -- Paillier::add(a, Paillier::mul(b, (unsigned
+ * long)-1))), fused into one program (all-ones addition chain).  The sibling
+ * histogram father - child (hist_tree_builder.cpp:678) and missing_gh (:724). */
+int fthe_sub_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
+                 size_t count, uint32_t *out);
+int fthe_sub(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
+             size_t count, uint32_t *out);
+
+
 /* ---- scalar mul: x^k mod n^2 (paillier.cpp:118), one k for the batch ------
  * The reference only multiplies by (unsigned long)-1 (subtraction,
  * common.h:264-267,311-317). */
@@ -145,6 +155,15 @@ int fthe_reduce_segments_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, si
                              const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out);
 int fthe_reduce_segments(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count,
                          const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out);
+
+/* Segmented inclusive scan: out[t] = prod of x[seg_start(t) .. t] mod n^2 --
+ * the inclusive_scan_by_key of the histogram over (node, feature)
+ * (hist_tree_builder.cpp:695-708).  seg_ptr (nseg+1 entries) is a HOST array;
+ * the elements are x[0 .. seg_ptr[nseg]). */
+int fthe_scan_segments_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, const int64_t *seg_ptr,
+                           size_t nseg, uint32_t *out);
+int fthe_scan_segments(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, const int64_t *seg_ptr,
+                       size_t nseg, uint32_t *out);
 
 /* ---- fixed-point codec (common.h:81-86,127-128,140-143) ------------------- */
 int fthe_encode_fixed_dev(fthe_ctx *ctx, const float *x, size_t count, uint64_t *m);

@@ -58,6 +58,22 @@ def mul(key, x, y):
     return pow(x, y, key["n2"])
 
 
+def sub(key, a, b):
+    """GHPair::operator- on two ciphertexts (common.h:311-317, NTL branch):
+    add(a, mul(b, (unsigned long)-1))."""
+    return add(key, a, mul(key, b, 2**64 - 1))
+
+
+def scan_segments(key, cts, seg_ptr):
+    """inclusive_scan_by_key (hist_tree_builder.cpp:695-708) with the add of
+    paillier.cpp:103 as the operator: running products inside each segment."""
+    out = list(cts[:seg_ptr[-1]])
+    for s in range(len(seg_ptr) - 1):
+        for t in range(seg_ptr[s] + 1, seg_ptr[s + 1]):
+            out[t] = add(key, out[t - 1], cts[t])
+    return out
+
+
 def segment_product(key, cts, seg_ptr, idx=None):
     """Products of ciphertext segments (the add of paillier.cpp:103 folded over
     each segment, in member order).  An empty segment gives 1."""

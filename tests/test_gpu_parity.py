@@ -388,3 +388,83 @@ def test_histogram_vs_reference_loop(dev, coracle):
         e = encode_fixed(x0)
         want = [e[idx[seg_ptr[b]:seg_ptr[b + 1]]].sum(dtype=np.uint64) for b in range(cut[-1])]
         assert np.array_equal(arr, decode_fixed(np.array(want, np.uint64)))
+
+
+@pytest.mark.parametrize("nbits", [1024, 2048])
+def test_sub_vs_oracle(dev, coracle, nbits):
+    """GHPair::operator- (common.h:311-317): a * b^(2^64-1), bit-exact; low 64
+    bits of the plaintext are ma - mb mod 2^64."""
+    pw, qw = _det_primes(coracle, nbits, 61 + nbits)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    key = pyoracle.keygen_from_primes(pl.p, pl.q)
+    rng = np.random.default_rng(nbits + 5)
+    cnt = 300
+    ma = rng.integers(0, 2**64, cnt, dtype=np.uint64)
+    mb = rng.integers(0, 2**64, cnt, dtype=np.uint64)
+    ca, cb = pl.encrypt_u64(ma, seed=1), pl.encrypt_u64(mb, seed=2)
+    got = pl.sub_batch(ca, cb)
+    want = [pyoracle.sub(key, pyoracle.from_words(x), pyoracle.from_words(y)) for x, y in zip(ca[:40], cb[:40])]
+    assert [pyoracle.from_words(x) for x in got[:40]] == want
+    assert np.array_equal(pl.decrypt_u64(got), ma - mb)
+    # scalar mul by 2^64-1 (all-ones chain) + add == fused sub
+    assert np.array_equal(pl.add_batch(ca, pl.scalar_mul(cb, 2**64 - 1)), got)
+
+
+@pytest.mark.parametrize("nbits", [1024, 2048])
+def test_scan_segments_vs_oracle(dev, coracle, nbits):
+    """Segmented inclusive scan (hist_tree_builder.cpp:695-708), ragged segments
+    including empty, single and a 300-long one (three radix-8 passes)."""
+    pw, qw = _det_primes(coracle, nbits, 71 + nbits)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    key = pyoracle.keygen_from_primes(pl.p, pl.q)
+    rng = np.random.default_rng(nbits + 9)
+    lens = [3, 0, 1, 300, 8, 9, 64, 65, 0, 17]
+    seg = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    N = int(seg[-1])
+    m = rng.integers(0, 2**40, N, dtype=np.uint64)
+    c = pl.encrypt_u64(m, seed=3)
+    got = pl.scan_segments(c, seg)
+    want = pyoracle.scan_segments(key, pyoracle.words_to_ints(c), list(seg))
+    assert [pyoracle.from_words(x) for x in got] == want
+    want_m = np.concatenate([np.cumsum(m[seg[s]:seg[s + 1]], dtype=np.uint64) for s in range(len(lens))])
+    assert np.array_equal(pl.decrypt_u64(got), want_m)
+
+
+def test_level_histogram_flow(dev, coracle):
+    """One tree level on the party side (hist_tree_builder.cpp:627-708): the
+    smaller child's histogram by segmented product, the sibling as father -
+    child (fused sub), then the per-feature prefix scan; every decrypted bin
+    equals the fixed-point sum over the right instances."""
+    from fedtree_amd.paillier import GHPairs, HEParty, decode_fixed, encode_fixed, histogram_segments
+    pw, qw = _det_primes(coracle, 1024, 81)
+    pl = _pl(dev, pyoracle.from_words(pw), pyoracle.from_words(qw))
+    rng = np.random.default_rng(8)
+    n_inst, n_col, max_bin = 400, 4, 16
+    per = rng.integers(2, max_bin + 1, n_col)
+    cut = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    bins = np.stack([rng.integers(0, per[f], n_inst) for f in range(n_col)], 1).astype(np.uint8)
+    g0 = rng.standard_normal(n_inst).astype(np.float32)
+    h0 = rng.random(n_inst).astype(np.float32)
+    gh = GHPairs(g0, h0).homo_encrypt(pl, seed=6)
+    party = HEParty(pl)
+    left = rng.random(n_inst) < 0.3
+
+    def sub_gh(mask):
+        s = GHPairs(np.zeros(mask.sum(), np.float32), None, pl)
+        s.g_enc, s.h_enc, s.encrypted = gh.g_enc[mask], gh.h_enc[mask], True
+        return s
+
+    father = party.compute_histogram(gh, bins.reshape(-1), cut, max_bin)
+    child = party.compute_histogram(sub_gh(left), bins[left].reshape(-1), cut, max_bin)
+    sib = party.sibling_histogram(father, child)
+    scanned = party.prefix_histogram(sib, cut)
+    scanned.homo_decrypt(pl)
+    sib.homo_decrypt(pl)
+    right = ~left
+    for arr_s, arr_p, x0 in ((sib.g, scanned.g, g0), (sib.h, scanned.h, h0)):
+        e = encode_fixed(x0[right])
+        seg_ptr, idx = histogram_segments(bins[right].reshape(-1), cut, max_bin)
+        per_bin = np.array([e[idx[seg_ptr[b]:seg_ptr[b + 1]]].sum(dtype=np.uint64) for b in range(cut[-1])], np.uint64)
+        assert np.array_equal(arr_s, decode_fixed(per_bin))
+        pref = np.concatenate([np.cumsum(per_bin[cut[f]:cut[f + 1]], dtype=np.uint64) for f in range(n_col)])
+        assert np.array_equal(arr_p, decode_fixed(pref))

@@ -63,6 +63,12 @@ def main():
         _lib.check(lib.fthe_scalar_mul_u64_dev(pl._key, dev.ctx, ctypes.c_void_p(c.data_ptr()), 2**64 - 1, k,
                                                ctypes.c_void_p(o.data_ptr())))
     res["scalar_mul_minus1_per_s"], _ = timed(smul, k, 1)
+    res["sub_per_s"], _ = timed(lambda: pl.sub_dev(c[:k], c[k:2 * k], o[:k]), k, 1)
+    # per-feature prefix scan of a 256-bin x 1024-feature histogram (g, h)
+    nsc = 2 * 256 * 1024
+    if nsc <= n:
+        seg = np.arange(0, nsc + 1, 256, dtype=np.int64)
+        res["scan_256bin_per_s"], _ = timed(lambda: pl.scan_segments_dev(c[:nsc], seg, o[:nsc]), nsc, 1)
     del c2
     # config 4: k-party merge of 256 x 4096 bins x {g,h}
     bins = 2 * a.hist_bins
