@@ -95,7 +95,9 @@ inline int kernel_limbs_for_bits(int bits) { return kernel_shape_for_bits(bits).
 
 // ---- uniform op program for the montprog kernel ---------------------------
 enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL = 4,
-                     OP_ADDSLOT = 5, OP_ADDSMALL = 6 };
+                     OP_ADDSLOT = 5, OP_ADDSMALL = 6,
+                     // four-lane kernel only: canonical 128-word rows, kernarg row table entry t
+                     OP_LOADW = 7, OP_MULW = 8, OP_STOREW = 9 };
 
 struct Prog {
     std::vector<uint32_t> w;
@@ -107,6 +109,9 @@ struct Prog {
     void mul(int s) { op(OP_MUL, s); montmuls += 1; }
     void addslot(int s) { op(OP_ADDSLOT, s); }
     void addsmall(uint32_t k) { op(OP_ADDSMALL, k); }
+    void loadw(int t) { op(OP_LOADW, t); }
+    void mulw(int t) { op(OP_MULW, t); montmuls += 1; }
+    void storew(int t) { op(OP_STOREW, t); }
     void end() { op(OP_END, 0); }
 
     // X <- X^(2^j - 1) (Montgomery domain) by the all-ones addition chain:

@@ -192,6 +192,8 @@ struct fthe_key {
     int c_R2p = -1, c_R3p = -1, c_nRp = -1, c_R2q = -1, c_R3q = -1, c_nRq = -1;
     int c_p2 = -1, c_q2 = -1, c_2p2 = -1, c_qinvRp2 = -1;
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
+    PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
+    bool rowio = false;
     PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 };
@@ -382,6 +384,16 @@ static int key_finish(fthe_key *k) {
         sb.loadx(SL_IN1); sb.mul(SL_C0); sb.pow_ones(64, SL_T0, SL_T1); sb.mul(SL_IN0);
         sb.storex(SL_OUTP); sb.end();
         k->pr_sub = k->add_prog(sb);
+        // row-I/O forms: canonical rows read / written by the kernel itself (no layout kernels)
+        k->rowio = k->sn2.lanes == 4 && 2 * k->n_words == 128 && !getenv("FTHE_NO_ROWIO");
+        if (k->rowio) {
+            Prog aw;
+            aw.loadw(0); aw.mulw(1); aw.mul(SL_C0); aw.storew(2); aw.end();
+            k->pr_add_w = k->add_prog(aw);
+            Prog sw;
+            sw.loadw(1); sw.mul(SL_C0); sw.pow_ones(64, SL_T0, SL_T1); sw.mulw(0); sw.storew(2); sw.end();
+            k->pr_sub_w = k->add_prog(sw);
+        }
     }
     if (k->priv) {
         int rc;
@@ -619,9 +631,13 @@ namespace {
 
 // Launch the montprog kernel, bracketed by profiling events when enabled.
 int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, const DevMod &mod, double lane_mm,
-                    size_t live) {
-    struct { void *s; const void *p; const void *cx; uint32_t ls, ss; } args = {
-        slots, prog, mod.d_ctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4)};
+                    size_t live, const void *const *rows = nullptr, int nrows = 0) {
+    struct {
+        void *s; const void *p; const void *cx; uint32_t ls, ss; uint32_t live, pad; const void *rows[16];
+    } args = {slots, prog, mod.d_ctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4), (uint32_t)live, 0, {}};
+    static_assert(sizeof(args) == 168, "kernarg layout of gen_montprog.py");
+    if (nrows > 16) return FTHE_ERR_ARG;
+    for (int i = 0; i < nrows; i++) args.rows[i] = rows[i];
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     int vi = variant_index(S);
@@ -673,9 +689,9 @@ struct Launch {
     void *base = nullptr;          // slot region (c->slots, or c->slots1 for small-modulus programs)
     uint32_t *slot(int s) const { return (uint32_t *)base + (size_t)s * S * L; }
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
-    int prog(const fthe_key::PH &ph, const DevMod &mod) {
+    int prog(const fthe_key::PH &ph, const DevMod &mod, const void *const *rows = nullptr, int nrows = 0) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live);
+        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows);
         if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;
@@ -973,11 +989,16 @@ static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
-        pack_rows(c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
-        pack_rows(c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
-        if ((rc = Lc.prog(sub ? k->pr_sub : k->pr_add, k->mn2))) return rc;
-        unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
-                           cnt, out + off * cw, cw, Lc.B);
+        if (k->rowio) {
+            const void *rows[3] = {a + off * cw, b + off * cw, out + off * cw};
+            if ((rc = Lc.prog(sub ? k->pr_sub_w : k->pr_add_w, k->mn2, rows, 3))) return rc;
+        } else {
+            pack_rows(c->stream, a + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+            pack_rows(c->stream, b + off * cw, cw, cnt, 0, Lc.slot(SL_IN1), S, L, Lc.B);
+            if ((rc = Lc.prog(sub ? k->pr_sub : k->pr_add, k->mn2))) return rc;
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
+                               cnt, out + off * cw, cw, Lc.B);
+        }
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);
@@ -1006,9 +1027,10 @@ static int upload_dyn_prog(fthe_ctx *c, const Prog &p, fthe_key::PH &ph, DevBuf 
 
 namespace {
 // Launch with an explicit (dynamic) program pointer.
-int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod) {
+int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod, const void *const *rows = nullptr,
+               int nrows = 0) {
     if (mod.m.S != Lc.S) return FTHE_ERR_ARG;
-    int rc = launch_montprog(Lc.c, Lc.base, Lc.S, Lc.L, prog, mod, mm, Lc.live);
+    int rc = launch_montprog(Lc.c, Lc.base, Lc.S, Lc.L, prog, mod, mm, Lc.live, rows, nrows);
     if (rc) return rc;
     Lc.mm += mm * (double)Lc.live;
     return FTHE_OK;
@@ -1027,11 +1049,19 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
     std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
+    const bool rowio = k->rowio && kk + 1 <= 16;
     Prog p;
-    p.loadx(base);
-    for (int j = 1; j < kk; j++) p.mul(base + j);
-    p.mul(SL_C0);
-    p.storex(SL_OUTP); p.end();
+    if (rowio) {
+        p.loadw(0);
+        for (int j = 1; j < kk; j++) p.mulw(j);
+        p.mul(SL_C0);
+        p.storew(kk); p.end();
+    } else {
+        p.loadx(base);
+        for (int j = 1; j < kk; j++) p.mul(base + j);
+        p.mul(SL_C0);
+        p.storex(SL_OUTP); p.end();
+    }
     std::vector<uint32_t> blob(p.w);
     size_t prog_words = blob.size();
     blob.insert(blob.end(), rl.begin(), rl.end());      // constant after the program
@@ -1044,6 +1074,13 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
+        if (rowio) {
+            const void *rows[16];
+            for (int j = 0; j < kk; j++) rows[j] = x + ((size_t)j * count + off) * cw;
+            rows[kk] = out + off * cw;
+            if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2, rows, kk + 1))) return rc;
+            continue;
+        }
         for (int j = 0; j < kk; j++)
             pack_rows(c->stream, x + ((size_t)j * count + off) * cw, cw,
                                cnt, 0, Lc.slot(base + j), S, L, Lc.B);
@@ -1251,16 +1288,19 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     int rc = begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
+    const bool rowio = k->rowio;
     Prog p;
     if (e == 0) {
         p.loadx(SL_C1);                 // x^0 = 1
     } else {
         Mpz ez; mpz_import(ez, 1, -1, 8, 0, 0, &e);
-        p.loadx(SL_IN0); p.mul(SL_C0);   // Montgomery form
+        if (rowio) p.loadw(0); else p.loadx(SL_IN0);
+        p.mul(SL_C0);                    // Montgomery form
         p.pow(ez, SL_TAB, SL_SQ, std::min(best_window(ez.bits()), 5));
         p.mul(SL_C1);                    // * 1 -> out of Montgomery
     }
-    p.storex(SL_OUTP); p.end();
+    if (rowio) p.storew(1); else p.storex(SL_OUTP);
+    p.end();
     fthe_key::PH ph;
     if ((rc = upload_dyn_prog(c, p, ph, c->io[3]))) return rc;
     HIPOK(hipEventRecord(c->ev0, c->stream));
@@ -1268,6 +1308,11 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
+        if (rowio) {
+            const void *rows[2] = {x + off * cw, out + off * cw};
+            if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2, rows, 2))) return rc;
+            continue;
+        }
         pack_rows(c->stream, x + off * cw, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
         unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,

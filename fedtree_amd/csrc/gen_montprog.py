@@ -37,6 +37,8 @@ Slot memory: slot s, limb k, lane g at  slots + s*slot_stride + k*L*4 + g*4
 Kernel arguments (kernarg segment):
     0  u64 slots         8  u64 prog        16 u64 ctx (N[S] u32, nprime u32)
     24 u32 limb_stride (=L*4 bytes)          28 u32 slot_stride (=S*L*4 bytes)
+    32 u32 live ciphertexts in this launch   36 u32 reserved
+    40 u64 rows[16]: row-array pointers of the row I/O ops (four-lane kernel only)
 """
 import argparse
 import sys
@@ -369,7 +371,7 @@ def _descriptor(name, lds_bytes, NVGPR, NSGPR):
     e(f'.amdhsa_kernel {name}')
     e(f'  .amdhsa_group_segment_fixed_size {lds_bytes}')
     e('  .amdhsa_private_segment_fixed_size 0')
-    e('  .amdhsa_kernarg_size 32')
+    e('  .amdhsa_kernarg_size 168')
     e('  .amdhsa_user_sgpr_count 2')
     e('  .amdhsa_user_sgpr_kernarg_segment_ptr 1')
     e('  .amdhsa_system_sgpr_workgroup_id_x 1')
@@ -387,9 +389,10 @@ def _descriptor(name, lds_bytes, NVGPR, NSGPR):
     e('---')
     e('amdhsa.kernels:')
     e('  - .args:')
-    for off_, sz, kind in ((0, 8, 'global_buffer'), (8, 8, 'global_buffer'),
-                           (16, 8, 'global_buffer'), (24, 4, 'by_value'),
-                           (28, 4, 'by_value')):
+    kargs = ((0, 8, 'global_buffer'), (8, 8, 'global_buffer'), (16, 8, 'global_buffer'),
+             (24, 4, 'by_value'), (28, 4, 'by_value'), (32, 4, 'by_value'), (36, 4, 'by_value'))
+    kargs += tuple((40 + 8 * t, 8, 'global_buffer') for t in range(16))
+    for off_, sz, kind in kargs:
         e(f'      - .offset: {off_}')
         e(f'        .size: {sz}')
         e(f'        .value_kind: {kind}')
@@ -397,7 +400,7 @@ def _descriptor(name, lds_bytes, NVGPR, NSGPR):
             e('        .address_space: global')
     e(f'    .group_segment_fixed_size: {lds_bytes}')
     e('    .kernarg_segment_align: 8')
-    e('    .kernarg_segment_size: 32')
+    e('    .kernarg_segment_size: 168')
     e('    .max_flat_workgroup_size: 256')
     e(f'    .name: {name}')
     e('    .private_segment_fixed_size: 0')
@@ -435,7 +438,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     # slot row, v2 A read cursor (rests at the ciphertext's A column), v3/v4 a_i,
     # v5 q, v[6:7] 64-bit temp, then X, N quarter, T window.
     V_TID = V_LDSW = 0
-    V_GOFF, V_LDSI = 1, 2
+    V_ROW, V_LDSI = 1, 2
     V_AI = (3, 4)
     V_Q = 5
     V_TMP = 6
@@ -447,7 +450,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     NT = Q + U
     NVGPR = TB + 2 * NT
     assert NVGPR <= 256, NVGPR
-    NSGPR = 32
+    NSGPR = 40
 
     def T(k):
         return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
@@ -481,6 +484,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
     e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
     e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
+    e('  s_load_dword s28, s[0:1], 0x20')                        # live ciphertexts
     # lane masks: k == 3 -> s[20:21], k == 0 -> s[22:23]
     e('  s_mov_b32 s20, 0x88888888')
     e('  s_mov_b32 s21, 0x88888888')
@@ -488,15 +492,13 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_mov_b32 s23, 0x11111111')
     e('  s_waitcnt lgkmcnt(0)')
     e(f'  s_load_dword s12, s[8:9], {hex(4 * S)}')
-    # g = wg*64 + tid>>2 ; k = tid & 3
-    e('  s_lshl_b32 s14, s2, 8')                                # wg*64*4 bytes
-    e(f'  v_lshrrev_b32_e32 v{V_GOFF}, 2, v{V_TID}')
-    e(f'  v_lshlrev_b32_e32 v{V_GOFF}, 2, v{V_GOFF}')
-    e(f'  v_add_u32_e32 v{V_GOFF}, s14, v{V_GOFF}')             # g*4
+    # ROW = g*512 + k*128 = wg*32768 + tid*128 (g = wg*64 + tid>>2, k = tid & 3):
+    # the lane's quarter of a 128-word row, and an encoding of (g, k) for the slot ops
+    e('  s_lshl_b32 s14, s2, 15')
+    e(f'  v_lshlrev_b32_e32 v{V_ROW}, 7, v{V_TID}')
+    e(f'  v_add_u32_e32 v{V_ROW}, s14, v{V_ROW}')
     e(f'  v_and_b32_e32 v{V_TMP}, 3, v{V_TID}')                 # k
     e(f'  v_mul_u32_u24_e32 v{V_TMP + 1}, {Q}, v{V_TMP}')       # k*Q
-    e(f'  v_mul_lo_u32 v{V_Q}, v{V_TMP + 1}, s10')               # k*Q*L*4
-    e(f'  v_add_u32_e32 v{V_GOFF}, v{V_GOFF}, v{V_Q}')
     e(f'  v_lshlrev_b32_e32 v{V_Q}, 2, v{V_TMP + 1}')            # k*Q*4
     for j in range(Q):
         e(f'  global_load_dword {NV(j)}, v{V_Q}, s[8:9] offset:{4 * j}')
@@ -516,7 +518,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_addc_u32 s7, s7, 0')
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
-                      (5, '.Laddslot'), (6, '.Laddsmall')):
+                      (5, '.Laddslot'), (6, '.Laddsmall'), (7, '.Lloadw'), (8, '.Lmulw'),
+                      (9, '.Lstorew')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -531,7 +534,18 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         e('  s_add_u32 s16, s16, s10')
         e('  s_addc_u32 s17, s17, 0')
 
+    V_GOFF = V_Q          # slot offset g*4 + k*Q*L*4, recomputed from ROW when needed
+
+    def goff():
+        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')            # g
+        e(f'  v_lshlrev_b32_e32 v{V_TMP}, 2, v{V_TMP}')            # g*4
+        e(f'  v_bfe_u32 v{V_TMP + 1}, v{V_ROW}, 7, 2')             # k
+        e(f'  v_mul_u32_u24_e32 v{V_TMP + 1}, {Q}, v{V_TMP + 1}')  # k*Q
+        e(f'  v_mul_lo_u32 v{V_TMP + 1}, v{V_TMP + 1}, s10')       # k*Q*L*4
+        e(f'  v_add_u32_e32 v{V_GOFF}, v{V_TMP}, v{V_TMP + 1}')
+
     def load_quarter(dst):
+        goff()
         slot_addr()
         for k in range(Q):
             e(f'  global_load_dword {dst(k)}, v{V_GOFF}, s[16:17]')
@@ -575,6 +589,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_branch .Lprog')
 
     e('.Lstorex:')
+    goff()
     slot_addr()
     for k in range(Q):
         e(f'  global_store_dword v{V_GOFF}, {X(k)}, s[16:17]')
@@ -617,6 +632,130 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_cbranch_scc1 .Lprog')
     write_a(X)
     e('  s_branch .Lmontmul')
+
+    # ---- row I/O: canonical 128-word rows (n^2 of Paillier-2048) read and
+    # written in place of the layout-conversion kernels.  Row table entry t
+    # (kernarg 32) points at row 0 of this launch; ciphertext g's lane k owns
+    # words [32k, 32k+32) and the radix-2^B limbs [kQ, kQ+Q) = bits [1026k, 1026k+1026).
+    assert Q == 38 and B == 27, "row I/O is laid out for 152 limbs of 27 bits (4096-bit rows)"
+    W0 = TB               # 33 row words (T window is free outside a product)
+    A0 = TB + 34          # 38 limbs of a MULW operand
+    D0 = TB               # STOREW: X - N
+    U0 = TB + 40          # STOREW: 32 output words (4-aligned for dwordx4)
+    SH = V_Q              # 2k
+
+    def row_ptr():         # row pointer t lives in the kernarg segment at 40 + 8t
+        e('  s_lshl_b32 s16, s15, 3')
+        e('  s_add_u32 s16, s16, 40')
+        e('  s_load_dwordx2 s[30:31], s[0:1], s16')
+        e('  s_waitcnt lgkmcnt(0)')
+
+    def live_mask():       # lanes of ciphertexts g >= live: off for the row access
+        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
+        e(f'  v_cmp_gt_u32_e32 vcc, s28, v{V_TMP}')
+        e('  s_and_saveexec_b64 s[24:25], vcc')
+
+    def restore_exec():
+        e('  s_mov_b64 exec, s[24:25]')
+
+    def load_row_limbs(dst):
+        """row words -> Q radix-2^B limbs of this lane's quarter, into dst(j)"""
+        for i in range(8):
+            e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v{V_ROW}, s[30:31] offset:{16 * i}')
+        # word 32k+32 (lane 3: none -- load word 127 and clear it)
+        e(f'  v_add_u32_e32 v{V_TMP}, 0x80, v{V_ROW}')
+        e(f'  v_add_u32_e32 v{V_TMP + 1}, 0x7c, v{V_ROW}')
+        e(f'  v_cndmask_b32_e64 v{V_TMP}, v{V_TMP}, v{V_TMP + 1}, s[20:21]')
+        e(f'  global_load_dword v{W0 + 32}, v{V_TMP}, s[30:31]')
+        e(f'  v_bfe_u32 v{SH}, v{V_ROW}, 6, 3')
+        e(f'  v_and_b32_e32 v{SH}, 6, v{SH}')                    # 2k
+        e('  s_waitcnt vmcnt(0)')
+        e(f'  v_cndmask_b32_e64 v{W0 + 32}, v{W0 + 32}, 0, s[20:21]')
+        # funnel the stream down by 2k bits: bit 1026k of the row becomes bit 0
+        for i in range(32):
+            e(f'  v_alignbit_b32 v{W0 + i}, v{W0 + i + 1}, v{W0 + i}, v{SH}')
+        e(f'  v_lshrrev_b32_e32 v{W0 + 32}, v{SH}, v{W0 + 32}')
+        for j in range(Q):
+            a, sh = (B * j) >> 5, (B * j) & 31
+            if sh + B <= 32:
+                e(f'  v_bfe_u32 {dst(j)}, v{W0 + a}, {sh}, {B}')
+            else:
+                e(f'  v_alignbit_b32 {dst(j)}, v{W0 + a + 1}, v{W0 + a}, {sh}')
+                e(f'  v_and_b32_e32 {dst(j)}, {hex(MASK)}, {dst(j)}')
+
+    e('.Lloadw:')
+    row_ptr()
+    live_mask()
+    load_row_limbs(X)
+    restore_exec()
+    e('  s_branch .Lprog')
+
+    e('.Lmulw:')
+    row_ptr()
+    live_mask()
+    load_row_limbs(lambda j: f"v{A0 + j}")
+    restore_exec()
+    write_a(lambda j: f"v{A0 + j}")
+    e('  s_mov_b32 s19, 0')
+    e('  s_branch .Lmontmul')
+
+    # STOREW: X (< 2N) -> X mod N -> row words.
+    e('.Lstorew:')
+    row_ptr()
+    live_mask()
+    bo, fin, t1 = f"v{V_AI[0]}", f"v{V_AI[1]}", f"v{V_TMP}"
+    for j in range(Q):                         # D = X - N (this quarter), borrow-out bo in {0,-1}
+        e(f'  v_sub_u32_e32 v{D0 + j}, {X(j)}, {NV(j)}')
+        if j:
+            e(f'  v_add_u32_e32 v{D0 + j}, v{D0 + j}, {bo}')
+        e(f'  v_ashrrev_i32_e32 {bo}, 31, v{D0 + j}')
+        e(f'  v_and_b32_e32 v{D0 + j}, {hex(MASK)}, v{D0 + j}')
+    e(f'  v_mov_b32_e32 {fin}, 0')
+    lab = '.Lsw_borrow'
+    e(f'{lab}_loop:')
+    e(f'  v_cndmask_b32_e64 {t1}, 0, {bo}, s[20:21]')            # lane 3: borrow out of the number
+    e(f'  v_or_b32_e32 {fin}, {fin}, {t1}')
+    e('  s_nop 1')
+    e(f'  v_mov_b32_dpp {t1}, {bo} quad_perm:[0,0,1,2] {DPP}')
+    e(f'  v_cndmask_b32_e64 {bo}, {t1}, 0, s[22:23]')            # borrow into lane k from lane k-1
+    e(f'  v_cmp_ne_u32_e32 vcc, 0, {bo}')
+    e('  s_nop 4')
+    e(f'  s_cbranch_vccz {lab}_done')
+    for j in range(Q):
+        e(f'  v_add_u32_e32 v{D0 + j}, v{D0 + j}, {bo}')
+        e(f'  v_ashrrev_i32_e32 {bo}, 31, v{D0 + j}')
+        e(f'  v_and_b32_e32 v{D0 + j}, {hex(MASK)}, v{D0 + j}')
+    e(f'  s_branch {lab}_loop')
+    e(f'{lab}_done:')
+    e('  s_nop 1')
+    e(f'  v_mov_b32_dpp {t1}, {fin} quad_perm:[3,3,3,3] {DPP}')
+    e(f'  v_cmp_eq_u32_e32 vcc, 0, {t1}')                      # no borrow: X >= N -> X - N
+    for j in range(Q):
+        e(f'  v_cndmask_b32_e32 {X(j)}, {X(j)}, v{D0 + j}, vcc')
+    # own bit stream -> words U_i (bits [32i, 32i+32) of this quarter)
+    for i in range(32):
+        lo, hi = 32 * i, 32 * i + 31
+        j0, j1 = lo // B, min(hi // B, Q - 1)
+        e(f'  v_lshrrev_b32_e32 v{U0 + i}, {lo - B * j0}, {X(j0)}')
+        for j in range(j0 + 1, j1 + 1):
+            e(f'  v_lshl_or_b32 v{U0 + i}, {X(j)}, {B * j - lo}, v{U0 + i}')
+    # shift up by 2k and take the low 2k bits from the top of lane k-1's quarter
+    e(f'  v_bfe_u32 v{SH}, v{V_ROW}, 6, 3')
+    e(f'  v_and_b32_e32 v{SH}, 6, v{SH}')                        # 2k
+    e(f'  v_sub_u32_e32 {bo}, 31, v{SH}')                        # 31 - 2k
+    for i in range(31, 0, -1):
+        e(f'  v_lshrrev_b32_e32 {t1}, {bo}, v{U0 + i - 1}')
+        e(f'  v_lshrrev_b32_e32 {t1}, 1, {t1}')
+        e(f'  v_lshl_or_b32 v{U0 + i}, v{U0 + i}, v{SH}, {t1}')
+    e(f'  v_mov_b32_dpp {t1}, {X(Q - 1)} quad_perm:[0,0,1,2] {DPP}')
+    e(f'  v_sub_u32_e32 {bo}, {B}, v{SH}')                       # lane 0: shift 27 -> no bits
+    e(f'  v_lshrrev_b32_e32 {t1}, {bo}, {t1}')
+    e(f'  v_lshl_or_b32 v{U0}, v{U0}, v{SH}, {t1}')
+    for i in range(8):
+        e(f'  global_store_dwordx4 v{V_ROW}, v[{U0 + 4 * i}:{U0 + 4 * i + 3}], s[30:31] offset:{16 * i}')
+    e('  s_waitcnt vmcnt(0)')
+    restore_exec()
+    e('  s_branch .Lprog')
 
     def iteration(u):
         ai = f"v{V_AI[u % 2]}"
