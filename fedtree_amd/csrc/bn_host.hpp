@@ -97,7 +97,9 @@ inline int kernel_limbs_for_bits(int bits) { return kernel_shape_for_bits(bits).
 enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL = 4,
                      OP_ADDSLOT = 5, OP_ADDSMALL = 6,
                      // four-lane kernel only: canonical 128-word rows, kernarg row table entry t
-                     OP_LOADW = 7, OP_MULW = 8, OP_STOREW = 9 };
+                     OP_LOADW = 7, OP_MULW = 8, OP_STOREW = 9,
+                     // gathered rows: row idx[g] of rows[0], idx (int64) at rows[t]; idx < 0 -> 1
+                     OP_LOADWG = 10, OP_MULWG = 11 };
 
 struct Prog {
     std::vector<uint32_t> w;
@@ -112,6 +114,8 @@ struct Prog {
     void loadw(int t) { op(OP_LOADW, t); }
     void mulw(int t) { op(OP_MULW, t); montmuls += 1; }
     void storew(int t) { op(OP_STOREW, t); }
+    void loadwg(int t) { op(OP_LOADWG, t); }
+    void mulwg(int t) { op(OP_MULWG, t); montmuls += 1; }
     void end() { op(OP_END, 0); }
 
     // X <- X^(2^j - 1) (Montgomery domain) by the all-ones addition chain:

@@ -1107,10 +1107,17 @@ struct GatherProd {
         Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)K, k->n2);
         std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
         Prog p;
-        p.loadx(base);
-        for (int j = 1; j < K; j++) p.mul(base + j);
-        p.mul(SL_C0);
-        p.storex(SL_OUTP); p.end();
+        if (k->rowio) {               // rows[0] = source, rows[1..K] = index lists, rows[K+1] = output
+            p.loadwg(1);
+            for (int j = 1; j < K; j++) p.mulwg(1 + j);
+            p.mul(SL_C0);
+            p.storew(K + 1); p.end();
+        } else {
+            p.loadx(base);
+            for (int j = 1; j < K; j++) p.mul(base + j);
+            p.mul(SL_C0);
+            p.storex(SL_OUTP); p.end();
+        }
         mm = p.montmuls;
         prog_words = p.w.size();
         Prog blob; blob.w = p.w; blob.w.insert(blob.w.end(), rl.begin(), rl.end());
@@ -1131,6 +1138,14 @@ struct GatherProd {
         for (size_t off = 0; off < G; off += L) {
             size_t cnt = std::min((size_t)L, G - off);
             Lc.live = cnt;
+            if (k->rowio) {
+                const void *rows[K + 2];
+                rows[0] = src;
+                for (int j = 0; j < K; j++) rows[1 + j] = (const int64_t *)c->scratch.p + (size_t)j * G + off;
+                rows[K + 1] = dst + off * cw;
+                if ((rc = launch_dyn(Lc, c->io[3].p, mm, k->mn2, rows, K + 2))) return rc;
+                continue;
+            }
             for (int j = 0; j < K; j++)
                 pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(base + j), S, L, Lc.B,
                           (const int64_t *)c->scratch.p + (size_t)j * G + off);

@@ -519,7 +519,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
                       (5, '.Laddslot'), (6, '.Laddsmall'), (7, '.Lloadw'), (8, '.Lmulw'),
-                      (9, '.Lstorew')):
+                      (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -667,9 +667,13 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         e(f'  v_add_u32_e32 v{V_TMP + 1}, 0x7c, v{V_ROW}')
         e(f'  v_cndmask_b32_e64 v{V_TMP}, v{V_TMP}, v{V_TMP + 1}, s[20:21]')
         e(f'  global_load_dword v{W0 + 32}, v{V_TMP}, s[30:31]')
+        e('  s_waitcnt vmcnt(0)')
+        words_to_limbs(dst)
+
+    def words_to_limbs(dst):
+        """W0 .. W0+32 (row words 32k .. 32k+32) -> this lane's Q limbs"""
         e(f'  v_bfe_u32 v{SH}, v{V_ROW}, 6, 3')
         e(f'  v_and_b32_e32 v{SH}, 6, v{SH}')                    # 2k
-        e('  s_waitcnt vmcnt(0)')
         e(f'  v_cndmask_b32_e64 v{W0 + 32}, v{W0 + 32}, 0, s[20:21]')
         # funnel the stream down by 2k bits: bit 1026k of the row becomes bit 0
         for i in range(32):
@@ -694,6 +698,56 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     row_ptr()
     live_mask()
     load_row_limbs(lambda j: f"v{A0 + j}")
+    restore_exec()
+    write_a(lambda j: f"v{A0 + j}")
+    e('  s_mov_b32 s19, 0')
+    e('  s_branch .Lmontmul')
+
+    # Gathered rows: LOADWG / MULWG t read row idx[g] of the array at rows[0], idx an
+    # int64 array at rows[t] (one entry per ciphertext of the launch); idx < 0 -> 1.
+    def load_gather_limbs(dst):
+        e('  s_lshl_b32 s16, s15, 3')
+        e('  s_add_u32 s16, s16, 40')
+        e('  s_load_dwordx2 s[32:33], s[0:1], s16')                # idx array
+        e('  s_load_dwordx2 s[30:31], s[0:1], 40')                 # row base
+        e('  s_waitcnt lgkmcnt(0)')
+        live_mask()
+        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
+        e(f'  v_lshlrev_b32_e32 v{V_TMP}, 3, v{V_TMP}')
+        e(f'  global_load_dwordx2 v[{V_TMP}:{V_TMP + 1}], v{V_TMP}, s[32:33]')
+        e('  s_waitcnt vmcnt(0)')
+        e(f'  v_cmp_gt_i32_e32 vcc, 0, v{V_TMP + 1}')               # idx < 0
+        e('  s_and_saveexec_b64 s[34:35], vcc')
+        for j in range(Q):
+            e(f'  v_mov_b32_e32 {dst(j)}, 0')
+        e(f'  v_cndmask_b32_e64 {dst(0)}, 0, 1, s[22:23]')        # the integer 1
+        e('  s_andn2_b64 exec, s[34:35], exec')                     # live lanes with idx >= 0
+        e(f'  v_lshlrev_b64 v[{V_TMP}:{V_TMP + 1}], 9, v[{V_TMP}:{V_TMP + 1}]')
+        e(f'  v_and_b32_e32 v{V_AI[0]}, 0x180, v{V_ROW}')           # 128k
+        e(f'  v_add_co_u32_e32 v{V_TMP}, vcc, v{V_TMP}, v{V_AI[0]}')
+        e(f'  v_addc_co_u32_e32 v{V_TMP + 1}, vcc, 0, v{V_TMP + 1}, vcc')
+        e(f'  v_mov_b32_e32 v{V_AI[0]}, s31')
+        e(f'  v_add_co_u32_e32 v{V_TMP}, vcc, s30, v{V_TMP}')
+        e(f'  v_addc_co_u32_e32 v{V_TMP + 1}, vcc, v{V_AI[0]}, v{V_TMP + 1}, vcc')
+        for i in range(8):
+            e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v[{V_TMP}:{V_TMP + 1}], off offset:{16 * i}')
+        e(f'  v_mov_b32_e32 v{V_AI[0]}, 0x80')
+        e(f'  v_mov_b32_e32 v{V_AI[1]}, 0x7c')
+        e(f'  v_cndmask_b32_e64 v{V_AI[0]}, v{V_AI[0]}, v{V_AI[1]}, s[20:21]')
+        e(f'  v_add_co_u32_e32 v{V_AI[1]}, vcc, v{V_TMP}, v{V_AI[0]}')
+        e(f'  v_addc_co_u32_e32 v{V_AI[1] + 1}, vcc, 0, v{V_TMP + 1}, vcc')
+        e(f'  global_load_dword v{W0 + 32}, v[{V_AI[1]}:{V_AI[1] + 1}], off')
+        e('  s_waitcnt vmcnt(0)')
+        words_to_limbs(dst)
+        e('  s_mov_b64 exec, s[34:35]')
+
+    e('.Lloadwg:')
+    load_gather_limbs(X)
+    restore_exec()
+    e('  s_branch .Lprog')
+
+    e('.Lmulwg:')
+    load_gather_limbs(lambda j: f"v{A0 + j}")
     restore_exec()
     write_a(lambda j: f"v{A0 + j}")
     e('  s_mov_b32 s19, 0')

@@ -529,3 +529,56 @@ class HEParty:
         """hist_tree_builder.cpp:670-680: the larger child's histogram as
         father - computed (GHPair::operator-, one fused device op per bin)."""
         return father - computed
+
+
+# --------------------------------------------------------------------------
+# wire formats (fthe_wire.cpp): no device needed
+def ct_to_decimal(ct, threads=0):
+    """Ciphertext rows -> the reference's GHEncBatch decimal strings
+    (`stream << g_enc`, distributed_server.cpp:37-54)."""
+    lib = _lib.load()
+    ct = np.ascontiguousarray(ct, dtype=np.uint32)
+    cnt, words = ct.shape
+    buf = np.zeros(max(1, cnt * lib.fthe_decimal_max_len(words)), dtype=np.uint8)
+    offs = np.zeros(cnt + 1, dtype=np.uint64)
+    _lib.check(lib.fthe_ct_to_decimal(_ptr(ct), words, cnt, _ptr(buf), buf.nbytes, _ptr(offs), threads), "to_decimal")
+    raw = buf[: int(offs[-1])].tobytes()
+    return [raw[int(offs[i]):int(offs[i + 1])].decode() for i in range(cnt)]
+
+
+def ct_from_decimal(strings, words, threads=0):
+    """NTL::to_ZZ(str) of the receiving side (distributed_party.cpp:1267-1273)."""
+    lib = _lib.load()
+    enc = [s.encode() for s in strings]
+    offs = np.zeros(len(enc) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in enc]) if enc else []
+    buf = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).copy()
+    out = np.zeros((len(enc), words), dtype=np.uint32)
+    _lib.check(lib.fthe_ct_from_decimal(_ptr(buf), _ptr(offs), len(enc), words, _ptr(out), threads), "from_decimal")
+    return out
+
+
+def wire_encode(g, h=None):
+    """Binary "FTHW" frame of raw little-endian words."""
+    lib = _lib.load()
+    g = np.ascontiguousarray(g, dtype=np.uint32)
+    cnt, words = g.shape
+    hh = None if h is None else np.ascontiguousarray(h, dtype=np.uint32)
+    out = np.zeros(lib.fthe_wire_size(cnt, words, hh is not None), dtype=np.uint8)
+    ln = ctypes.c_size_t()
+    _lib.check(lib.fthe_wire_encode(_ptr(g), _ptr(hh), cnt, words, _ptr(out), out.nbytes, ctypes.byref(ln)), "wire_encode")
+    return out.tobytes()
+
+
+def wire_decode(frame, words):
+    lib = _lib.load()
+    buf = np.frombuffer(frame, dtype=np.uint8).copy()
+    cnt = ctypes.c_size_t()
+    lib.fthe_wire_decode(_ptr(buf), buf.nbytes, words, None, None, 0, ctypes.byref(cnt))
+    n = cnt.value
+    g = np.zeros((n, words), np.uint32)
+    h = np.zeros((n, words), np.uint32)
+    with_h = len(frame) >= 8 and (frame[6] & 1)
+    _lib.check(lib.fthe_wire_decode(_ptr(buf), buf.nbytes, words, _ptr(g), _ptr(h) if with_h else None, n,
+                                    ctypes.byref(cnt)), "wire_decode")
+    return (g, h) if with_h else (g, None)

@@ -165,6 +165,26 @@ int fthe_scan_segments_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, cons
 int fthe_scan_segments(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, const int64_t *seg_ptr,
                        size_t nseg, uint32_t *out);
 
+/* ---- ciphertext wire formats (host only; fthe_wire.cpp) --------------------
+ * Decimal: the reference's GHEncBatch strings (fedtree.proto:82-99), written
+ * by `stream << g_enc` (distributed_server.cpp:37-54, distributed_party.cpp:
+ * 1285-1300) and read by NTL::to_ZZ (distributed_party.cpp:1267-1273,
+ * distributed_server.cpp:1427-1433); byte-identical both ways.  Strings are
+ * concatenated in buf; offsets has count+1 entries (offsets[count] = total
+ * bytes; when buf_len is too small the call fails with FTHE_ERR_ARG and
+ * offsets[count] tells the size needed).  threads <= 0: all cores.
+ * Binary: the "FTHW" frame of raw little-endian words. */
+size_t fthe_decimal_max_len(int words);
+int fthe_ct_to_decimal(const uint32_t *ct, int words, size_t count, char *buf, size_t buf_len,
+                       size_t *offsets, int threads);
+int fthe_ct_from_decimal(const char *buf, const size_t *offsets, size_t count, int words,
+                         uint32_t *ct, int threads);
+size_t fthe_wire_size(size_t count, int words, int with_h);
+int fthe_wire_encode(const uint32_t *g, const uint32_t *h, size_t count, int words,
+                     uint8_t *out, size_t cap, size_t *len);
+int fthe_wire_decode(const uint8_t *in, size_t len, int words, uint32_t *g, uint32_t *h,
+                     size_t cap, size_t *count);
+
 /* ---- fixed-point codec (common.h:81-86,127-128,140-143) ------------------- */
 int fthe_encode_fixed_dev(fthe_ctx *ctx, const float *x, size_t count, uint64_t *m);
 int fthe_decode_fixed_dev(fthe_ctx *ctx, const uint64_t *m, size_t count, float *x);
