@@ -247,7 +247,26 @@ def main():
         pl.add_batch(ch[:nh], ch[nh:2 * nh])
         dt = time.perf_counter() - t0
         secondary["e2e_host_add_per_s"] = round(nh / dt)
-        del ch
+        # wire formats (host): the reference's decimal GHEncBatch strings vs the binary FTHW frame
+        from fedtree_amd.paillier import ct_from_decimal, ct_to_decimal, wire_decode, wire_encode
+        nw_ = min(ne, 1 << 16)
+        sample = ch[:nw_]
+        t0 = time.perf_counter()
+        strs = ct_to_decimal(sample, threads=a.cpu_threads)
+        t_enc = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        back = ct_from_decimal(strs, sample.shape[1], threads=a.cpu_threads)
+        t_dec = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        fr = wire_encode(sample)
+        g_, _ = wire_decode(fr, sample.shape[1])
+        t_bin = time.perf_counter() - t0
+        secondary["wire"] = {"ciphertexts": nw_, "threads": a.cpu_threads,
+                             "decimal_encode_per_s": round(nw_ / t_enc), "decimal_decode_per_s": round(nw_ / t_dec),
+                             "decimal_bytes_per_ct": round(sum(len(x) for x in strs) / nw_, 1),
+                             "binary_roundtrip_per_s": round(nw_ / t_bin), "binary_bytes_per_ct": sample.shape[1] * 4,
+                             "roundtrip_ok": bool(np.array_equal(back, sample) and np.array_equal(g_, sample))}
+        del ch, strs, back, fr, g_
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_sample, a.cpu_threads)

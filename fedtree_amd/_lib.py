@@ -8,7 +8,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfthe.so")
+LIB_PATH = os.environ.get("FTHE_LIB") or os.path.join(_HERE, "libfthe.so")   # FTHE_LIB: A/B builds only
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fthe.h")
 
 FTHE_OK = 0

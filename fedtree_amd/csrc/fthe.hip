@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <thread>
 #include <vector>
 #include <fcntl.h>
 #include <unistd.h>
@@ -731,6 +732,21 @@ int end_call(fthe_ctx *c, Launch &Lc) {
 // chunk i's output drained while the kernels of the neighbouring chunk run,
 // so a host-to-host call costs ~max(compute, PCIe + host memcpy) rather than
 // their sum.  Caller buffers that are already page-locked are DMA'd directly.
+// Large host copies (pageable caller buffer <-> pinned staging) on several cores.
+void par_memcpy(void *dst, const void *src, size_t n) {
+    const size_t grain = (size_t)16 << 20;
+    int nt = (int)std::min<size_t>(8, n / grain);
+    if (nt <= 1) { memcpy(dst, src, n); return; }
+    std::vector<std::thread> th;
+    size_t per = (n + nt - 1) / nt;
+    for (int t = 1; t < nt; t++) {
+        size_t b = t * per, e = std::min(n, b + per);
+        if (b < e) th.emplace_back([=] { memcpy((char *)dst + b, (const char *)src + b, e - b); });
+    }
+    memcpy(dst, src, std::min(n, per));
+    for (auto &x : th) x.join();
+}
+
 struct HostPipe {
     struct In { const uint8_t *h; uint8_t *d; size_t row; bool pinned; };
     struct Out { uint8_t *h; const uint8_t *d; size_t row; bool pinned; };
@@ -763,7 +779,7 @@ struct HostPipe {
             if (in[i].pinned) {
                 HIPOK(hipMemcpyAsync(in[i].d + o, in[i].h + o, b, hipMemcpyHostToDevice, c->copy));
             } else {
-                memcpy(st, in[i].h + o, b);
+                par_memcpy(st, in[i].h + o, b);
                 HIPOK(hipMemcpyAsync(in[i].d + o, st, b, hipMemcpyHostToDevice, c->copy));
                 st += b;
             }
@@ -778,7 +794,7 @@ struct HostPipe {
         for (int i = 0; i < nout; i++) {
             if (out[i].pinned) continue;
             const size_t b = pend_cnt * out[i].row;
-            memcpy(out[i].h + pend_off * out[i].row, st, b);
+            par_memcpy(out[i].h + pend_off * out[i].row, st, b);
             st += b;
         }
         pend = false;

@@ -41,7 +41,12 @@ Kernel arguments (kernarg segment):
     40 u64 rows[16]: row-array pointers of the row I/O ops (four-lane kernel only)
 """
 import argparse
+import os
 import sys
+
+# q = T0 n' mod 2^B from the low word of a v_mad_u64_u32 (full rate) instead of
+# v_mul_lo_u32 (quarter rate); FTHE_GEN_QLO=1 restores the latter (A/B builds)
+Q_VIA_MAD = not os.environ.get("FTHE_GEN_QLO")
 
 
 def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
@@ -165,7 +170,11 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
         for i in range(S):
             if i == 0:
                 mad(0, X(0), X(0))
-            e(f'  v_mul_lo_u32 {q}, {Rlo(i)}, s12')
+            # q = T_i n' mod 2^B: the low word of a (full-rate) 32x32->64 multiply-add
+            if Q_VIA_MAD:
+                e(f'  v_mad_u64_u32 {tmp}, vcc, {Rlo(i)}, s12, 0')
+            else:
+                e(f'  v_mul_lo_u32 v{V_TMP}, {Rlo(i)}, s12')
             e(f'  v_lshlrev_b32_e32 {d}, 1, {X(i)}')
             cnt = 0
             if i > 0:
@@ -175,9 +184,9 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
                 mad(i + j, d, X(j))
                 cnt += 1
                 if cnt == 2:
-                    e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+                    e(f'  v_and_b32_e32 {q}, {hex(MASK)}, v{V_TMP}')
             if cnt < 2:
-                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, v{V_TMP}')
             for j in range(S):
                 mad(i + j, q, f"s{SN + j}")
                 if j == 3:
@@ -300,9 +309,12 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
         for j in range(S):
             e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {ai}, {X(j)}, {T(u + j)}')
             if j == 3:
-                e(f'  v_mul_lo_u32 {q}, {Tlo(u)}, s12')
+                if Q_VIA_MAD:
+                    e(f'  v_mad_u64_u32 v[{V_TMP}:{V_TMP + 1}], vcc, {Tlo(u)}, s12, 0')
+                else:
+                    e(f'  v_mul_lo_u32 v{V_TMP}, {Tlo(u)}, s12')
             if j == 6:
-                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, v{V_TMP}')
             if j == 8:
                 # prefetch next a limb (next iteration / next trip / tail)
                 e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * 256}')
@@ -818,9 +830,12 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         for j in range(Q):
             e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {ai}, {X(j)}, {T(u + j)}')
             if j == 3:
-                e(f'  v_mul_lo_u32 {q}, {Tlo(u)}, s12')
+                if Q_VIA_MAD:
+                    e(f'  v_mad_u64_u32 {tmp}, vcc, {Tlo(u)}, s12, 0')
+                else:
+                    e(f'  v_mul_lo_u32 v{V_TMP}, {Tlo(u)}, s12')
             if j == 6:
-                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, {q}')
+                e(f'  v_and_b32_e32 {q}, {hex(MASK)}, v{V_TMP}')
             if j == 9:
                 e(f'  v_mov_b32_dpp {q}, {q} quad_perm:[0,0,0,0] {DPP}')
             if j == 11:

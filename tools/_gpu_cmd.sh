@@ -1,3 +1,5 @@
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r01c_ops_trace -o ops -- python3 tools/prof_ops.py --n 393216 > gpurun_out/r01c_ops.log 2>&1
+for i in 1 2; do
+  timeout -k 10 200 python tools/ab_rates.py >> gpurun_out/ab.jsonl 2>>gpurun_out/ab.err || exit 1
+  FTHE_LIB=build/ab/libfthe_qlo.so timeout -k 10 200 python tools/ab_rates.py >> gpurun_out/ab.jsonl 2>>gpurun_out/ab.err || exit 1
+done

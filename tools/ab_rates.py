@@ -1,0 +1,44 @@
+"""A/B helper: device-resident rates of one library build (FTHE_LIB selects it).
+
+  FTHE_LIB=build/ab/libX.so python tools/ab_rates.py [--n 786432]
+Prints one JSON line: CRT encrypt, add and sub rates (best of reps)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=786432)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    pl = Paillier(dev).keygen(2048, seed=20261015)
+    cw = 2 * pl.n_words
+    m = torch.randint(0, 2**62, (a.n,), dtype=torch.int64, device="cuda")
+    c = torch.empty((a.n, cw), dtype=torch.int32, device="cuda")
+    o = torch.empty_like(c)
+
+    def best(fn, units):
+        fn(); dev.sync()
+        t = 1e30
+        for _ in range(a.reps):
+            fn(); dev.sync()
+            t = min(t, dev.last_kernel_ms())
+        return round(units / (t * 1e-3))
+
+    res = {"lib": os.environ.get("FTHE_LIB", "default")}
+    res["encrypt"] = best(lambda: pl.encrypt_u64_dev(m, c, seed=1), a.n)
+    res["add"] = best(lambda: pl.add_dev(c, c, o), a.n)
+    k = a.n // 8
+    res["sub"] = best(lambda: pl.sub_dev(c[:k], c[k:2 * k], o[:k]), k)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
