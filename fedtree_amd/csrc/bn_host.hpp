@@ -99,11 +99,16 @@ enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL
                      // four-lane kernel only: canonical 128-word rows, kernarg row table entry t
                      OP_LOADW = 7, OP_MULW = 8, OP_STOREW = 9,
                      // gathered rows: row idx[g] of rows[0], idx (int64) at rows[t]; idx < 0 -> 1
-                     OP_LOADWG = 10, OP_MULWG = 11 };
+                     OP_LOADWG = 10, OP_MULWG = 11,
+                     // one-lane kernels only: LDS-DMA prefetch of the next multiplier
+                     OP_PREFA = 12, OP_MULA = 13 };
 
 struct Prog {
     std::vector<uint32_t> w;
     double montmuls = 0;   // Montgomery products per lane (roofline accounting)
+    // one-lane kernels: pow()/pow_ones() prefetch each multiplier into LDS
+    // (PREFA) ahead of the squarings that precede it, then MULA
+    bool lds_a = false;
     void op(Op o, uint32_t a) { w.push_back(o); w.push_back(a); }
     void loadx(int s) { op(OP_LOADX, s); }
     void storex(int s) { op(OP_STOREX, s); }
@@ -115,6 +120,13 @@ struct Prog {
     void mulw(int t) { op(OP_MULW, t); montmuls += 1; }
     void storew(int t) { op(OP_STOREW, t); }
     void loadwg(int t) { op(OP_LOADWG, t); }
+    void prefa(int s) { op(OP_PREFA, s); }
+    void mula() { op(OP_MULA, 0); montmuls += 1; }
+    // multiply by slot s, the squarings `n` before it (prefetch form when lds_a)
+    void sqr_mul(int n, int s) {
+        if (lds_a) { prefa(s); sqr(n); mula(); }
+        else { sqr(n); mul(s); }
+    }
     void mulwg(int t) { op(OP_MULWG, t); montmuls += 1; }
     void end() { op(OP_END, 0); }
 
@@ -128,8 +140,8 @@ struct Prog {
         int top = 31 - __builtin_clz(j);
         unsigned a = 1;
         for (int b = top - 1; b >= 0; b--) {
-            storex(tmp_slot); sqr((int)a); mul(tmp_slot); a *= 2;          // 2^(2a)-1
-            if ((j >> b) & 1) { sqr(1); mul(base_slot); a += 1; }         // 2^(a+1)-1
+            storex(tmp_slot); sqr_mul((int)a, tmp_slot); a *= 2;          // 2^(2a)-1
+            if ((j >> b) & 1) { sqr_mul(1, base_slot); a += 1; }          // 2^(a+1)-1
         }
     }
 
@@ -145,8 +157,12 @@ struct Prog {
         storex(tbl0);
         sqr(1);
         storex(sq_slot);
+        if (lds_a) prefa(sq_slot);      // x^2 stays in the LDS A buffer for the whole table
         loadx(tbl0);
-        for (int k = 1; k < ntab; k++) { mul(sq_slot); storex(tbl0 + k); }
+        for (int k = 1; k < ntab; k++) {
+            if (lds_a) mula(); else mul(sq_slot);
+            storex(tbl0 + k);
+        }
         long i = (long)nb - 1;
         auto bit = [&](long b) { return mpz_tstbit(e, (mp_bitcnt_t)b); };
         auto window = [&](long top, long &low, unsigned &val) {
@@ -164,8 +180,7 @@ struct Prog {
             if (!bit(i)) { pend++; i--; continue; }
             window(i, low, v);
             pend += (int)(i - low + 1);
-            sqr(pend); pend = 0;
-            mul(tbl0 + (int)((v - 1) / 2));
+            sqr_mul(pend, tbl0 + (int)((v - 1) / 2)); pend = 0;
             i = low - 1;
         }
         sqr(pend);

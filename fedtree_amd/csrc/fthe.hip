@@ -208,6 +208,12 @@ enum Slot : int {
 
 static int nslots_for(const fthe_key *k) { return SL_TAB + k->tabn_max; }
 
+// One-lane kernels prefetch multipliers into LDS (PREFA/MULA); FTHE_NO_LDSDMA=1 turns it off (A/B).
+static bool lds_prefetch(const Shape &sh) {
+    static const bool off = getenv("FTHE_NO_LDSDMA") != nullptr;
+    return sh.lanes == 1 && !off;
+}
+
 // ---------------------------------------------------------------------------
 extern "C" int fthe_version(void) { return 100; }
 
@@ -367,6 +373,7 @@ static int key_finish(fthe_key *k) {
         k->c_n2 = k->add_const(M.limbs(k->n2));
         // encrypt: X = r R; X^n; (1 + m n) X  (paillier.cpp:135-137 with g^m = 1 + m n)
         Prog e;
+        e.lds_a = lds_prefetch(k->sn2);
         k->w_pub = best_window(k->n.bits());
         e.loadx(SL_IN0); e.mul(SL_C0);
         e.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
@@ -382,6 +389,7 @@ static int key_finish(fthe_key *k) {
         // sub: a * b^(2^64-1) mod n^2 (GHPair::operator-, common.h:311-317): b R; (b R)^(2^64-1)
         // in the Montgomery domain by the all-ones chain; times a (plain) leaves the plain product
         Prog sb;
+        sb.lds_a = lds_prefetch(k->sn2);
         sb.loadx(SL_IN1); sb.mul(SL_C0); sb.pow_ones(64, SL_T0, SL_T1); sb.mul(SL_IN0);
         sb.storex(SL_OUTP); sb.end();
         k->pr_sub = k->add_prog(sb);
@@ -454,6 +462,7 @@ static int key_finish(fthe_key *k) {
             k->tabn_max = std::max(k->tabn_max, std::max(1 << (wA - 1), 1 << (wB - 1)));
             for (int side = 0; side < 2; side++) {
                 Prog a;                                          // slots in the small region
+                a.lds_a = lds_prefetch(k->sp1);
                 a.loadx(SL_IN1); a.mul(side ? SL_C3 : SL_C1);    // r_hi R^2
                 a.storex(SL_T0);
                 a.loadx(SL_IN0); a.mul(side ? SL_C2 : SL_C0);    // r_lo R
@@ -463,6 +472,7 @@ static int key_finish(fthe_key *k) {
                 a.storex(side ? SL_OUTQ : SL_OUTP); a.end();
                 (side ? k->pr_encA_q : k->pr_encA_p) = k->add_prog(a);
                 Prog e;                                          // slots in the P^2 region
+                e.lds_a = lds_prefetch(sh);
                 e.loadx(side ? SL_T4 : SL_T3); e.mul(side ? SL_C2 : SL_C0);   // y R mod P^2
                 e.pow(side ? k->q : k->p, SL_TAB, SL_SQ, wB);     // y^P R = r^n R
                 e.storex(SL_SAVED);
@@ -505,6 +515,7 @@ static int key_finish(fthe_key *k) {
         k->tabn_max = std::max(k->tabn_max, 1 << (k->w_dec - 1));
         for (int side = 0; side < 2; side++) {
             Prog d;
+            d.lds_a = lds_prefetch(sh);
             d.loadx(SL_IN1); d.mul(side ? SL_C3 : SL_C1);        // c_hi R^2  (= Montgomery of c_hi R)
             d.storex(SL_T0);
             d.loadx(SL_IN0); d.mul(side ? SL_C2 : SL_C0);        // c_lo R
@@ -1321,6 +1332,7 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     const bool rowio = k->rowio;
     Prog p;
+    p.lds_a = lds_prefetch(k->sn2);
     if (e == 0) {
         p.loadx(SL_C1);                 // x^0 = 1
     } else {

@@ -30,6 +30,8 @@ Ops (uint32 pairs, read with s_load from the program buffer):
     4 MUL    slot   A <- slot ; X <- MontMul(A, X)
     5 ADDSLOT slot  X <- X + slot          (integer add, limbs renormalised)
     6 ADDSMALL k    X <- X + k             (k < 2^B)
+   12 PREFA  slot   LDS A buffer <- slot, asynchronously (LDS-DMA)
+   13 MULA   -      X <- MontMul(A buffer, X) after the PREFA landed
 
 Slot memory: slot s, limb k, lane g at  slots + s*slot_stride + k*L*4 + g*4
 (limb-major, lane-interleaved: every global access is fully coalesced).
@@ -123,6 +125,7 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
     e(f'  v_mul_u32_u24_e32 v{V_LDSA}, {hex(lds_per_wave)}, v{V_LDSA}')
     e(f'  v_and_b32_e32 v{V_Q}, 63, v{V_TID}')
     e(f'  v_lshl_add_u32 v{V_LDSA}, v{V_Q}, 2, v{V_LDSA}')
+    e(f'  v_readfirstlane_b32 s13, v{V_LDSA}')       # this wave's A buffer (LDS-DMA base)
     e('  s_waitcnt lgkmcnt(0)')
 
     # -- op dispatcher
@@ -132,7 +135,7 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
     e('  s_addc_u32 s7, s7, 0')
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
-                      (5, '.Laddslot'), (6, '.Laddsmall')):
+                      (5, '.Laddslot'), (6, '.Laddsmall'), (12, '.Lprefa'), (13, '.Lmula')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -277,6 +280,27 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
             e('  s_waitcnt lgkmcnt(0)')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_mov_b32 s19, 0')      # after the product: back to the dispatcher
+    e('  s_branch .Lmontmul')
+
+    # PREFA slot: the A operand of the next MULA goes slot -> LDS A buffer by
+    # LDS-DMA (global_load_lds: wave base in M0 + 4*lane, no VGPRs) and is left
+    # in flight across the squarings that precede the multiply (they never touch
+    # LDS).  MULA: wait for it, multiply; the buffer keeps A for further MULAs.
+    e('.Lprefa:')
+    slot_addr()
+    e('  s_mov_b32 m0, s13')
+    e('  s_nop 0')
+    for k in range(S):
+        e(f'  global_load_lds_dword v{V_GOFF}, s[16:17]')
+        if k != S - 1:
+            step_addr()
+            e('  s_add_u32 m0, m0, 0x100')
+            e('  s_nop 0')
+    e('  s_branch .Lprog')
+
+    e('.Lmula:')
+    e('  s_waitcnt vmcnt(0)')
+    e('  s_mov_b32 s19, 0')
     e('  s_branch .Lmontmul')
 
     # SQR: count in s15.  Fully unrolled Montgomery squaring: a = X is in
