@@ -49,6 +49,9 @@ import sys
 # q = T0 n' mod 2^B from the low word of a v_mad_u64_u32 (full rate) instead of
 # v_mul_lo_u32 (quarter rate); FTHE_GEN_QLO=1 restores the latter (A/B builds)
 Q_VIA_MAD = not os.environ.get("FTHE_GEN_QLO")
+# four-lane kernel: accumulator window as a register ring (no window moves);
+# FTHE_GEN_NORING=1 restores the sliding window (A/B builds)
+QUAD_RING = not os.environ.get("FTHE_GEN_NORING")
 
 
 def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
@@ -488,14 +491,16 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     assert NVGPR <= 256, NVGPR
     NSGPR = 40
 
+    # window position k -> register pair k mod NT (a ring in the ring form)
     def T(k):
+        k %= NT
         return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
 
     def Tlo(k):
-        return f"v{TB + 2 * k}"
+        return f"v{TB + 2 * (k % NT)}"
 
     def Thi(k):
-        return f"v{TB + 2 * k + 1}"
+        return f"v{TB + 2 * (k % NT) + 1}"
 
     def X(k):
         return f"v{XB + k}"
@@ -885,20 +890,28 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         e(f'  v_mov_b64_e32 {T(k)}, 0')
     e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
     e('  s_waitcnt lgkmcnt(0)')
-    if NTRIPS > 0:
-        e(f'  s_mov_b32 s18, {NTRIPS}')
+    # trips of STEP iterations: ring form = one full turn of the NT-pair ring
+    # (window positions wrap onto the same registers, nothing moves); sliding
+    # form = U iterations then a Q-pair window move
+    STEP = NT if QUAD_RING else U
+    assert STEP % 2 == 0                       # a_i double-buffer parity across trips
+    NTRIP, TL = S // STEP, S % STEP
+    if NTRIP > 0:
+        e(f'  s_mov_b32 s18, {NTRIP}')
         e('.Ltrip:')
-        for u in range(U):
+        for u in range(STEP):
             iteration(u)
-        for k in range(Q):
-            e(f'  v_mov_b64_e32 {T(k)}, {T(k + U)}')
-        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(U * 64)}, v{V_LDSI}')
+        if not QUAD_RING:
+            for k in range(Q):
+                e(f'  v_mov_b64_e32 {T(k)}, {T(k + U)}')
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(STEP * 64)}, v{V_LDSI}')
         e('  s_sub_u32 s18, s18, 1')
         e('  s_cmp_lg_u32 s18, 0')
         e('  s_cbranch_scc1 .Ltrip')
-    for u in range(TAIL):
+    for u in range(TL):
         iteration(u)
-    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIPS * U * 64)}, v{V_LDSI}')    # back to the column base
+    TAIL = TL
+    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * STEP * 64)}, v{V_LDSI}')    # back to the column base
     # normalise T[TAIL .. TAIL+Q-1] (64-bit columns) into X, then across lanes
     e(f'  v_mov_b64_e32 {tmp}, 0')
     for k in range(Q):
