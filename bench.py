@@ -42,6 +42,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
+PMC_FILE = "r01b_pmc.json"
 
 
 def parse():
@@ -180,12 +181,14 @@ def main():
         lib.fthe_prof_variant(dev.ctx, S, ctypes.byref(vms), ctypes.byref(vn))
         if vn.value:
             roof["avg_expo_launch_ms_by_kernel"][f"fthe_montprog_s{S}"] = round(vms.value / vn.value, 3)
-    prof_hbm = os.path.join(ROOT, "profiles", "r01_montprog_pmc.json")
+    # HBM traffic per full-chunk s74 launch from the committed PMC passes
+    # (tools/pmc_round.sh; 2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section)
+    pmc = {}
+    prof_hbm = os.path.join(ROOT, "profiles", PMC_FILE)
     if os.path.exists(prof_hbm):
-        try:
-            roof["traffic"] = json.load(open(prof_hbm)).get("hbm_bytes_per_launch")
-        except Exception:
-            pass
+        pmc = json.load(open(prof_hbm))
+        roof["traffic"] = pmc.get("enc", {}).get("fthe_montprog_s74", {}).get("hbm_bytes_per_launch")
+        roof["traffic_source"] = f"profiles/{PMC_FILE} (s74 full-chunk launch)"
 
     secondary = {}
     if rank == 0 and not a.no_secondary:
@@ -203,7 +206,14 @@ def main():
         pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
         pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
         dev.sync()
-        secondary["p2048_add_per_s"] = round(na / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        add_s = lib.fthe_last_kernel_ms(dev.ctx) * 1e-3
+        secondary["p2048_add_per_s"] = round(na / add_s)
+        # the add kernel's HBM side (north star): algorithmic bytes (2 rows in, 1 out, 512 B each)
+        # over the live launch time, and the PMC-measured bytes of a full-chunk launch
+        pk = pmc.get("add", {}).get("fthe_montprog_s152", {})
+        secondary["p2048_add_hbm"] = {"algorithmic_GBps": round(na * 1536 / add_s / 1e9, 1),
+                                      "pmc_GBps": pk.get("hbm_GBps"), "pmc_VALUBusy": pk.get("VALUBusy"),
+                                      "peak_GBps": 8000, "bound": "valu (2 Montgomery products of 4096 bits per add)"}
         del o
         # configs[3]: 8-party merge of 256 x 4096 bins x {g, h} (hist_tree_builder.cpp:1015-1058)
         bins, parties = 2 * 256 * 4096, 8

@@ -98,8 +98,66 @@ def pmc(dirs, out):
     print(json.dumps(res, indent=1))
 
 
+
+
+def pmc_round(tag, out):
+    """Summary of tools/pmc_round.sh TAG: per workload (enc, add, kway) and montprog
+    kernel, the mean counters of its dominant dispatches (>= 90% of the largest value: the
+    full-chunk launches), HBM bytes per launch = 2*FETCH_SIZE + WRITE_SIZE
+    (KiB; gfx950 FETCH_SIZE counts half of a 16-B/lane streaming read,
+    MI355X_MICROARCH.md HBM section) and the launch duration from the ops kernel
+    trace (add, kway) or the bench trace (enc) for the achieved GB/s."""
+    res = {}
+    for w in ("enc", "add", "kway"):
+        per = {}
+        for t in ("fetch", "write", "vb", "occ", "sq"):
+            for f in glob.glob(f"gpurun_out/{tag}_pmc_{w}_{t}/**/*counter_collection.csv", recursive=True):
+                acc = {}
+                for r in csv.DictReader(open(f)):
+                    kn = r["Kernel_Name"]
+                    if not kn.startswith("fthe_montprog"):
+                        continue
+                    key = (kn, r["Dispatch_Id"], r["Counter_Name"])
+                    acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
+                for (kn, _, cn), v in acc.items():
+                    per.setdefault(kn, {}).setdefault(cn, []).append(v)
+        wr = {}
+        for kn, cs in per.items():
+            d = {}
+            for cn, v in cs.items():
+                top = max(v)
+                heavy = [x for x in v if x >= 0.9 * top] if top > 0 else v     # full-size launches
+                d[cn] = round(sum(heavy) / len(heavy), 3)
+            if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+                d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+            wr[kn] = d
+        res[w] = wr
+    # launch durations of the s152 row-I/O kernels (ops trace: add launches first, then kway)
+    tr = glob.glob(f"gpurun_out/{tag}_ops_trace/*kernel_trace.csv")
+    if tr:
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                for r in csv.DictReader(open(tr[0])) if r["Kernel_Name"] == "fthe_montprog_s152"]
+        # prof_ops --n 1048576 --ops add,kway: 11 add chunks (98,304 rows) then 11 kway chunks
+        add, kway = durs[:10], durs[11:21]
+        for w, ds, units in (("add", add, 98304), ("kway", kway, 98304)):
+            if ds and "fthe_montprog_s152" in res[w]:
+                k = res[w]["fthe_montprog_s152"]
+                ms = sum(ds) / len(ds)
+                k["full_chunk_launch_ms"] = round(ms, 4)
+                k["rows_out_per_launch"] = units
+                if "hbm_bytes_per_launch" in k:
+                    k["hbm_GBps"] = round(k["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
+                    k["hbm_frac_of_8TBps"] = round(k["hbm_bytes_per_launch"] / (ms * 1e-3) / 8e12, 4)
+                ins = 3 if w == "add" else 9       # rows read + written per output (add: x, y, out; kway: 8 in, 1 out)
+                k["algorithmic_bytes_per_launch"] = units * 512 * ins
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "trace":
+    if sys.argv[1] == "pmcround":
+        pmc_round(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "trace":
         (trace_csv if sys.argv[2].endswith(".csv") else trace)(sys.argv[2], sys.argv[3])
     else:
         pmc(sys.argv[2:-1], sys.argv[-1])
