@@ -200,6 +200,31 @@ def main():
         secondary["crt_decrypt_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
         ok = torch.equal(low, m[:nd])
         secondary["decrypt_roundtrip_ok"] = bool(ok)
+        # public-key encrypt (a party without the factorization, party.h:118-142) and the
+        # opt-in fixed-base randomizer (r = h^alpha, include/fthe.h FTHE_ENC_FIXED_BASE; not
+        # the reference's uniform-r algorithm, so never the headline `value`)
+        npub = min(2 * P, 1 << 18)
+        pl.encrypt_u64_dev(m[:npub], c[:npub], seed=5, public=True)
+        dev.sync()
+        secondary["public_encrypt_per_s"] = round(npub / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        t0 = time.perf_counter()
+        pl.set_fixed_base(None)
+        fb_build_s = time.perf_counter() - t0
+        nfb = min(2 * P, 1 << 21)
+        cfb = torch.empty((nfb, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+        fbr = {"table_build_s": round(fb_build_s, 3)}
+        for name, pub in (("crt_encrypt_per_s", False), ("public_encrypt_per_s", True)):
+            pl.encrypt_u64_dev(m[:nfb], cfb, seed=6, public=pub, fixed_base=True)
+            dev.sync()
+            fbr[name] = round(nfb / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        lowfb = torch.empty(nfb, dtype=torch.int64, device=f"cuda:{local}")
+        pl.decrypt_u64_dev(cfb, lowfb)
+        dev.sync()
+        fbr["decrypt_roundtrip_ok"] = bool(torch.equal(lowfb, m[:nfb]))
+        fbr["note"] = ("opt-in FTHE_ENC_FIXED_BASE: c = (1+mn) hs^alpha, hs = h^n mod n^2, alpha from the device "
+                       "CSPRNG; 8-bit-window tables; not bit-comparable with the reference (no r)")
+        secondary["fixed_base"] = fbr
+        del cfb, lowfb
         # ciphertext adds (x*y mod n^2, 4096-bit n^2 on the four-lane kernel), device-resident
         na = min(2 * P, 1 << 20)
         o = torch.empty((na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")

@@ -101,7 +101,11 @@ enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL
                      // gathered rows: row idx[g] of rows[0], idx (int64) at rows[t]; idx < 0 -> 1
                      OP_LOADWG = 10, OP_MULWG = 11,
                      // one-lane kernels only: LDS-DMA prefetch of the next multiplier
-                     OP_PREFA = 12, OP_MULA = 13 };
+                     OP_PREFA = 12, OP_MULA = 13,
+                     // fixed-base tables gathered by a per-lane digit (rows[0] table,
+                     // rows[1] u8 digits [window][L]); one-lane: radix-2^B entries,
+                     // four-lane: canonical 128-word rows
+                     OP_LOADGD = 14, OP_MULGD = 15 };
 
 struct Prog {
     std::vector<uint32_t> w;
@@ -128,6 +132,8 @@ struct Prog {
         else { sqr(n); mul(s); }
     }
     void mulwg(int t) { op(OP_MULWG, t); montmuls += 1; }
+    void loadgd(int j) { op(OP_LOADGD, j); }
+    void mulgd(int j) { op(OP_MULGD, j); montmuls += 1; }
     void end() { op(OP_END, 0); }
 
     // X <- X^(2^j - 1) (Montgomery domain) by the all-ones addition chain:

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <random>
@@ -168,6 +169,7 @@ struct fthe_key {
         if (d_consts) hipFree(d_consts);
         if (d_progs) hipFree(d_progs);
         if (d_nwords) hipFree(d_nwords);
+        for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) hipFree(p);
     }
     // constant handles
     int add_const(const std::vector<uint32_t> &limbs) {
@@ -197,6 +199,22 @@ struct fthe_key {
     bool rowio = false;
     PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
+
+    // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
+    // r^n = hs^alpha with hs = h^n mod n^2 for one random h per key: 8-bit-window
+    // tables entry[j][d] = hs^(d 256^j) (Montgomery form) turn the exponentiation
+    // into one gathered product per window (no squarings).
+    struct FixedBase {
+        bool ready = false;
+        Mpz h, hs;
+        int nwin_pub = 0, nwin_crt = 0;   // 8-bit windows of alpha: public / per prime
+        int ew_pub = 0, ew_crt = 0;       // words per table entry
+        bool pub = false, pub_rows = false;
+        uint32_t *d_tab_pub = nullptr, *d_tab_p = nullptr, *d_tab_q = nullptr, *d_prog = nullptr;
+        size_t off_pub = 0, off_p = 0, off_q = 0;
+        double mm_pub = 0, mm_crt = 0;
+    } fb;
+    std::mutex fb_mu;
 };
 
 // slot numbering shared by all programs
@@ -708,6 +726,13 @@ struct Launch {
         mm += ph.mm * (double)live;
         return FTHE_OK;
     }
+    int prog_raw(const uint32_t *p, double pmm, const DevMod &mod, const void *const *rows, int nrows) {
+        if (mod.m.S != S) return FTHE_ERR_ARG;
+        int rc = launch_montprog(c, base, S, L, p, mod, pmm, live, rows, nrows);
+        if (rc) return rc;
+        mm += pmm * (double)live;
+        return FTHE_OK;
+    }
     void fill(int s, int h) {
         hipLaunchKernelGGL(k_fill_const, grid(), dim3(256), 0, c->stream, k->cst(h), slot(s), S, L);
     }
@@ -864,12 +889,15 @@ struct HostPipe {
 
 // ---------------------------------------------------------------------------
 // Encrypt
+static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *alpha,
+                           int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe);
 static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r, int r_words,
                         uint64_t rng_seed, uint32_t *out, int flags, HostPipe *pipe) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
-    if (r && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
+    if (r && !(flags & FTHE_ENC_FIXED_BASE) && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
     bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
     if (!crt && !k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (flags & FTHE_ENC_FIXED_BASE) return encrypt_fb_impl(k, c, m, count, r, r_words, rng_seed, out, crt, pipe);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, nslots_for(k), crt ? k->spq : k->sn2);
     if (rc) return rc;
@@ -938,6 +966,232 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
                                S, L, cnt, out + off * cw, cw, Lc.B);
         }
         Lc.mm += L1.mm; L1.mm = 0;
+        if (pipe && (rc = pipe->after(off, cnt))) return rc;
+    }
+    return end_call(c, Lc);
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-base randomizer (FTHE_ENC_FIXED_BASE).
+//
+// The reference draws r uniform in Z_n^* and pays PowerMod(r, n, n^2) per
+// ciphertext (paillier.cpp:127-136).  Here one random h per key gives
+// hs = h^n mod n^2, and a ciphertext is (1 + m n) hs^alpha mod n^2 = g^m (h^alpha)^n:
+// a Paillier encryption of m with r = h^alpha (the Damgard-Jurik-Nielsen
+// fixed-base randomizer).  alpha is uniform over 8*nwin bits, 64 bits more than
+// the order of hs (which divides lambda; p-1 for the CRT halves), so r^n is
+// statistically uniform over <hs> (CRT: over <hs mod p^2> x <hs mod q^2>, with
+// independent exponents).  With 8-bit windows and tables entry[j][d] = hs^(d 256^j)
+// the exponentiation is nwin gathered products and no squarings.
+namespace {
+
+// entries[j][d] = store(base^(d 256^j) mod N), nwin windows, ew words each
+std::vector<uint32_t> fb_table(const mpz_t base, const mpz_t N, int nwin, int ew,
+                               const std::function<void(const mpz_t, uint32_t *)> &store) {
+    std::vector<uint32_t> tab((size_t)nwin * 256 * ew, 0);
+    std::vector<Mpz> b(nwin);
+    mpz_mod(b[0], base, N);
+    for (int j = 1; j < nwin; j++) mpz_powm_ui(b[j], b[j - 1], 256, N);
+    int nt = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            Mpz acc, tmp;
+            for (int j = t; j < nwin; j += nt) {
+                mpz_set_ui(acc, 1);
+                for (int d = 0; d < 256; d++) {
+                    store(acc, &tab[((size_t)j * 256 + d) * ew]);
+                    mpz_mul(tmp, acc, b[j]);
+                    mpz_mod(acc, tmp, N);
+                }
+            }
+        });
+    for (auto &x : th) x.join();
+    return tab;
+}
+
+int fb_upload(const std::vector<uint32_t> &v, uint32_t **d) {
+    if (hipMalloc((void **)d, v.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    HIPOK(hipMemcpy(*d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    return FTHE_OK;
+}
+
+// one-lane kernels: radix-2^B limbs of x R mod N, padded to ew words
+std::function<void(const mpz_t, uint32_t *)> fb_store_limbs(const MontMod &M) {
+    return [&M](const mpz_t x, uint32_t *dst) {
+        std::vector<uint32_t> l = M.mont(x);
+        std::copy(l.begin(), l.end(), dst);
+    };
+}
+
+int fb_build(fthe_key *k, const mpz_t h) {
+    fthe_key::FixedBase &F = k->fb;
+    if (mpz_sgn(h) <= 0 || mpz_cmp(h, k->n) >= 0) return FTHE_ERR_ARG;
+    for (uint32_t **p : {&F.d_tab_pub, &F.d_tab_p, &F.d_tab_q, &F.d_prog})
+        if (*p) { hipFree(*p); *p = nullptr; }
+    F.ready = false;
+    mpz_set(F.h, h);
+    mpz_powm(F.hs, h, k->n, k->n2);
+    std::vector<uint32_t> progs;
+    auto add = [&](const Prog &p, size_t &off, double &mm) {
+        off = progs.size(); mm = p.montmuls;
+        progs.insert(progs.end(), p.w.begin(), p.w.end());
+    };
+    int rc;
+    // public-key form: one-lane n^2 kernels, or the four-lane kernel's 128-word rows
+    F.pub = k->pub_ok && (k->sn2.lanes == 1 || k->rowio);
+    if (F.pub) {
+        F.nwin_pub = (k->n_bits + 64 + 7) / 8;
+        F.pub_rows = k->sn2.lanes == 4;
+        const MontMod &M = k->mn2.m;
+        std::vector<uint32_t> tab;
+        if (F.pub_rows) {
+            F.ew_pub = 2 * k->n_words;
+            const int cw = F.ew_pub;
+            tab = fb_table(F.hs, k->n2, F.nwin_pub, cw, [&M, cw](const mpz_t x, uint32_t *dst) {
+                Mpz t; mpz_mul(t, x, M.R); mpz_mod(t, t, M.N);
+                mpz_to_words(t, dst, cw);
+            });
+        } else {
+            F.ew_pub = 4 * ((M.S + 3) / 4);
+            tab = fb_table(F.hs, k->n2, F.nwin_pub, F.ew_pub, fb_store_limbs(M));
+        }
+        if ((rc = fb_upload(tab, &F.d_tab_pub))) return rc;
+        Prog e;
+        e.loadgd(0);
+        for (int j = 1; j < F.nwin_pub; j++) e.mulgd(j);
+        e.storex(SL_SAVED);
+        e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);   // (1 + m n) hs^alpha
+        if (F.pub_rows) e.storew(2); else e.storex(SL_OUTP);
+        e.end();
+        add(e, F.off_pub, F.mm_pub);
+    }
+    if (k->priv) {
+        F.nwin_crt = (int)((std::max(k->p.bits(), k->q.bits()) + 64 + 7) / 8);
+        F.ew_crt = 4 * ((k->spq.S + 3) / 4);
+        for (int side = 0; side < 2; side++) {
+            const DevMod &D = side ? k->mq2 : k->mp2;
+            Mpz hsP; mpz_mod(hsP, F.hs, D.m.N);
+            std::vector<uint32_t> tab = fb_table(hsP, D.m.N, F.nwin_crt, F.ew_crt, fb_store_limbs(D.m));
+            if ((rc = fb_upload(tab, side ? &F.d_tab_q : &F.d_tab_p))) return rc;
+            Prog e;
+            e.loadgd(0);
+            for (int j = 1; j < F.nwin_crt; j++) e.mulgd(j);
+            e.storex(SL_SAVED);
+            e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
+            e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+            double mm;
+            add(e, side ? F.off_q : F.off_p, mm);
+            F.mm_crt = mm;
+        }
+    }
+    if (progs.empty()) return FTHE_ERR_UNSUPPORTED;
+    if ((rc = fb_upload(progs, &F.d_prog))) return rc;
+    F.ready = true;
+    return FTHE_OK;
+}
+
+int fb_ensure(fthe_key *k, fthe_ctx *c) {
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    if (k->fb.ready) return FTHE_OK;
+    HIPOK(hipSetDevice(c->device));
+    // h uniform in [1, n) from /dev/urandom
+    gmp_randstate_t st;
+    gmp_randinit_default(st);
+    Mpz seed; mpz_set_ui(seed, urandom64()); mpz_mul_2exp(seed, seed, 64); mpz_add_ui(seed, seed, urandom64());
+    gmp_randseed(st, seed);
+    Mpz h, nm1; mpz_sub_ui(nm1, k->n, 1);
+    mpz_urandomm(h, st, nm1); mpz_add_ui(h, h, 1);
+    gmp_randclear(st);
+    return fb_build(k, h);
+}
+
+}  // namespace
+
+extern "C" int fthe_key_fixed_base(fthe_key *k, fthe_ctx *c, const uint32_t *h, int h_words) {
+    if (!k || !c || k->device != c->device) return FTHE_ERR_ARG;
+    if (!h) {
+        { std::lock_guard<std::mutex> g(k->fb_mu); k->fb.ready = false; }
+        return fb_ensure(k, c);
+    }
+    if (h_words <= 0 || h_words > k->n_words) return FTHE_ERR_ARG;
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipDeviceSynchronize());            // no call may still read the old tables
+    Mpz hh; mpz_from_words(hh, h, h_words);
+    return fb_build(k, hh);
+}
+
+extern "C" int fthe_key_fixed_base_info(fthe_key *k, int *alpha_bits_public, int *alpha_bits_crt, uint32_t *hs) {
+    if (!k) return FTHE_ERR_ARG;
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    if (!k->fb.ready) return FTHE_ERR_ARG;
+    if (alpha_bits_public) *alpha_bits_public = k->fb.pub ? 8 * k->fb.nwin_pub : 0;
+    if (alpha_bits_crt) *alpha_bits_crt = k->priv ? 8 * k->fb.nwin_crt : 0;
+    if (hs) mpz_to_words(k->fb.hs, hs, 2 * k->n_words);
+    return FTHE_OK;
+}
+
+static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *alpha,
+                           int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe) {
+    int rc = fb_ensure(k, c);
+    if (rc) return rc;
+    const fthe_key::FixedBase &F = k->fb;
+    if (!crt && !F.pub) return FTHE_ERR_UNSUPPORTED;
+    const int nwin = crt ? F.nwin_crt : F.nwin_pub;
+    if (alpha && (a_words <= 0 || a_words > (8 * nwin + 31) / 32)) return FTHE_ERR_ARG;
+    Launch Lc;
+    if ((rc = begin_call(c, k, count, Lc, nslots_for(k), crt ? k->spq : k->sn2))) return rc;
+    const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
+    const size_t dig_bytes = (size_t)nwin * L;                 // [window][L] u8, per side
+    if ((rc = c->scratch.ensure(2 * dig_bytes))) return rc;
+    uint8_t *dig_p = (uint8_t *)c->scratch.p, *dig_q = dig_p + dig_bytes;
+    RngKey rk{};
+    if (!alpha) {
+        uint64_t sd = rng_seed ? rng_seed : urandom64();
+        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(sd); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
+        rk.nonce = splitmix64(sd) ^ 0x6669786564626173ull;     // a stream apart from k_rng_r's
+    }
+    if (crt) {
+        Lc.fill(SL_C1, k->c_nRp); Lc.fill(SL_C3, k->c_nRq);
+        Lc.fill(SL_T1, k->c_qinvRp2);
+    } else {
+        Lc.fill(SL_C1, k->c_nRn2);
+    }
+    const uint32_t *prog = F.d_prog;
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        if (pipe && (rc = pipe->before(off, L, count))) return rc;
+        const int sides = crt && !alpha ? 2 : 1;
+        if (alpha) {
+            hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, alpha + off * a_words, a_words,
+                               cnt, nwin, L, dig_p);
+        } else {
+            for (int sd = 0; sd < sides; sd++)
+                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, rk, (uint64_t)off, cnt, nwin, L,
+                                   sd, sd ? dig_q : dig_p);
+        }
+        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+        if (crt) {
+            const void *rp[2] = {F.d_tab_p, dig_p};
+            const void *rq[2] = {F.d_tab_q, sides == 2 ? dig_q : dig_p};
+            if ((rc = Lc.prog_raw(prog + F.off_p, F.mm_crt, k->mp2, rp, 2))) return rc;
+            if ((rc = Lc.prog_raw(prog + F.off_q, F.mm_crt, k->mq2, rq, 2))) return rc;
+            hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
+                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+            if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
+            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
+                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+        } else if (F.pub_rows) {
+            const void *rows[3] = {F.d_tab_pub, dig_p, out + off * cw};
+            if ((rc = Lc.prog_raw(prog + F.off_pub, F.mm_pub, k->mn2, rows, 3))) return rc;
+        } else {
+            const void *rows[2] = {F.d_tab_pub, dig_p};
+            if ((rc = Lc.prog_raw(prog + F.off_pub, F.mm_pub, k->mn2, rows, 2))) return rc;
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L, cnt, out + off * cw, cw, Lc.B);
+        }
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);
@@ -1393,7 +1647,7 @@ struct HostIO {
 extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
                                 int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
-    if (r && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
+    if (r && (r_words <= 0 || r_words > k->n_words + ((flags & FTHE_ENC_FIXED_BASE) ? 4 : 0))) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     size_t cw = 2 * (size_t)k->n_words;
     int rc;

@@ -32,6 +32,10 @@ Ops (uint32 pairs, read with s_load from the program buffer):
     6 ADDSMALL k    X <- X + k             (k < 2^B)
    12 PREFA  slot   LDS A buffer <- slot, asynchronously (LDS-DMA)
    13 MULA   -      X <- MontMul(A buffer, X) after the PREFA landed
+   14 LOADXGD j     X <- table entry j*256 + dig[j][g]       (fixed-base tables:
+   15 MULGD   j     X <- MontMul(table entry j*256 + dig[j][g], X)  rows[0] = table
+                    of entries of EW = 4*ceil(S/4) radix-2^B words, rows[1] = u8
+                    digit array [window][L])
 
 Slot memory: slot s, limb k, lane g at  slots + s*slot_stride + k*L*4 + g*4
 (limb-major, lane-interleaved: every global access is fully coalesced).
@@ -138,7 +142,8 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
     e('  s_addc_u32 s7, s7, 0')
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
-                      (5, '.Laddslot'), (6, '.Laddsmall'), (12, '.Lprefa'), (13, '.Lmula')):
+                      (5, '.Laddslot'), (6, '.Laddsmall'), (12, '.Lprefa'), (13, '.Lmula'),
+                      (14, '.Lloadxgd'), (15, '.Lmulgd')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -303,6 +308,46 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
 
     e('.Lmula:')
     e('  s_waitcnt vmcnt(0)')
+    e('  s_mov_b32 s19, 0')
+    e('  s_branch .Lmontmul')
+
+    # Fixed-base tables (gathered by a per-lane digit): entry j*256 + dig[j][g] of
+    # rows[0], EW words each; the digit byte array rows[1] is [window][L].  The
+    # entry lands in the free T registers (dwordx4 loads), then X or the LDS A column.
+    EW = 4 * ((S + 3) // 4)
+    assert 2 * NT >= EW and TB % 2 == 0
+
+    def gather_entry():
+        e('  s_load_dwordx2 s[16:17], s[0:1], 0x30')        # digit array
+        e('  s_lshr_b32 s14, s10, 2')                        # L
+        e('  s_mul_i32 s14, s14, s15')                       # j*L
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_add_u32 s16, s16, s14')
+        e('  s_addc_u32 s17, s17, 0')
+        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 2, v{V_GOFF}')      # lane index g
+        e(f'  global_load_ubyte v{V_TMP}, v{V_TMP}, s[16:17]')
+        e('  s_load_dwordx2 s[16:17], s[0:1], 0x28')        # table
+        e('  s_lshl_b32 s14, s15, 8')                        # j*256
+        e('  s_waitcnt vmcnt(0) lgkmcnt(0)')
+        e(f'  v_or_b32_e32 v{V_TMP}, s14, v{V_TMP}')
+        e(f'  v_mul_u32_u24_e32 v{V_TMP}, {4 * EW}, v{V_TMP}')
+        for i in range(EW // 4):
+            e(f'  global_load_dwordx4 v[{TB + 4 * i}:{TB + 4 * i + 3}], v{V_TMP}, s[16:17] offset:{16 * i}')
+        e('  s_waitcnt vmcnt(0)')
+
+    e('.Lloadxgd:')
+    gather_entry()
+    for k in range(S):
+        e(f'  v_mov_b32_e32 {X(k)}, v{TB + k}')
+    e('  s_branch .Lprog')
+
+    e('.Lmulgd:')
+    gather_entry()
+    for k in range(S):
+        e(f'  ds_write_b32 v{V_LDSA}, v{TB + k} offset:{k * 256}')
+        if k % 8 == 7:
+            e('  s_waitcnt lgkmcnt(0)')
+    e('  s_waitcnt lgkmcnt(0)')
     e('  s_mov_b32 s19, 0')
     e('  s_branch .Lmontmul')
 
@@ -560,7 +605,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
                       (5, '.Laddslot'), (6, '.Laddsmall'), (7, '.Lloadw'), (8, '.Lmulw'),
-                      (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg')):
+                      (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg'), (14, '.Lloadwd'), (15, '.Lmulwd')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -746,23 +791,42 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
 
     # Gathered rows: LOADWG / MULWG t read row idx[g] of the array at rows[0], idx an
     # int64 array at rows[t] (one entry per ciphertext of the launch); idx < 0 -> 1.
-    def load_gather_limbs(dst):
-        e('  s_lshl_b32 s16, s15, 3')
-        e('  s_add_u32 s16, s16, 40')
-        e('  s_load_dwordx2 s[32:33], s[0:1], s16')                # idx array
-        e('  s_load_dwordx2 s[30:31], s[0:1], 40')                 # row base
-        e('  s_waitcnt lgkmcnt(0)')
-        live_mask()
-        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
-        e(f'  v_lshlrev_b32_e32 v{V_TMP}, 3, v{V_TMP}')
-        e(f'  global_load_dwordx2 v[{V_TMP}:{V_TMP + 1}], v{V_TMP}, s[32:33]')
-        e('  s_waitcnt vmcnt(0)')
-        e(f'  v_cmp_gt_i32_e32 vcc, 0, v{V_TMP + 1}')               # idx < 0
-        e('  s_and_saveexec_b64 s[34:35], vcc')
-        for j in range(Q):
-            e(f'  v_mov_b32_e32 {dst(j)}, 0')
-        e(f'  v_cndmask_b32_e64 {dst(0)}, 0, 1, s[22:23]')        # the integer 1
-        e('  s_andn2_b64 exec, s[34:35], exec')                     # live lanes with idx >= 0
+    def load_gather_limbs(dst, digits=False):
+        if digits:
+            # fixed-base table: row j*256 + dig[j][g] of rows[0]; u8 digit array
+            # [window][L] at rows[1]; arg = window j
+            e('  s_load_dwordx2 s[32:33], s[0:1], 0x30')           # digit array
+            e('  s_load_dwordx2 s[30:31], s[0:1], 0x28')           # table rows
+            e('  s_lshr_b32 s16, s10, 2')                           # L
+            e('  s_mul_i32 s16, s16, s15')                          # j*L
+            e('  s_waitcnt lgkmcnt(0)')
+            e('  s_add_u32 s32, s32, s16')
+            e('  s_addc_u32 s33, s33, 0')
+            live_mask()
+            e('  s_mov_b64 s[34:35], exec')
+            e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')          # g
+            e(f'  global_load_ubyte v{V_TMP}, v{V_TMP}, s[32:33]')
+            e('  s_lshl_b32 s16, s15, 8')                           # j*256
+            e('  s_waitcnt vmcnt(0)')
+            e(f'  v_or_b32_e32 v{V_TMP}, s16, v{V_TMP}')
+            e(f'  v_mov_b32_e32 v{V_TMP + 1}, 0')
+        else:
+            e('  s_lshl_b32 s16, s15, 3')
+            e('  s_add_u32 s16, s16, 40')
+            e('  s_load_dwordx2 s[32:33], s[0:1], s16')                # idx array
+            e('  s_load_dwordx2 s[30:31], s[0:1], 40')                 # row base
+            e('  s_waitcnt lgkmcnt(0)')
+            live_mask()
+            e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
+            e(f'  v_lshlrev_b32_e32 v{V_TMP}, 3, v{V_TMP}')
+            e(f'  global_load_dwordx2 v[{V_TMP}:{V_TMP + 1}], v{V_TMP}, s[32:33]')
+            e('  s_waitcnt vmcnt(0)')
+            e(f'  v_cmp_gt_i32_e32 vcc, 0, v{V_TMP + 1}')               # idx < 0
+            e('  s_and_saveexec_b64 s[34:35], vcc')
+            for j in range(Q):
+                e(f'  v_mov_b32_e32 {dst(j)}, 0')
+            e(f'  v_cndmask_b32_e64 {dst(0)}, 0, 1, s[22:23]')        # the integer 1
+            e('  s_andn2_b64 exec, s[34:35], exec')                     # live lanes with idx >= 0
         e(f'  v_lshlrev_b64 v[{V_TMP}:{V_TMP + 1}], 9, v[{V_TMP}:{V_TMP + 1}]')
         e(f'  v_and_b32_e32 v{V_AI[0]}, 0x180, v{V_ROW}')           # 128k
         e(f'  v_add_co_u32_e32 v{V_TMP}, vcc, v{V_TMP}, v{V_AI[0]}')
@@ -789,6 +853,18 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
 
     e('.Lmulwg:')
     load_gather_limbs(lambda j: f"v{A0 + j}")
+    restore_exec()
+    write_a(lambda j: f"v{A0 + j}")
+    e('  s_mov_b32 s19, 0')
+    e('  s_branch .Lmontmul')
+
+    e('.Lloadwd:')
+    load_gather_limbs(X, digits=True)
+    restore_exec()
+    e('  s_branch .Lprog')
+
+    e('.Lmulwd:')
+    load_gather_limbs(lambda j: f"v{A0 + j}", digits=True)
     restore_exec()
     write_a(lambda j: f"v{A0 + j}")
     e('  s_mov_b32 s19, 0')

@@ -179,19 +179,43 @@ class Paillier:
     def _cw(self):
         return 2 * self.n_words
 
-    def encrypt_u64(self, m, r=None, seed=0, public=False):
+    @staticmethod
+    def _flags(public, fixed_base):
+        return (_lib.FTHE_ENC_PUBLIC if public else _lib.FTHE_ENC_DEFAULT) | \
+            (_lib.FTHE_ENC_FIXED_BASE if fixed_base else 0)
+
+    def set_fixed_base(self, h=None):
+        """(Re)build the fixed-base randomizer tables for base h (None: random h)."""
+        hw = None if h is None else _words(int(h), self.n_words)
+        _lib.check(self.lib.fthe_key_fixed_base(self._key, self.dev.ctx, _ptr(hw), self.n_words if hw is not None else 0),
+                   "key_fixed_base")
+
+    def fixed_base_info(self):
+        """(alpha_bits_public, alpha_bits_crt, hs) of the built fixed-base tables."""
+        ap, ac = ctypes.c_int(), ctypes.c_int()
+        hs = np.zeros(self._cw(), dtype=np.uint32)
+        _lib.check(self.lib.fthe_key_fixed_base_info(self._key, ctypes.byref(ap), ctypes.byref(ac), _ptr(hs)),
+                   "key_fixed_base_info")
+        return ap.value, ac.value, int.from_bytes(hs.tobytes(), "little")
+
+    def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False):
         """c = g^m r^n mod n^2 for every m (paillier.cpp:134-137).
         r: None -> fresh uniform r per ciphertext from the device CSPRNG;
-           else (count, n_words) uint32 words or a list of ints."""
+           else (count, n_words) uint32 words or a list of ints.
+        fixed_base: r = h^alpha from the key's fixed-base tables (include/fthe.h);
+           r then injects alpha (ints or (count, words) uint32) instead of r."""
         m = np.ascontiguousarray(m, dtype=np.uint64).reshape(-1)
         cnt = len(m)
         out = np.zeros((cnt, self._cw()), dtype=np.uint32)
         rw = None
         if r is not None:
             if not isinstance(r, np.ndarray):
-                r = np.stack([_words(int(x), self.n_words) for x in r]) if cnt else np.zeros((0, self.n_words), np.uint32)
+                nw = self.n_words + (2 if fixed_base else 0)
+                if fixed_base and cnt:
+                    nw = max(1, max((int(x).bit_length() + 31) // 32 for x in r))
+                r = np.stack([_words(int(x), nw) for x in r]) if cnt else np.zeros((0, nw), np.uint32)
             rw = np.ascontiguousarray(r, dtype=np.uint32).reshape(cnt, -1)
-        flags = _lib.FTHE_ENC_PUBLIC if public else _lib.FTHE_ENC_DEFAULT
+        flags = self._flags(public, fixed_base)
         _lib.check(self.lib.fthe_encrypt_u64(self._key, self.dev.ctx, _ptr(m), cnt, _ptr(rw),
                                              rw.shape[1] if rw is not None else 0, int(seed), _ptr(out), flags),
                    "encrypt")
@@ -261,8 +285,8 @@ class Paillier:
         return out
 
     # ---- device-resident batch API (torch tensors on this device) -------------
-    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False):
-        flags = _lib.FTHE_ENC_PUBLIC if public else _lib.FTHE_ENC_DEFAULT
+    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False, fixed_base=False):
+        flags = self._flags(public, fixed_base)
         rp = ctypes.c_void_p(r.data_ptr()) if r is not None else None
         rw = r.shape[-1] if r is not None else 0
         _lib.check(self.lib.fthe_encrypt_u64_dev(self._key, self.dev.ctx, ctypes.c_void_p(m.data_ptr()), m.numel(),

@@ -45,6 +45,7 @@ extern "C" {
 /* fthe_encrypt flags */
 #define FTHE_ENC_DEFAULT      0   /* CRT when the private key is present */
 #define FTHE_ENC_PUBLIC       1   /* force the public-key (no CRT) formula */
+#define FTHE_ENC_FIXED_BASE   2   /* fixed-base randomizer r = h^alpha (see fthe_key_fixed_base) */
 
 typedef struct fthe_ctx fthe_ctx;
 typedef struct fthe_key fthe_key;
@@ -95,6 +96,27 @@ int fthe_encrypt_u64_dev(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t
 int fthe_encrypt_u64(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
                      const uint32_t *r, int r_words, uint64_t rng_seed,
                      uint32_t *c, int flags);
+
+/* ---- fixed-base randomizer (flag FTHE_ENC_FIXED_BASE) -----------------------
+ * Not in the reference: an opt-in encryption mode for throughput.  One random
+ * h per key; c = (1 + m n) * hs^alpha mod n^2 with hs = h^n mod n^2, i.e. a
+ * Paillier encryption of m under r = h^alpha (Damgard-Jurik-Nielsen fixed-base
+ * randomizer).  Decryption, add, mul are unchanged.  alpha is drawn per
+ * ciphertext from the device ChaCha20 stream (r == NULL: 8*nwin random bits,
+ * 64 more than the order of hs, independently mod p^2 and q^2 under CRT), or
+ * injected through the r / r_words arguments of fthe_encrypt_u64[_dev]
+ * (little-endian words, alpha < 2^alpha_bits; the same alpha for both CRT
+ * halves).  8-bit windows: nwin gathered products from precomputed tables
+ * (hs^(d 256^j), 256 entries per window, ~34 MB per key at P-2048) instead of
+ * ~1.2 log2(n) products.
+ * fthe_key_fixed_base        (re)build the tables for base h (h_words words,
+ *                            1 <= h < n); h == NULL draws h from /dev/urandom.
+ *                            Built on first use otherwise.  Not concurrent with
+ *                            calls that use the key.
+ * fthe_key_fixed_base_info   exponent bits per form (0 if unavailable) and hs
+ *                            (2*n_words words, nullable), after a build. */
+int fthe_key_fixed_base(fthe_key *key, fthe_ctx *ctx, const uint32_t *h, int h_words);
+int fthe_key_fixed_base_info(fthe_key *key, int *alpha_bits_public, int *alpha_bits_crt, uint32_t *hs);
 
 /* ---- decrypt: m = L(c^lambda mod n^2) * mu mod n (paillier.cpp:153-156) ---
  * Computed with CRT over p^2, q^2 (identical canonical result).

@@ -35,6 +35,11 @@ def main():
     res = {"lib": os.environ.get("FTHE_LIB", "default")}
     res["encrypt"] = best(lambda: pl.encrypt_u64_dev(m, c, seed=1), a.n)
     res["add"] = best(lambda: pl.add_dev(c, c, o), a.n)
+    if os.environ.get("FTHE_AB_FB", "1") == "1":
+        pl.set_fixed_base(None)
+        res["encrypt_fixed_base"] = best(lambda: pl.encrypt_u64_dev(m, c, seed=1, fixed_base=True), a.n)
+        res["encrypt_public_fixed_base"] = best(lambda: pl.encrypt_u64_dev(m, c, seed=1, public=True, fixed_base=True), a.n)
+        res["encrypt_public"] = best(lambda: pl.encrypt_u64_dev(m[:a.n // 4], c[:a.n // 4], seed=1, public=True), a.n // 4)
     k = a.n // 8
     res["sub"] = best(lambda: pl.sub_dev(c[:k], c[k:2 * k], o[:k]), k)
     print(json.dumps(res), flush=True)
