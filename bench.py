@@ -251,6 +251,24 @@ def main():
             secondary["hist_merge_8party_1M_bins"] = {"ms": round(ms_h, 2), "ciphertexts_out": bins,
                                                       "adds_per_s": round(bins * (parties - 1) / (ms_h * 1e-3))}
             del x, ho
+        # party-side node histogram on the device (hist_tree_builder.cpp:565-595): 1M instances
+        # x 28 features x 255 bins, g and h planes = 55.7M member products, CSR built in HBM
+        nh, ncol = min(P, 1_000_000), 28
+        gen = torch.Generator(device=f"cuda:{local}").manual_seed(SEED)
+        hbins = torch.randint(0, 256, (nh, ncol), dtype=torch.uint8, device=f"cuda:{local}", generator=gen)
+        hcut = (np.arange(ncol + 1) * 255).astype(np.int32)
+        hx = torch.cat([c[:nh], c[P:P + nh]])                          # g plane, h plane
+        hout = torch.empty((2 * int(hcut[-1]), 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+        pl.histogram_dev(hx[:8192], 4096, 2, hbins[:4096], hcut, 255, hout)
+        dev.sync()
+        t0 = time.perf_counter()
+        pl.histogram_dev(hx, nh, 2, hbins, hcut, 255, hout)
+        dev.sync()
+        dt = time.perf_counter() - t0
+        members = int((hbins != 255).sum().item()) * 2
+        secondary["histogram_node_dev"] = {"instances": nh, "features": ncol, "bins": int(hcut[-1]), "planes": 2,
+                                           "s": round(dt, 4), "member_adds_per_s": round(members / dt)}
+        del hx, hout, hbins
         # end to end, host-resident in/out: chunked, double-buffered transfers on a copy
         # stream overlapped with the kernels (pageable caller buffers go through pinned staging)
         ne = min(2 * P, 1 << 21)

@@ -78,6 +78,8 @@ _PROTOS = {
     "fthe_scan_segments": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_reduce_segments_dev": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
     "fthe_reduce_segments": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
+    "fthe_reduce_segments_csr_dev": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
+    "fthe_histogram_dev": (_I, [_P, _P, _P, _SZ, _I, _P, _I, _P, _I, _P, _SZ, _P]),
     "fthe_encode_fixed_dev": (_I, [_P, _P, _SZ, _P]),
     "fthe_decode_fixed_dev": (_I, [_P, _P, _SZ, _P]),
     "fthe_last_kernel_ms": (ctypes.c_double, [_P]),
@@ -103,6 +105,14 @@ def load(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise OSError(f"libfthe.so not built at {path} (run python fedtree_amd/build.py)")
+    # One HIP runtime per process: when PyTorch is present (device buffers, streams),
+    # load it first so libfthe.so binds to the libamdhip64.so.7 it already mapped;
+    # loading ours first would bring up a second HIP/HSA runtime and torch then
+    # reports "No HIP GPUs are available".
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)

@@ -117,6 +117,8 @@ struct fthe_ctx {
     hipModule_t mod[MAX_VARIANTS] = {};
     hipFunction_t fn[MAX_VARIANTS] = {};
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
+    DevBuf hb[6];                           // histogram CSR / segmented-product plan (device)
+    void *cub_tmp = nullptr; size_t cub_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_mm = 0;
     bool timed = false;
@@ -285,6 +287,7 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->copy) hipStreamSynchronize(c->copy);
     for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) hipModuleUnload(c->mod[i]);
+    if (c->cub_tmp) hipFree(c->cub_tmp);
     for (auto &e : c->prof_ev) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -1411,25 +1414,30 @@ struct GatherProd {
     }
     // idx: K x G host indices into src (rows of cw words)
     int run(const uint32_t *src, const std::vector<int64_t> &idx, size_t G, uint32_t *dst) {
-        const int cw = 2 * k->n_words, S = Lc.S, L = Lc.L;
         int rc;
         HIPOK(hipStreamSynchronize(c->stream));          // previous pass done with scratch
         if ((rc = c->scratch.ensure(std::max<size_t>(8, idx.size() * 8)))) return rc;
         if (!idx.empty()) HIPOK(hipMemcpy(c->scratch.p, idx.data(), idx.size() * 8, hipMemcpyHostToDevice));
+        return run_dev(src, (const int64_t *)c->scratch.p, G, dst);
+    }
+    // gidx: K x G device indices into src
+    int run_dev(const uint32_t *src, const int64_t *gidx, size_t G, uint32_t *dst) {
+        const int cw = 2 * k->n_words, S = Lc.S, L = Lc.L;
+        int rc;
         for (size_t off = 0; off < G; off += L) {
             size_t cnt = std::min((size_t)L, G - off);
             Lc.live = cnt;
             if (k->rowio) {
                 const void *rows[K + 2];
                 rows[0] = src;
-                for (int j = 0; j < K; j++) rows[1 + j] = (const int64_t *)c->scratch.p + (size_t)j * G + off;
+                for (int j = 0; j < K; j++) rows[1 + j] = gidx + (size_t)j * G + off;
                 rows[K + 1] = dst + off * cw;
                 if ((rc = launch_dyn(Lc, c->io[3].p, mm, k->mn2, rows, K + 2))) return rc;
                 continue;
             }
             for (int j = 0; j < K; j++)
                 pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(base + j), S, L, Lc.B,
-                          (const int64_t *)c->scratch.p + (size_t)j * G + off);
+                          gidx + (size_t)j * G + off);
             if ((rc = launch_dyn(Lc, c->io[3].p, mm, k->mn2))) return rc;
             unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L, cnt, dst + off * cw, cw, Lc.B);
         }
@@ -1494,6 +1502,118 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
         bufsel = 3 - bufsel;       // ping-pong io[1] / io[2]
     }
     return end_call(c, gp.Lc);
+}
+
+// Segmented product with the CSR on the device: the same passes as above, planned
+// by k_group_counts / scan / k_plan_groups in HBM (one 8-byte read-back of the
+// group count per pass).  seg_ptr (nseg+1) and idx (nullable: identity) are
+// device arrays and are only read.
+namespace {
+int reduce_segments_csr(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64_t *seg_dev, const int64_t *idx_dev,
+                        size_t nseg, int64_t total, uint32_t *out) {
+    const int K = GatherProd::K;
+    const int cw = 2 * k->n_words;
+    const size_t maxg = (size_t)total / K + nseg;                // groups of the first (largest) pass
+    int rc;
+    if ((rc = c->io[2].ensure(maxg * cw * 4)) || (rc = c->io[1].ensure(maxg * cw * 4))) return rc;
+    if ((rc = c->hb[2].ensure((nseg + 1) * 8)) || (rc = c->hb[3].ensure((maxg + 1) * 8)) ||
+        (rc = c->hb[4].ensure((maxg + 1) * 8)) || (rc = c->hb[5].ensure((size_t)K * maxg * 8))) return rc;
+    GatherProd gp{k, c};
+    if ((rc = gp.init(maxg))) return rc;
+    hipStream_t st = c->stream;
+    const int64_t *seg = seg_dev, *members = idx_dev;
+    const uint32_t *src = x;
+    int bufsel = 1, gsel = 3;
+    size_t n = nseg;
+    while (true) {
+        int64_t *ng = (int64_t *)c->hb[2].p;
+        int64_t *gptr = (int64_t *)c->hb[gsel].p;
+        hipLaunchKernelGGL(k_group_counts, dim3((unsigned)((n + 256) / 256)), dim3(256), 0, st, seg, n, K, ng);
+        if ((rc = exclusive_scan_i64(ng, gptr, n + 1, c->cub_tmp, c->cub_bytes, st))) return rc;
+        int64_t G = 0;
+        HIPOK(hipMemcpyAsync(&G, gptr + n, 8, hipMemcpyDeviceToHost, st));
+        HIPOK(hipStreamSynchronize(st));
+        if (G <= 0 || (size_t)G > maxg) return FTHE_ERR_ARG;
+        int64_t *gidx = (int64_t *)c->hb[5].p;
+        hipLaunchKernelGGL(k_plan_groups, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, seg, members, n, gptr,
+                           (size_t)G, K, gidx);
+        const bool last = (size_t)G == nseg;                      // one group per segment: final pass
+        uint32_t *dst = last ? out : (uint32_t *)c->io[bufsel].p;
+        if ((rc = gp.run_dev(src, gidx, (size_t)G, dst))) return rc;
+        if (last) break;
+        // next pass: segment s owns groups [gptr[s], gptr[s+1]) of dst, members = identity
+        seg = gptr; members = nullptr; src = dst;
+        bufsel = 3 - bufsel; gsel = 7 - gsel;                      // ping-pong io[1]/io[2], hb[3]/hb[4]
+        // n stays nseg: the segments are the same, only their members shrink
+    }
+    return end_call(c, gp.Lc);
+}
+}  // namespace
+
+extern "C" int fthe_reduce_segments_csr_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
+                                            const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out) {
+    if (!k || !c || !seg_ptr || (nseg && !out)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (!nseg) return FTHE_OK;
+    HIPOK(hipSetDevice(c->device));
+    int64_t ends[1] = {0};
+    HIPOK(hipMemcpyAsync(ends, seg_ptr + nseg, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    if (ends[0] < 0 || (!idx && (size_t)ends[0] > count)) return FTHE_ERR_ARG;
+    if (!x && ends[0]) return FTHE_ERR_ARG;
+    (void)count;
+    return reduce_segments_csr(k, c, x, seg_ptr, idx, nseg, ends[0], out);
+}
+
+// Histogram of a node on the device (hist_tree_builder.cpp:565-595 for the root,
+// :640-664 for the smaller child of a sibling pair): the CSR of (plane, feature,
+// bin) segments from dense_bin_id (atomic count, scan, atomic scatter), then the
+// segmented K-way product.  out[p*n_bins + cut[f] + bid] = prod x[p*count + iid]
+// over the selected iid with bin_ids[iid*n_col + f] == bid != max_num_bin.
+extern "C" int fthe_histogram_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, int planes,
+                                  const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
+                                  const int32_t *inst, size_t n_sel, uint32_t *out) {
+    if (!k || !c || !cut_col_ptr || n_col <= 0 || planes <= 0 || (!inst && n_sel > count)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (cut_col_ptr[0] != 0) return FTHE_ERR_ARG;
+    for (int f = 0; f < n_col; f++) if (cut_col_ptr[f + 1] < cut_col_ptr[f]) return FTHE_ERR_ARG;
+    const int64_t n_bins = cut_col_ptr[n_col];
+    const size_t nseg = (size_t)planes * (size_t)n_bins;
+    if (!nseg) return FTHE_OK;
+    if (!out || (n_sel && (!x || !bin_ids))) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc;
+    const size_t cells = n_sel * (size_t)n_col;
+    // hb[0]: cut (int32) | counts (u64, nseg+1) ; hb[1]: seg (nseg+1) | cursor (nseg) ; io[0]: idx
+    const size_t cut_b = ((size_t)(n_col + 1) * 4 + 255) / 256 * 256;
+    if ((rc = c->hb[0].ensure(cut_b + (nseg + 1) * 8)) || (rc = c->hb[1].ensure((2 * nseg + 1) * 8))) return rc;
+    int32_t *d_cut = (int32_t *)c->hb[0].p;
+    unsigned long long *cnt = (unsigned long long *)((char *)c->hb[0].p + cut_b);
+    int64_t *seg = (int64_t *)c->hb[1].p;
+    unsigned long long *cursor = (unsigned long long *)(seg + nseg + 1);
+    HIPOK(hipMemcpyAsync(d_cut, cut_col_ptr, (size_t)(n_col + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPOK(hipMemsetAsync(cnt, 0, (nseg + 1) * 8, st));
+    HIPOK(hipMemsetAsync(cursor, 0, nseg * 8, st));
+    const unsigned gb = (unsigned)std::max<size_t>(1, (cells + 255) / 256);
+    if (cells)
+        hipLaunchKernelGGL(k_hist_count, dim3(gb), dim3(256), 0, st, bin_ids, n_col, d_cut, max_num_bin, inst, n_sel,
+                           planes, n_bins, cnt);
+    // counts -> int64 in seg, exclusive scan in place through io[0] as temp
+    if ((rc = c->io[0].ensure((nseg + 1) * 8))) return rc;
+    int64_t *tmp = (int64_t *)c->io[0].p;
+    hipLaunchKernelGGL(k_u64_to_i64, dim3((unsigned)((nseg + 256) / 256)), dim3(256), 0, st, cnt, tmp, nseg + 1);
+    if ((rc = exclusive_scan_i64(tmp, seg, nseg + 1, c->cub_tmp, c->cub_bytes, st))) return rc;
+    int64_t total = 0;
+    HIPOK(hipMemcpyAsync(&total, seg + nseg, 8, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    if ((rc = c->io[0].ensure(std::max<int64_t>(1, total) * 8))) return rc;
+    int64_t *idx = (int64_t *)c->io[0].p;
+    if (cells)
+        hipLaunchKernelGGL(k_hist_scatter, dim3(gb), dim3(256), 0, st, bin_ids, n_col, d_cut, max_num_bin, inst, n_sel,
+                           planes, n_bins, count, seg, cursor, idx);
+    // io[0] (idx) and hb[1] (seg) stay untouched by the product passes (io[1]/io[2], hb[2..5])
+    return reduce_segments_csr(k, c, x, seg, idx, nseg, total, out);
 }
 
 // Segmented inclusive scan: out[t] = prod_{t' in [seg_start(t), t]} x[t'] mod n^2, the

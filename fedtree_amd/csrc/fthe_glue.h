@@ -26,6 +26,17 @@ __global__ void k_crt_dec_prep(uint32_t *mp, uint32_t *mq, const uint32_t *p, co
 __global__ void k_rng_r(const uint32_t *n_words, int nw, int nbits, RngKey key, uint64_t index0, size_t count, uint32_t *r);
 __global__ void k_rng_digits(RngKey key, uint64_t index0, size_t count, int nwin, int L, int side, uint8_t *dig);
 __global__ void k_alpha_digits(const uint32_t *alpha, int aw, size_t count, int nwin, int L, uint8_t *dig);
+// fthe_hist.hip: histogram CSR and the segmented-product planner
+__global__ void k_hist_count(const uint8_t *bin, int n_col, const int32_t *cut, int max_bin, const int32_t *inst,
+                             size_t n_sel, int planes, int64_t n_bins, unsigned long long *cnt);
+__global__ void k_hist_scatter(const uint8_t *bin, int n_col, const int32_t *cut, int max_bin, const int32_t *inst,
+                               size_t n_sel, int planes, int64_t n_bins, size_t count, const int64_t *seg,
+                               unsigned long long *cursor, int64_t *idx);
+__global__ void k_group_counts(const int64_t *seg, size_t nseg, int K, int64_t *ng);
+__global__ void k_plan_groups(const int64_t *seg, const int64_t *members, size_t nseg, const int64_t *gptr, size_t G,
+                              int K, int64_t *gidx);
+__global__ void k_u64_to_i64(const unsigned long long *a, int64_t *b, size_t n);
+int exclusive_scan_i64(const int64_t *in, int64_t *out, size_t n, void *&tmp, size_t &tmp_bytes, hipStream_t st);
 __global__ void k_encode_fixed(const float *x, size_t count, uint64_t *m);
 __global__ void k_decode_fixed(const uint64_t *m, size_t count, float *x);
 }  // namespace fthe

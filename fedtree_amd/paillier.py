@@ -336,6 +336,30 @@ class Paillier:
                                                      ctypes.c_void_p(out.data_ptr())), "reduce_segments_dev")
         return out
 
+    def reduce_segments_csr_dev(self, x, seg_ptr, out, idx=None):
+        """Segmented product with the CSR (int64 seg_ptr, optional int64 idx) on the device."""
+        cnt = x.numel() // self._cw()
+        _lib.check(self.lib.fthe_reduce_segments_csr_dev(
+            self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), cnt, ctypes.c_void_p(seg_ptr.data_ptr()),
+            ctypes.c_void_p(idx.data_ptr()) if idx is not None else None, seg_ptr.numel() - 1,
+            ctypes.c_void_p(out.data_ptr())), "reduce_segments_csr_dev")
+        return out
+
+    def histogram_dev(self, x, count, planes, bin_ids, cut_col_ptr, max_num_bin, out, inst=None):
+        """Node histogram on the device (hist_tree_builder.cpp:565-595, :640-664).
+        x: device (planes*count, 2nw) ciphertexts (g plane, h plane); bin_ids: device
+        uint8 (count, n_col); inst: device int32 instance ids of the node or None;
+        out: device (planes*n_bins, 2nw)."""
+        cut = np.ascontiguousarray(cut_col_ptr, dtype=np.int32)
+        n_col = len(cut) - 1
+        n_sel = inst.numel() if inst is not None else count
+        _lib.check(self.lib.fthe_histogram_dev(
+            self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), int(count), int(planes),
+            ctypes.c_void_p(bin_ids.data_ptr()), n_col, _ptr(cut), int(max_num_bin),
+            ctypes.c_void_p(inst.data_ptr()) if inst is not None else None, int(n_sel),
+            ctypes.c_void_p(out.data_ptr())), "histogram_dev")
+        return out
+
     # ---- reference single-value signatures (batch of one) ------------------
     def encrypt(self, message, r=None):
         """Paillier::encrypt(const ZZ&) (paillier.cpp:122).  message < 2^64."""

@@ -178,6 +178,27 @@ int fthe_reduce_segments_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, si
 int fthe_reduce_segments(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count,
                          const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out);
 
+/* The same with the CSR in device memory (seg_ptr: nseg+1 int64, idx: int64 or
+ * NULL for the identity), planned on the device: no host-side index work. */
+int fthe_reduce_segments_csr_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count,
+                                 const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out);
+
+/* ---- homomorphic histogram of one tree node, all on the device ------------
+ * Replaces the scatter loop of HistTreeBuilder::compute_histogram_in_a_level
+ * (hist_tree_builder.cpp:565-595 root, :640-664 smaller child of a sibling
+ * pair: hist[cut_col_ptr[fid] + bid] = hist[...] + gh[iid], bid =
+ * dense_bin_id[iid*n_col + fid] != max_num_bin).
+ *   x        planes * count ciphertexts (plane p = x[p*count ..]: g_enc, h_enc)
+ *   bin_ids  device, count * n_col bytes (dense_bin_id, row-major by instance)
+ *   cut_col_ptr  HOST, n_col + 1 int32 (cut.cut_col_ptr)
+ *   inst     device int32 instance ids of the node (node_idx range), or NULL
+ *            for instances 0 .. n_sel-1
+ *   out      device, planes * n_bins ciphertexts; a bin without members is
+ *            the integer 1 (the reference keeps an unencrypted zero there). */
+int fthe_histogram_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count, int planes,
+                       const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
+                       const int32_t *inst, size_t n_sel, uint32_t *out);
+
 /* Segmented inclusive scan: out[t] = prod of x[seg_start(t) .. t] mod n^2 --
  * the inclusive_scan_by_key of the histogram over (node, feature)
  * (hist_tree_builder.cpp:695-708).  seg_ptr (nseg+1 entries) is a HOST array;
