@@ -166,11 +166,14 @@ struct fthe_key {
     uint32_t *d_progs = nullptr;
     size_t n_words_dev_off = 0;     // offset (in u32) of n words in d_consts
     uint32_t *d_nwords = nullptr;
+    uint32_t *d_pqwords = nullptr;  // p then q as pq_w u32 words each (device-drawn y_p, y_q)
+    int pq_w = 0;
     ~fthe_key() {
         for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1}) if (d->d_ctx) hipFree(d->d_ctx);
         if (d_consts) hipFree(d_consts);
         if (d_progs) hipFree(d_progs);
         if (d_nwords) hipFree(d_nwords);
+        if (d_pqwords) hipFree(d_pqwords);
         for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) hipFree(p);
     }
     // constant handles
@@ -563,6 +566,14 @@ static int key_finish(fthe_key *k) {
     HIPOK(hipMemcpy(k->d_consts, flat.data(), flat.size() * 4, hipMemcpyHostToDevice));
     if (hipMalloc(&k->d_progs, k->host_progs.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(k->d_progs, k->host_progs.data(), k->host_progs.size() * 4, hipMemcpyHostToDevice));
+    if (k->priv) {
+        k->pq_w = (int)((std::max(k->p.bits(), k->q.bits()) + 31) / 32);
+        std::vector<uint32_t> pq(2 * (size_t)k->pq_w);
+        mpz_to_words(k->p, pq.data(), k->pq_w);
+        mpz_to_words(k->q, pq.data() + k->pq_w, k->pq_w);
+        if (hipMalloc(&k->d_pqwords, pq.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+        HIPOK(hipMemcpy(k->d_pqwords, pq.data(), pq.size() * 4, hipMemcpyHostToDevice));
+    }
     std::vector<uint32_t> nw(k->n_words);
     mpz_to_words(k->n, nw.data(), k->n_words);
     if (hipMalloc(&k->d_nwords, nw.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
@@ -905,8 +916,16 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
     int rc = begin_call(c, k, count, Lc, nslots_for(k), crt ? k->spq : k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    // Device-drawn randomness under CRT draws y_p, y_q uniform in [1,p), [1,q) and
+    // skips stage A: r^n mod P^2 = (r^Q mod P)^P and r -> r^Q mod P is a bijection of
+    // Z_P^* (gcd(n, phi(n)) = 1, checked at key set-up as paillier.cpp:60), so
+    // y^P mod P^2 for uniform y has exactly the distribution of r^n mod P^2 for the
+    // reference's uniform r, independently for P = p, q (CRT).  FTHE_NO_DIRECT_Y=1
+    // keeps the explicit r (A/B).  Injected r always takes both stages (bit-exact).
+    static const bool no_direct = getenv("FTHE_NO_DIRECT_Y") != nullptr;
+    const bool direct_y = crt && !r && !no_direct;
     // scratch: AoS r words for the device RNG
-    if (!r && (rc = c->scratch.ensure((size_t)L * nw * 4))) return rc;
+    if (!r && (rc = c->scratch.ensure((size_t)L * nw * 4 * (direct_y ? 2 : 1)))) return rc;
     RngKey rk{};
     if (!r) {
         uint64_t s = rng_seed ? rng_seed : urandom64();
@@ -914,7 +933,11 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
         rk.nonce = splitmix64(s);
     }
     Launch L1 = Lc;                    // stage A: mod p, q on the small-limb kernel, own slot region
-    if (crt) {
+    if (direct_y) {
+        Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
+        Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_nRq);
+        Lc.fill(SL_T1, k->c_qinvRp2);
+    } else if (crt) {
         L1.S = k->sp1.S; L1.B = k->sp1.B;
         if ((rc = c->slots1.ensure((size_t)nslots_for(k) * L1.S * L * 4))) return rc;
         L1.base = c->slots1.p;
@@ -933,6 +956,27 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         const uint32_t *rw = r + (r ? off * r_words : 0);
         int rwn = r_words;
+        if (direct_y) {
+            uint32_t *yp = (uint32_t *)c->scratch.p, *yq = yp + (size_t)L * k->pq_w;
+            RngKey rq = rk; rq.nonce ^= 0x7172737475767778ull;       // an independent stream for y_q
+            hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords, k->pq_w, (int)k->p.bits(),
+                               rk, (uint64_t)off, cnt, yp);
+            hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords + k->pq_w, k->pq_w,
+                               (int)k->q.bits(), rq, (uint64_t)off, cnt, yq);
+            hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+            pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lc.slot(SL_T3), S, L, Lc.B);
+            pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lc.slot(SL_T4), S, L, Lc.B);
+            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;
+            if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
+            hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
+                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+            if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
+            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
+                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+            if (pipe && (rc = pipe->after(off, cnt))) return rc;
+            continue;
+        }
         if (!r) {
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_nwords, nw, k->n_bits, rk,
                                (uint64_t)off, cnt, (uint32_t *)c->scratch.p);
