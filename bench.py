@@ -202,6 +202,11 @@ def main():
         secondary["crt_decrypt_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
         ok = torch.equal(low, m[:nd])
         secondary["decrypt_roundtrip_ok"] = bool(ok)
+        # opt-in short-plaintext decrypt (plaintext < p, true of every FedTree codec value): p half only
+        pl.decrypt_u64_dev(c[:nd], low, short=True)
+        dev.sync()
+        secondary["crt_decrypt_short_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        secondary["decrypt_short_roundtrip_ok"] = bool(torch.equal(low, m[:nd]))
         # public-key encrypt (a party without the factorization, party.h:118-142) and the
         # opt-in fixed-base randomizer (r = h^alpha, include/fthe.h FTHE_ENC_FIXED_BASE; not
         # the reference's uniform-r algorithm, so never the headline `value`)

@@ -60,6 +60,8 @@ _PROTOS = {
     "fthe_encrypt_u64": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_decrypt_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_decrypt": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "fthe_decrypt_short_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),
+    "fthe_decrypt_short": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_add_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_add": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_scalar_mul_u64_dev": (_I, [_P, _P, _P, _U64, _SZ, _P]),

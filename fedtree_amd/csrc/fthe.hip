@@ -199,6 +199,7 @@ struct fthe_key {
     int c_one = -1, c_one_n2 = -1, c_R2n2 = -1, c_nRn2 = -1, c_n2 = -1;
     int c_R2p = -1, c_R3p = -1, c_nRp = -1, c_R2q = -1, c_R3q = -1, c_nRq = -1;
     int c_p2 = -1, c_q2 = -1, c_2p2 = -1, c_qinvRp2 = -1;
+    int c_zero = -1;
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
@@ -439,6 +440,7 @@ static int key_finish(fthe_key *k) {
         if ((rc = upload_mod(k->mq, k->q, sh))) return rc;
         auto L_ = [&](const mpz_t x) { return to_limbs(x, S, RB); };
         k->c_one = k->add_const(L_(one));
+        k->c_zero = k->add_const(std::vector<uint32_t>(1, 0u));
         k->kp = (int)((k->p.bits() + RB - 1) / RB);
         k->kq = (int)((k->q.bits() + RB - 1) / RB);
         // --- CRT encrypt constants
@@ -1253,7 +1255,7 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
 // ---------------------------------------------------------------------------
 // Decrypt (CRT)
 static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low,
-                        uint32_t *m_full, HostPipe *pipe) {
+                        uint32_t *m_full, HostPipe *pipe, bool short_pt = false) {
     if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
     if (!k->priv) return FTHE_ERR_NOPRIV;
     Launch Lc;
@@ -1272,6 +1274,21 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         pack_rows(c->stream, src, cw, cnt, Lc.B * S,
                            Lc.slot(SL_IN1), S, L, Lc.B);
         if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
+        if (short_pt) {
+            // plaintext < p: m = m_p = L_p(c^(p-1) mod p^2) h_p mod p, the q half and the CRT skipped
+            hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,
+                               k->cst(k->c_pinv), k->kp, Lc.slot(SL_T1), L, Lc.B);
+            Lc.fill(SL_C0, k->c_hRp);
+            if ((rc = Lc.prog(k->pr_dec_hp, k->mp))) return rc;
+            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p), S, L, Lc.B);
+            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->kp,
+                               k->cst(k->c_zero), 1, Lc.slot(SL_OUTP), k->kp, L, cnt,
+                               m_full ? m_full + off * nw : (uint32_t *)nullptr, nw,
+                               m_low ? m_low + off : (uint64_t *)nullptr, Lc.B);
+            if (off + L < count) Lc.fill(SL_C0, k->c_R2p);
+            if (pipe && (rc = pipe->after(off, cnt))) return rc;
+            continue;
+        }
         if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) return rc;
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,
                            k->cst(k->c_pinv), k->kp, Lc.slot(SL_T1), L, Lc.B);
@@ -1300,6 +1317,11 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
 extern "C" int fthe_decrypt_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count,
                                 uint64_t *m_low, uint32_t *m_full) {
     return decrypt_impl(k, c, ct, count, m_low, m_full, nullptr);
+}
+
+extern "C" int fthe_decrypt_short_dev(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count,
+                                      uint64_t *m_low, uint32_t *m_full) {
+    return decrypt_impl(k, c, ct, count, m_low, m_full, nullptr, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -1827,7 +1849,8 @@ extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, siz
     return pipe.finish();
 }
 
-extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full) {
+static int decrypt_host(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full,
+                        bool short_pt) {
     if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     size_t cw = 2 * (size_t)k->n_words, nw = k->n_words;
@@ -1840,8 +1863,17 @@ extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t
     if (m_low) pipe.add_out(m_low, c->io[1].p, 8);
     if (m_full) pipe.add_out(m_full, c->io[2].p, nw * 4);
     if ((rc = decrypt_impl(k, c, (const uint32_t *)c->io[0].p, count, m_low ? (uint64_t *)c->io[1].p : nullptr,
-                           m_full ? (uint32_t *)c->io[2].p : nullptr, count ? &pipe : nullptr))) return rc;
+                           m_full ? (uint32_t *)c->io[2].p : nullptr, count ? &pipe : nullptr, short_pt))) return rc;
     return pipe.finish();
+}
+
+extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full) {
+    return decrypt_host(k, c, ct, count, m_low, m_full, false);
+}
+
+extern "C" int fthe_decrypt_short(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low,
+                                  uint32_t *m_full) {
+    return decrypt_host(k, c, ct, count, m_low, m_full, true);
 }
 
 static int pair_host(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,

@@ -221,13 +221,16 @@ class Paillier:
                    "encrypt")
         return out
 
-    def decrypt_u64(self, c, full=False):
-        """Low 64 bits of m = L(c^lambda mod n^2) mu mod n (paillier.cpp:153-156)."""
+    def decrypt_u64(self, c, full=False, short=False):
+        """Low 64 bits of m = L(c^lambda mod n^2) mu mod n (paillier.cpp:153-156).
+        short: plaintexts known to be < p (FedTree's codec values and their sums):
+        the p half of the CRT only (fthe_decrypt_short), half the work."""
         c = np.ascontiguousarray(c, dtype=np.uint32).reshape(-1, self._cw())
         cnt = len(c)
         low = np.zeros(cnt, dtype=np.uint64)
         fullw = np.zeros((cnt, self.n_words), dtype=np.uint32) if full else None
-        _lib.check(self.lib.fthe_decrypt(self._key, self.dev.ctx, _ptr(c), cnt, _ptr(low), _ptr(fullw)), "decrypt")
+        fn = self.lib.fthe_decrypt_short if short else self.lib.fthe_decrypt
+        _lib.check(fn(self._key, self.dev.ctx, _ptr(c), cnt, _ptr(low), _ptr(fullw)), "decrypt")
         return (low, fullw) if full else low
 
     def add_batch(self, a, b):
@@ -294,10 +297,11 @@ class Paillier:
                    "encrypt_dev")
         return out
 
-    def decrypt_u64_dev(self, c, out_low):
+    def decrypt_u64_dev(self, c, out_low, short=False):
         cnt = c.numel() // self._cw()
-        _lib.check(self.lib.fthe_decrypt_dev(self._key, self.dev.ctx, ctypes.c_void_p(c.data_ptr()), cnt,
-                                             ctypes.c_void_p(out_low.data_ptr()), None), "decrypt_dev")
+        fn = self.lib.fthe_decrypt_short_dev if short else self.lib.fthe_decrypt_dev
+        _lib.check(fn(self._key, self.dev.ctx, ctypes.c_void_p(c.data_ptr()), cnt,
+                      ctypes.c_void_p(out_low.data_ptr()), None), "decrypt_dev")
         return out_low
 
     def add_dev(self, a, b, out):

@@ -129,6 +129,17 @@ int fthe_decrypt_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t cou
 int fthe_decrypt(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t count,
                  uint64_t *m_low, uint32_t *m_full);
 
+/* Short-plaintext decryption (opt-in): only the p half of the CRT,
+ * m = L_p(c^(p-1) mod p^2) h_p mod p -- equal to the plaintext when it is
+ * below p.  FedTree's plaintexts always are: 64-bit fixed-point codes and
+ * sums / differences of them (common.h:81-86, 253-337) stay below 2^130 for
+ * any batch that fits in memory, and p has n_bits/2 >= 256 bits.  Half the
+ * work of fthe_decrypt; a plaintext >= p decrypts to m mod p. */
+int fthe_decrypt_short_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t count,
+                           uint64_t *m_low, uint32_t *m_full);
+int fthe_decrypt_short(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t count,
+                       uint64_t *m_low, uint32_t *m_full);
+
 /* ---- homomorphic add: x*y mod n^2 (paillier.cpp:103) ------------------------
  * Replaces Paillier::add / Paillier_GMP::add (paillier_gmp.cpp:16) and
  * Paillier_GPU::add (paillier_gpu.cu:58).  Alias-safe: out may equal a or b
