@@ -105,7 +105,9 @@ enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL
                      // fixed-base tables gathered by a per-lane digit (rows[0] table,
                      // rows[1] u8 digits [window][L]); one-lane: radix-2^B entries,
                      // four-lane: canonical 128-word rows
-                     OP_LOADGD = 14, OP_MULGD = 15 };
+                     OP_LOADGD = 14, OP_MULGD = 15,
+                     // the same with 16-bit windows (u16 digits, entry j*65536 + digit)
+                     OP_LOADGD16 = 16, OP_MULGD16 = 17 };
 
 struct Prog {
     std::vector<uint32_t> w;
@@ -134,6 +136,8 @@ struct Prog {
     void mulwg(int t) { op(OP_MULWG, t); montmuls += 1; }
     void loadgd(int j) { op(OP_LOADGD, j); }
     void mulgd(int j) { op(OP_MULGD, j); montmuls += 1; }
+    void loadgd16(int j) { op(OP_LOADGD16, j); }
+    void mulgd16(int j) { op(OP_MULGD16, j); montmuls += 1; }
     void end() { op(OP_END, 0); }
 
     // X <- X^(2^j - 1) (Montgomery domain) by the all-ones addition chain:

@@ -213,7 +213,8 @@ struct fthe_key {
     struct FixedBase {
         bool ready = false;
         Mpz h, hs;
-        int nwin_pub = 0, nwin_crt = 0;   // 8-bit windows of alpha: public / per prime
+        int window = 16;                  // bits per window (digit width)
+        int nwin_pub = 0, nwin_crt = 0;   // windows of alpha: public / per prime
         int ew_pub = 0, ew_crt = 0;       // words per table entry
         bool pub = false, pub_rows = false;
         uint32_t *d_tab_pub = nullptr, *d_tab_p = nullptr, *d_tab_q = nullptr, *d_prog = nullptr;
@@ -903,6 +904,28 @@ struct HostPipe {
 
 }  // namespace
 
+// Programs built per call (k-way product, scalar exponent, table widening) go
+// through a per-context device buffer; the stream is drained before it is rewritten.
+static int upload_dyn_prog(fthe_ctx *c, const Prog &p, fthe_key::PH &ph, DevBuf &buf) {
+    HIPOK(hipStreamSynchronize(c->stream));
+    int rc = buf.ensure(p.w.size() * 4);
+    if (rc) return rc;
+    HIPOK(hipMemcpy(buf.p, p.w.data(), p.w.size() * 4, hipMemcpyHostToDevice));
+    ph.off = 0; ph.mm = p.montmuls;
+    return FTHE_OK;
+}
+namespace {
+// Launch with an explicit (dynamic) program pointer.
+int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod, const void *const *rows = nullptr,
+               int nrows = 0) {
+    if (mod.m.S != Lc.S) return FTHE_ERR_ARG;
+    int rc = launch_montprog(Lc.c, Lc.base, Lc.S, Lc.L, prog, mod, mm, Lc.live, rows, nrows);
+    if (rc) return rc;
+    Lc.mm += mm * (double)Lc.live;
+    return FTHE_OK;
+}
+}  // namespace
+
 // ---------------------------------------------------------------------------
 // Encrypt
 static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *alpha,
@@ -1073,12 +1096,62 @@ std::function<void(const mpz_t, uint32_t *)> fb_store_limbs(const MontMod &M) {
     };
 }
 
-int fb_build(fthe_key *k, const mpz_t h) {
+// Widen 8-bit-window tables to 16-bit windows on the device: entry (j, d) of the
+// wide table = MontMul(entry (2j, d & 255), entry (2j+1, d >> 8)) of the narrow one
+// (Montgomery forms multiply to the Montgomery form of the product), one launch of
+// 65,536 lanes per wide window.  One-lane kernels: the product leaves in a slot and
+// k_slot_to_entries transposes it into entries; the four-lane kernel writes the
+// canonical rows itself (STOREW).
+int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32_t *tab8, int nwin16, int ew,
+             bool rows_form, uint32_t **out) {
+    const size_t W16 = 65536;
+    int rc;
+    if (hipMalloc((void **)out, (size_t)nwin16 * W16 * ew * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    Launch Lc;
+    if ((rc = begin_call(c, k, W16, Lc, nslots_for(k), sh))) return rc;
+    if ((size_t)Lc.L < W16) return FTHE_ERR_UNSUPPORTED;
+    Lc.live = W16;
+    // digits: row 0 = g & 255, row 1 = g >> 8 (u8, row stride L)
+    if ((rc = c->hb[0].ensure(2 * (size_t)Lc.L))) return rc;
+    std::vector<uint8_t> dg(2 * (size_t)Lc.L, 0);
+    for (size_t g = 0; g < W16; g++) { dg[g] = (uint8_t)(g & 255); dg[Lc.L + g] = (uint8_t)(g >> 8); }
+    HIPOK(hipMemcpy(c->hb[0].p, dg.data(), dg.size(), hipMemcpyHostToDevice));
+    Prog pr;
+    if (rows_form) { pr.loadgd(0); pr.mulgd(1); pr.storew(2); }
+    else { pr.loadgd(0); pr.mulgd(1); pr.storex(SL_OUTP); }
+    pr.end();
+    fthe_key::PH ph;
+    if ((rc = upload_dyn_prog(c, pr, ph, c->io[3]))) return rc;
+    const size_t eb = (size_t)ew * 4;
+    for (int j = 0; j < nwin16; j++) {
+        uint32_t *dst = *out + (size_t)j * W16 * ew;
+        const void *rows[3] = {(const uint8_t *)tab8 + (size_t)(2 * j) * 256 * eb, c->hb[0].p, dst};
+        if ((rc = launch_dyn(Lc, c->io[3].p, pr.montmuls, mod, rows, rows_form ? 3 : 2))) return rc;
+        if (!rows_form)
+            hipLaunchKernelGGL(k_slot_to_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
+                               Lc.slot(SL_OUTP), Lc.S, Lc.L, W16, ew, dst);
+    }
+    HIPOK(hipStreamSynchronize(c->stream));
+    return end_call(c, Lc);
+}
+
+// FTHE_FB_WINDOW=8 keeps the host-built 8-bit tables; the default widens them to 16 bits
+// on the device (2x fewer products per encryption, 65536 entries per window).
+int fb_window() {
+    const char *e = getenv("FTHE_FB_WINDOW");
+    return e && atoi(e) == 8 ? 8 : 16;
+}
+
+int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
     fthe_key::FixedBase &F = k->fb;
     if (mpz_sgn(h) <= 0 || mpz_cmp(h, k->n) >= 0) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipStreamSynchronize(c->stream));
     for (uint32_t **p : {&F.d_tab_pub, &F.d_tab_p, &F.d_tab_q, &F.d_prog})
         if (*p) { hipFree(*p); *p = nullptr; }
     F.ready = false;
+    F.window = fb_window();
+    const bool wide = F.window == 16;
     mpz_set(F.h, h);
     mpz_powm(F.hs, h, k->n, k->n2);
     std::vector<uint32_t> progs;
@@ -1086,29 +1159,41 @@ int fb_build(fthe_key *k, const mpz_t h) {
         off = progs.size(); mm = p.montmuls;
         progs.insert(progs.end(), p.w.begin(), p.w.end());
     };
+    // the exponent program: X = entry(0); X <- X entry(j), j = 1 .. nwin-1
+    auto expo = [&](Prog &e, int nwin) {
+        if (wide) { e.loadgd16(0); for (int j = 1; j < nwin; j++) e.mulgd16(j); }
+        else { e.loadgd(0); for (int j = 1; j < nwin; j++) e.mulgd(j); }
+    };
     int rc;
     // public-key form: one-lane n^2 kernels, or the four-lane kernel's 128-word rows
     F.pub = k->pub_ok && (k->sn2.lanes == 1 || k->rowio);
     if (F.pub) {
-        F.nwin_pub = (k->n_bits + 64 + 7) / 8;
+        const int nwin16 = (k->n_bits + 64 + 15) / 16;          // alpha: n_bits + 64 bits
+        F.nwin_pub = wide ? nwin16 : 2 * nwin16;
         F.pub_rows = k->sn2.lanes == 4;
         const MontMod &M = k->mn2.m;
         std::vector<uint32_t> tab;
         if (F.pub_rows) {
             F.ew_pub = 2 * k->n_words;
             const int cw = F.ew_pub;
-            tab = fb_table(F.hs, k->n2, F.nwin_pub, cw, [&M, cw](const mpz_t x, uint32_t *dst) {
+            tab = fb_table(F.hs, k->n2, 2 * nwin16, cw, [&M, cw](const mpz_t x, uint32_t *dst) {
                 Mpz t; mpz_mul(t, x, M.R); mpz_mod(t, t, M.N);
                 mpz_to_words(t, dst, cw);
             });
         } else {
             F.ew_pub = 4 * ((M.S + 3) / 4);
-            tab = fb_table(F.hs, k->n2, F.nwin_pub, F.ew_pub, fb_store_limbs(M));
+            tab = fb_table(F.hs, k->n2, 2 * nwin16, F.ew_pub, fb_store_limbs(M));
         }
         if ((rc = fb_upload(tab, &F.d_tab_pub))) return rc;
+        if (wide) {
+            uint32_t *t16 = nullptr;
+            rc = fb_widen(k, c, k->mn2, k->sn2, F.d_tab_pub, nwin16, F.ew_pub, F.pub_rows, &t16);
+            hipFree(F.d_tab_pub);
+            F.d_tab_pub = t16;
+            if (rc) return rc;
+        }
         Prog e;
-        e.loadgd(0);
-        for (int j = 1; j < F.nwin_pub; j++) e.mulgd(j);
+        expo(e, F.nwin_pub);
         e.storex(SL_SAVED);
         e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);   // (1 + m n) hs^alpha
         if (F.pub_rows) e.storew(2); else e.storex(SL_OUTP);
@@ -1116,16 +1201,24 @@ int fb_build(fthe_key *k, const mpz_t h) {
         add(e, F.off_pub, F.mm_pub);
     }
     if (k->priv) {
-        F.nwin_crt = (int)((std::max(k->p.bits(), k->q.bits()) + 64 + 7) / 8);
+        const int nwin16 = (int)((std::max(k->p.bits(), k->q.bits()) + 64 + 15) / 16);
+        F.nwin_crt = wide ? nwin16 : 2 * nwin16;
         F.ew_crt = 4 * ((k->spq.S + 3) / 4);
         for (int side = 0; side < 2; side++) {
             const DevMod &D = side ? k->mq2 : k->mp2;
+            uint32_t **dt = side ? &F.d_tab_q : &F.d_tab_p;
             Mpz hsP; mpz_mod(hsP, F.hs, D.m.N);
-            std::vector<uint32_t> tab = fb_table(hsP, D.m.N, F.nwin_crt, F.ew_crt, fb_store_limbs(D.m));
-            if ((rc = fb_upload(tab, side ? &F.d_tab_q : &F.d_tab_p))) return rc;
+            std::vector<uint32_t> tab = fb_table(hsP, D.m.N, 2 * nwin16, F.ew_crt, fb_store_limbs(D.m));
+            if ((rc = fb_upload(tab, dt))) return rc;
+            if (wide) {
+                uint32_t *t16 = nullptr;
+                rc = fb_widen(k, c, D, k->spq, *dt, nwin16, F.ew_crt, false, &t16);
+                hipFree(*dt);
+                *dt = t16;
+                if (rc) return rc;
+            }
             Prog e;
-            e.loadgd(0);
-            for (int j = 1; j < F.nwin_crt; j++) e.mulgd(j);
+            expo(e, F.nwin_crt);
             e.storex(SL_SAVED);
             e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
             e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
@@ -1152,7 +1245,7 @@ int fb_ensure(fthe_key *k, fthe_ctx *c) {
     Mpz h, nm1; mpz_sub_ui(nm1, k->n, 1);
     mpz_urandomm(h, st, nm1); mpz_add_ui(h, h, 1);
     gmp_randclear(st);
-    return fb_build(k, h);
+    return fb_build(k, c, h);
 }
 
 }  // namespace
@@ -1168,15 +1261,15 @@ extern "C" int fthe_key_fixed_base(fthe_key *k, fthe_ctx *c, const uint32_t *h, 
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipDeviceSynchronize());            // no call may still read the old tables
     Mpz hh; mpz_from_words(hh, h, h_words);
-    return fb_build(k, hh);
+    return fb_build(k, c, hh);
 }
 
 extern "C" int fthe_key_fixed_base_info(fthe_key *k, int *alpha_bits_public, int *alpha_bits_crt, uint32_t *hs) {
     if (!k) return FTHE_ERR_ARG;
     std::lock_guard<std::mutex> g(k->fb_mu);
     if (!k->fb.ready) return FTHE_ERR_ARG;
-    if (alpha_bits_public) *alpha_bits_public = k->fb.pub ? 8 * k->fb.nwin_pub : 0;
-    if (alpha_bits_crt) *alpha_bits_crt = k->priv ? 8 * k->fb.nwin_crt : 0;
+    if (alpha_bits_public) *alpha_bits_public = k->fb.pub ? k->fb.window * k->fb.nwin_pub : 0;
+    if (alpha_bits_crt) *alpha_bits_crt = k->priv ? k->fb.window * k->fb.nwin_crt : 0;
     if (hs) mpz_to_words(k->fb.hs, hs, 2 * k->n_words);
     return FTHE_OK;
 }
@@ -1187,12 +1280,12 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
     if (rc) return rc;
     const fthe_key::FixedBase &F = k->fb;
     if (!crt && !F.pub) return FTHE_ERR_UNSUPPORTED;
-    const int nwin = crt ? F.nwin_crt : F.nwin_pub;
-    if (alpha && (a_words <= 0 || a_words > (8 * nwin + 31) / 32)) return FTHE_ERR_ARG;
+    const int nwin = crt ? F.nwin_crt : F.nwin_pub, bpd = F.window / 8;   // bytes per digit
+    if (alpha && (a_words <= 0 || a_words > (F.window * nwin + 31) / 32)) return FTHE_ERR_ARG;
     Launch Lc;
     if ((rc = begin_call(c, k, count, Lc, nslots_for(k), crt ? k->spq : k->sn2))) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
-    const size_t dig_bytes = (size_t)nwin * L;                 // [window][L] u8, per side
+    const size_t dig_bytes = (size_t)nwin * L * bpd;           // [window][L] digits, per side
     if ((rc = c->scratch.ensure(2 * dig_bytes))) return rc;
     uint8_t *dig_p = (uint8_t *)c->scratch.p, *dig_q = dig_p + dig_bytes;
     RngKey rk{};
@@ -1215,11 +1308,11 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
         const int sides = crt && !alpha ? 2 : 1;
         if (alpha) {
             hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, alpha + off * a_words, a_words,
-                               cnt, nwin, L, dig_p);
+                               cnt, nwin, L, bpd, dig_p);
         } else {
             for (int sd = 0; sd < sides; sd++)
                 hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, rk, (uint64_t)off, cnt, nwin, L,
-                                   sd, sd ? dig_q : dig_p);
+                                   bpd, sd, sd ? dig_q : dig_p);
         }
         hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (crt) {
@@ -1366,25 +1459,9 @@ extern "C" int fthe_sub_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const u
 
 // Programs built per call (k-way product, scalar exponent) go through a
 // per-context device buffer; the stream is drained before it is rewritten.
-static int upload_dyn_prog(fthe_ctx *c, const Prog &p, fthe_key::PH &ph, DevBuf &buf) {
-    HIPOK(hipStreamSynchronize(c->stream));
-    int rc = buf.ensure(p.w.size() * 4);
-    if (rc) return rc;
-    HIPOK(hipMemcpy(buf.p, p.w.data(), p.w.size() * 4, hipMemcpyHostToDevice));
-    ph.off = 0; ph.mm = p.montmuls;
-    return FTHE_OK;
-}
 
 namespace {
 // Launch with an explicit (dynamic) program pointer.
-int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod, const void *const *rows = nullptr,
-               int nrows = 0) {
-    if (mod.m.S != Lc.S) return FTHE_ERR_ARG;
-    int rc = launch_montprog(Lc.c, Lc.base, Lc.S, Lc.L, prog, mod, mm, Lc.live, rows, nrows);
-    if (rc) return rc;
-    Lc.mm += mm * (double)Lc.live;
-    return FTHE_OK;
-}
 }  // namespace
 
 // out[i] = prod_j x[j*count + i] mod n^2.

@@ -36,6 +36,7 @@ Ops (uint32 pairs, read with s_load from the program buffer):
    15 MULGD   j     X <- MontMul(table entry j*256 + dig[j][g], X)  rows[0] = table
                     of entries of EW = 4*ceil(S/4) radix-2^B words, rows[1] = u8
                     digit array [window][L])
+   16/17            the same with 16-bit windows: u16 digits, entry j*65536 + dig
 
 Slot memory: slot s, limb k, lane g at  slots + s*slot_stride + k*L*4 + g*4
 (limb-major, lane-interleaved: every global access is fully coalesced).
@@ -143,7 +144,8 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
                       (5, '.Laddslot'), (6, '.Laddsmall'), (12, '.Lprefa'), (13, '.Lmula'),
-                      (14, '.Lloadxgd'), (15, '.Lmulgd')):
+                      (14, '.Lloadxgd'), (15, '.Lmulgd'),
+                      (16, '.Lloadxgd16'), (17, '.Lmulgd16')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -315,41 +317,48 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
     # rows[0], EW words each; the digit byte array rows[1] is [window][L].  The
     # entry lands in the free T registers (dwordx4 loads), then X or the LDS A column.
     EW = 4 * ((S + 3) // 4)
-    assert 2 * NT >= EW and TB % 2 == 0
+    assert 2 * NT >= EW + 2 and TB % 2 == 0
 
-    def gather_entry():
+    def gather_entry(wide):
+        """Entry (j << W) | dig[j][g] of the table at rows[0] (W = 8, or 16 when
+        wide: u16 digits) -> v[TB+2 ..]; 64-bit entry address (tables > 4 GiB)."""
         e('  s_load_dwordx2 s[16:17], s[0:1], 0x30')        # digit array
         e('  s_lshr_b32 s14, s10, 2')                        # L
         e('  s_mul_i32 s14, s14, s15')                       # j*L
+        if wide:
+            e('  s_lshl_b32 s14, s14, 1')                    # u16 digits
         e('  s_waitcnt lgkmcnt(0)')
         e('  s_add_u32 s16, s16, s14')
         e('  s_addc_u32 s17, s17, 0')
-        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 2, v{V_GOFF}')      # lane index g
-        e(f'  global_load_ubyte v{V_TMP}, v{V_TMP}, s[16:17]')
+        e(f'  v_lshrrev_b32_e32 v{V_TMP}, {1 if wide else 2}, v{V_GOFF}')   # g (bytes: g * digit size)
+        e(f'  global_load_{"ushort" if wide else "ubyte"} v{V_TMP}, v{V_TMP}, s[16:17]')
         e('  s_load_dwordx2 s[16:17], s[0:1], 0x28')        # table
-        e('  s_lshl_b32 s14, s15, 8')                        # j*256
+        e(f'  s_lshl_b32 s14, s15, {16 if wide else 8}')     # j << W
+        e(f'  v_mov_b32_e32 v{V_TMP + 1}, {4 * EW}')
         e('  s_waitcnt vmcnt(0) lgkmcnt(0)')
         e(f'  v_or_b32_e32 v{V_TMP}, s14, v{V_TMP}')
-        e(f'  v_mul_u32_u24_e32 v{V_TMP}, {4 * EW}, v{V_TMP}')
+        e(f'  v_mad_u64_u32 v[{TB}:{TB + 1}], vcc, v{V_TMP}, v{V_TMP + 1}, s[16:17]')
         for i in range(EW // 4):
-            e(f'  global_load_dwordx4 v[{TB + 4 * i}:{TB + 4 * i + 3}], v{V_TMP}, s[16:17] offset:{16 * i}')
+            e(f'  global_load_dwordx4 v[{TB + 2 + 4 * i}:{TB + 5 + 4 * i}], v[{TB}:{TB + 1}], off offset:{16 * i}')
         e('  s_waitcnt vmcnt(0)')
 
-    e('.Lloadxgd:')
-    gather_entry()
-    for k in range(S):
-        e(f'  v_mov_b32_e32 {X(k)}, v{TB + k}')
-    e('  s_branch .Lprog')
+    for wide in (False, True):
+        sfx = "16" if wide else ""
+        e(f'.Lloadxgd{sfx}:')
+        gather_entry(wide)
+        for k in range(S):
+            e(f'  v_mov_b32_e32 {X(k)}, v{TB + 2 + k}')
+        e('  s_branch .Lprog')
+        e(f'.Lmulgd{sfx}:')
+        gather_entry(wide)
+        for k in range(S):
+            e(f'  ds_write_b32 v{V_LDSA}, v{TB + 2 + k} offset:{k * 256}')
+            if k % 8 == 7:
+                e('  s_waitcnt lgkmcnt(0)')
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_mov_b32 s19, 0')
+        e('  s_branch .Lmontmul')
 
-    e('.Lmulgd:')
-    gather_entry()
-    for k in range(S):
-        e(f'  ds_write_b32 v{V_LDSA}, v{TB + k} offset:{k * 256}')
-        if k % 8 == 7:
-            e('  s_waitcnt lgkmcnt(0)')
-    e('  s_waitcnt lgkmcnt(0)')
-    e('  s_mov_b32 s19, 0')
-    e('  s_branch .Lmontmul')
 
     # SQR: count in s15.  Fully unrolled Montgomery squaring: a = X is in
     # registers (no LDS), only the j >= i half of the a*X products is formed
@@ -605,7 +614,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_waitcnt lgkmcnt(0)')
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
                       (5, '.Laddslot'), (6, '.Laddsmall'), (7, '.Lloadw'), (8, '.Lmulw'),
-                      (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg'), (14, '.Lloadwd'), (15, '.Lmulwd')):
+                      (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg'), (14, '.Lloadwd'), (15, '.Lmulwd'),
+                      (16, '.Lloadwd16'), (17, '.Lmulwd16')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -791,22 +801,26 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
 
     # Gathered rows: LOADWG / MULWG t read row idx[g] of the array at rows[0], idx an
     # int64 array at rows[t] (one entry per ciphertext of the launch); idx < 0 -> 1.
-    def load_gather_limbs(dst, digits=False):
+    def load_gather_limbs(dst, digits=False, wide=False):
         if digits:
-            # fixed-base table: row j*256 + dig[j][g] of rows[0]; u8 digit array
-            # [window][L] at rows[1]; arg = window j
+            # fixed-base table: row (j << W) | dig[j][g] of rows[0]; digit array
+            # [window][L] (u8, or u16 when wide: W = 16) at rows[1]; arg = window j
             e('  s_load_dwordx2 s[32:33], s[0:1], 0x30')           # digit array
             e('  s_load_dwordx2 s[30:31], s[0:1], 0x28')           # table rows
             e('  s_lshr_b32 s16, s10, 2')                           # L
             e('  s_mul_i32 s16, s16, s15')                          # j*L
+            if wide:
+                e('  s_lshl_b32 s16, s16, 1')
             e('  s_waitcnt lgkmcnt(0)')
             e('  s_add_u32 s32, s32, s16')
             e('  s_addc_u32 s33, s33, 0')
             live_mask()
             e('  s_mov_b64 s[34:35], exec')
             e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')          # g
-            e(f'  global_load_ubyte v{V_TMP}, v{V_TMP}, s[32:33]')
-            e('  s_lshl_b32 s16, s15, 8')                           # j*256
+            if wide:
+                e(f'  v_lshlrev_b32_e32 v{V_TMP}, 1, v{V_TMP}')
+            e(f'  global_load_{"ushort" if wide else "ubyte"} v{V_TMP}, v{V_TMP}, s[32:33]')
+            e(f'  s_lshl_b32 s16, s15, {16 if wide else 8}')        # j << W
             e('  s_waitcnt vmcnt(0)')
             e(f'  v_or_b32_e32 v{V_TMP}, s16, v{V_TMP}')
             e(f'  v_mov_b32_e32 v{V_TMP + 1}, 0')
@@ -858,17 +872,18 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_mov_b32 s19, 0')
     e('  s_branch .Lmontmul')
 
-    e('.Lloadwd:')
-    load_gather_limbs(X, digits=True)
-    restore_exec()
-    e('  s_branch .Lprog')
-
-    e('.Lmulwd:')
-    load_gather_limbs(lambda j: f"v{A0 + j}", digits=True)
-    restore_exec()
-    write_a(lambda j: f"v{A0 + j}")
-    e('  s_mov_b32 s19, 0')
-    e('  s_branch .Lmontmul')
+    for wide in (False, True):
+        sfx = "16" if wide else ""
+        e(f'.Lloadwd{sfx}:')
+        load_gather_limbs(X, digits=True, wide=wide)
+        restore_exec()
+        e('  s_branch .Lprog')
+        e(f'.Lmulwd{sfx}:')
+        load_gather_limbs(lambda j: f"v{A0 + j}", digits=True, wide=wide)
+        restore_exec()
+        write_a(lambda j: f"v{A0 + j}")
+        e('  s_mov_b32 s19, 0')
+        e('  s_branch .Lmontmul')
 
     # STOREW: X (< 2N) -> X mod N -> row words.
     e('.Lstorew:')
