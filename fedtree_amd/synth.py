@@ -32,3 +32,18 @@ def logistic_gradients(n, seed=20261015):
     g = (p - y).astype(np.float32)
     h = np.maximum(p * (1.0 - p), np.float32(1e-16)).astype(np.float32)
     return g, h
+
+
+def exact_gradients(n, seed=20261015):
+    """(g, h) float32 pairs from integer-exact arithmetic only, for committed fixtures:
+    p = k / 2^24 (k uniform in [1, 2^24)), y ~ Bernoulli(0.5), g = p - y (exact),
+    h = p * (1 - p) (one IEEE float32 product, correctly rounded).  Unlike
+    logistic_gradients no libm call is involved, so the values -- and hence the
+    fixed-point plaintexts and ciphertexts -- are identical on every host."""
+    y = (splitmix64(seed, n, 3) >> np.uint64(63)).astype(np.float32)
+    k = (splitmix64(seed, n, 4) >> np.uint64(40)).astype(np.int64)
+    k[k == 0] = 1
+    p = (k.astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float32)
+    g = (p - y).astype(np.float32)
+    h = (p * (np.float32(1.0) - p)).astype(np.float32)
+    return g, h
