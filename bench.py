@@ -106,9 +106,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FTHE_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- exercises the multi-rank
+    # path (barriers, max-over-ranks timing, rank-0 reporting) on a one-GPU box, where
+    # RCCL refuses two ranks on one device.  Never used for reported numbers.
+    rehearse = os.environ.get("FTHE_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
+    backend = "gloo" if rehearse else "nccl"
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group(backend)
+        else:
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
     from fedtree_amd.paillier import Device, Paillier
     from fedtree_amd.synth import logistic_gradients
     from fedtree_amd import _lib
@@ -152,7 +162,7 @@ def main():
                                   ctypes.byref(amacs)))
     lib.fthe_prof_enable(dev.ctx, 0)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     enc_total = world * 2 * P * a.steps
