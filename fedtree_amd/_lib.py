@@ -21,6 +21,7 @@ FTHE_ERR_NOMEM = -6
 FTHE_ENC_DEFAULT = 0
 FTHE_ENC_PUBLIC = 1
 FTHE_ENC_FIXED_BASE = 2
+FTHE_ENC_FIXED_BASE_EXACT = 4
 
 
 class FtheError(RuntimeError):
@@ -56,6 +57,8 @@ _PROTOS = {
     "fthe_key_export": (_I, [_P, _P, _P, _P, _P, _P]),
     "fthe_key_fixed_base": (_I, [_P, _P, _P, _I]),
     "fthe_key_fixed_base_info": (_I, [_P, _P, _P, _P]),
+    "fthe_key_fixed_base_exact": (_I, [_P, _P, _U64]),
+    "fthe_key_fixed_base_exact_info": (_I, [_P, _I, _I, _P, _P]),
     "fthe_encrypt_u64_dev": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_encrypt_u64": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_decrypt_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),

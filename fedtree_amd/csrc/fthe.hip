@@ -175,6 +175,7 @@ struct fthe_key {
         if (d_nwords) hipFree(d_nwords);
         if (d_pqwords) hipFree(d_pqwords);
         for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) hipFree(p);
+        for (uint32_t *p : {xb.d_tab[0], xb.d_tab[1], xb.d_prog}) if (p) hipFree(p);
     }
     // constant handles
     int add_const(const std::vector<uint32_t> &limbs) {
@@ -222,6 +223,19 @@ struct fthe_key {
         double mm_pub = 0, mm_crt = 0;
     } fb;
     std::mutex fb_mu;
+
+    // ---- exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT, key holder) ----
+    // Per prime P: three bases gam[i] = t_i^P mod P^2 whose t_i generate Z_P^*
+    // (checked for every prime l < 2^24 dividing P - 1), tables of 16-bit windows
+    // for exponents y_i < P; r^n mod P^2 is drawn as prod_i gam[i]^y_i.
+    struct ExactBase {
+        bool ready = false;
+        int nwin = 0, ew = 0;             // 16-bit windows per exponent, words per entry
+        Mpz gam[2][3];
+        uint32_t *d_tab[2] = {nullptr, nullptr}, *d_prog = nullptr;
+        size_t off[2] = {0, 0};
+        double mm = 0;
+    } xb;
 };
 
 // slot numbering shared by all programs
@@ -458,7 +472,14 @@ static int key_finish(fthe_key *k) {
         k->c_R3q = k->add_const(L_(k->mq2.m.R3));
         k->c_p2 = k->add_const(L_(p2));
         k->c_q2 = k->add_const(L_(q2));
-        mpz_mul_2exp(t, p2, 1);
+        // u = cp + K - cq (k_crt_enc_prep) with K = p^2 (floor(q^2 / p^2) + 1) > q^2 > cq:
+        // u >= 0 and u = cp - cq (mod p^2) whatever the ratio q / p (K = 2 p^2 failed for
+        // q > sqrt(2) p).  u < K + p^2 must stay a valid Montgomery operand: < R / 2.
+        mpz_fdiv_q(t, q2, p2); mpz_add_ui(t, t, 1); mpz_mul(t, t, p2);
+        {
+            Mpz lim; mpz_add(lim, t, p2); mpz_mul_2exp(lim, lim, 1);
+            if (mpz_cmp(lim, k->mp2.m.R) >= 0) return FTHE_ERR_UNSUPPORTED;
+        }
         k->c_2p2 = k->add_const(L_(t));
         Mpz qi; if (!mpz_invert(qi, q2, p2)) return FTHE_ERR_KEY;
         k->c_qinvRp2 = k->add_const(k->mp2.m.mont(qi));
@@ -516,7 +537,12 @@ static int key_finish(fthe_key *k) {
         // --- CRT decrypt constants
         k->c_p = k->add_const(L_(k->p));
         k->c_q = k->add_const(L_(k->q));
-        mpz_mul_2exp(t, k->p, 1);
+        // d = m_p + K - m_q (k_crt_dec_prep), K = p (floor(q / p) + 1) > q > m_q: see c_2p2
+        mpz_fdiv_q(t, k->q, k->p); mpz_add_ui(t, t, 1); mpz_mul(t, t, k->p);
+        {
+            Mpz lim; mpz_add(lim, t, k->p); mpz_mul_2exp(lim, lim, 1);
+            if (mpz_cmp(lim, k->mp.m.R) >= 0) return FTHE_ERR_UNSUPPORTED;
+        }
         k->c_2p = k->add_const(L_(t));
         Mpz m2k, pinv, qinv;
         mpz_set_ui(m2k, 1); mpz_mul_2exp(m2k, m2k, (mp_bitcnt_t)RB * k->kp);
@@ -930,11 +956,18 @@ int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod, const
 // Encrypt
 static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *alpha,
                            int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe);
+static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *y,
+                           int y_words, uint64_t rng_seed, uint32_t *out, HostPipe *pipe);
 static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r, int r_words,
                         uint64_t rng_seed, uint32_t *out, int flags, HostPipe *pipe) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
-    if (r && !(flags & FTHE_ENC_FIXED_BASE) && (r_words <= 0 || r_words > k->n_words)) return FTHE_ERR_ARG;
+    if (r && !(flags & (FTHE_ENC_FIXED_BASE | FTHE_ENC_FIXED_BASE_EXACT)) && (r_words <= 0 || r_words > k->n_words))
+        return FTHE_ERR_ARG;
     bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
+    if (flags & FTHE_ENC_FIXED_BASE_EXACT) {
+        if (!crt) return k->priv ? FTHE_ERR_UNSUPPORTED : FTHE_ERR_NOPRIV;
+        return encrypt_xb_impl(k, c, m, count, r, r_words, rng_seed, out, pipe);
+    }
     if (!crt && !k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     if (flags & FTHE_ENC_FIXED_BASE) return encrypt_fb_impl(k, c, m, count, r, r_words, rng_seed, out, crt, pipe);
     Launch Lc;
@@ -1308,7 +1341,7 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
         const int sides = crt && !alpha ? 2 : 1;
         if (alpha) {
             hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, alpha + off * a_words, a_words,
-                               cnt, nwin, L, bpd, dig_p);
+                               a_words, cnt, nwin, L, bpd, dig_p);
         } else {
             for (int sd = 0; sd < sides; sd++)
                 hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, rk, (uint64_t)off, cnt, nwin, L,
@@ -1334,6 +1367,191 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
             if ((rc = Lc.prog_raw(prog + F.off_pub, F.mm_pub, k->mn2, rows, 2))) return rc;
             unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L, cnt, out + off * cw, cw, Lc.B);
         }
+        if (pipe && (rc = pipe->after(off, cnt))) return rc;
+    }
+    return end_call(c, Lc);
+}
+
+// ---------------------------------------------------------------------------
+// Exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT; key holder, CRT).
+//
+// The reference's r is uniform in Z_n^* (paillier.cpp:127-133), so r^n mod P^2
+// (P = p, q) is uniform over G_P = {x^P mod P^2}, the cyclic subgroup of order
+// P - 1 of Z_{P^2}^* (r -> (r^Q mod P)^P), independently for p and q.
+// With bases gam_i = t_i^P mod P^2 such that <t_1, t_2, t_3> = Z_P^*, the map
+// (y_1, y_2, y_3) -> prod gam_i^y_i is a homomorphism from Z_{P-1}^3 ONTO G_P, so
+// uniform exponents (y_i uniform in [1, P), i.e. uniform mod P - 1) give an exactly
+// uniform element of G_P: the reference's distribution, with precomputed tables
+// (16-bit windows, 3 * ceil(bits(P)/16) gathered products, no squarings).
+// <t_1, t_2, t_3> = Z_P^* iff no prime l | P - 1 has all three t_i l-th powers;
+// every l < 2^24 is checked (bases redrawn until it holds).  A larger l escapes
+// the check with probability l^-3 per l, at most 43 * 2^-72 < 2^-66 per key.
+namespace {
+
+const std::vector<uint32_t> &small_primes() {           // primes below 2^24
+    static const std::vector<uint32_t> v = [] {
+        const uint32_t L = 1u << 24;
+        std::vector<uint8_t> comp(L, 0);
+        std::vector<uint32_t> ps;
+        for (uint32_t i = 2; i < L; i++) {
+            if (comp[i]) continue;
+            ps.push_back(i);
+            for (uint64_t j = (uint64_t)i * i; j < L; j += i) comp[j] = 1;
+        }
+        return ps;
+    }();
+    return v;
+}
+
+// three t_i in [2, P - 1) generating Z_P^* at every prime l < 2^24 dividing P - 1
+void xb_pick_bases(gmp_randstate_t st, const mpz_t P, Mpz t[3]) {
+    Mpz Pm1, e, x, span;
+    mpz_sub_ui(Pm1, P, 1);
+    mpz_sub_ui(span, P, 3);
+    std::vector<uint32_t> f;
+    for (uint32_t l : small_primes())
+        if (mpz_fdiv_ui(Pm1, l) == 0) f.push_back(l);
+    for (;;) {
+        for (int i = 0; i < 3; i++) { mpz_urandomm(t[i], st, span); mpz_add_ui(t[i], t[i], 2); }
+        bool ok = true;
+        for (uint32_t l : f) {
+            mpz_divexact_ui(e, Pm1, l);
+            bool all = true;
+            for (int i = 0; i < 3 && all; i++) { mpz_powm(x, t[i], e, P); all = mpz_cmp_ui(x, 1) == 0; }
+            if (all) { ok = false; break; }
+        }
+        if (ok) return;
+    }
+}
+
+int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
+    fthe_key::ExactBase &X = k->xb;
+    if (!k->priv) return FTHE_ERR_NOPRIV;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipStreamSynchronize(c->stream));
+    for (uint32_t **p : {&X.d_tab[0], &X.d_tab[1], &X.d_prog})
+        if (*p) { hipFree(*p); *p = nullptr; }
+    X.ready = false;
+    gmp_randstate_t st;
+    gmp_randinit_default(st);
+    Mpz sd;
+    mpz_set_ui(sd, seed ? seed : urandom64());
+    mpz_mul_2exp(sd, sd, 64);
+    mpz_add_ui(sd, sd, seed ? 0x5845584143544241ull : urandom64());
+    gmp_randseed(st, sd);
+    X.nwin = (int)((std::max(k->p.bits(), k->q.bits()) + 15) / 16);
+    X.ew = 4 * ((k->spq.S + 3) / 4);
+    std::vector<uint32_t> progs;
+    int rc = FTHE_OK;
+    for (int side = 0; side < 2 && rc == FTHE_OK; side++) {
+        const Mpz &P = side ? k->q : k->p;
+        const DevMod &D = side ? k->mq2 : k->mp2;
+        Mpz t[3];
+        xb_pick_bases(st, P, t);
+        std::vector<uint32_t> tab;                        // 8-bit windows, base after base
+        for (int b = 0; b < 3; b++) {
+            mpz_powm(X.gam[side][b], t[b], P, D.m.N);
+            std::vector<uint32_t> tb = fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, fb_store_limbs(D.m));
+            tab.insert(tab.end(), tb.begin(), tb.end());
+        }
+        uint32_t *d8 = nullptr;
+        if ((rc = fb_upload(tab, &d8))) break;
+        rc = fb_widen(k, c, D, k->spq, d8, 3 * X.nwin, X.ew, false, &X.d_tab[side]);
+        hipFree(d8);
+        if (rc) break;
+        Prog e;                                           // X = prod_j entry(j, digit j), then (1 + m n) X
+        e.loadgd16(0);
+        for (int j = 1; j < 3 * X.nwin; j++) e.mulgd16(j);
+        e.storex(SL_SAVED);
+        e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
+        e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+        X.off[side] = progs.size(); X.mm = e.montmuls;
+        progs.insert(progs.end(), e.w.begin(), e.w.end());
+    }
+    gmp_randclear(st);
+    if (rc) return rc;
+    if ((rc = fb_upload(progs, &X.d_prog))) return rc;
+    X.ready = true;
+    return FTHE_OK;
+}
+
+int xb_ensure(fthe_key *k, fthe_ctx *c) {
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    return k->xb.ready ? FTHE_OK : xb_build(k, c, 0);
+}
+
+}  // namespace
+
+extern "C" int fthe_key_fixed_base_exact(fthe_key *k, fthe_ctx *c, uint64_t seed) {
+    if (!k || !c || k->device != c->device) return FTHE_ERR_ARG;
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipDeviceSynchronize());            // no call may still read the old tables
+    return xb_build(k, c, seed);
+}
+
+extern "C" int fthe_key_fixed_base_exact_info(fthe_key *k, int side, int base, uint32_t *gamma, int *exp_words) {
+    if (!k || side < 0 || side > 1 || base < 0 || base > 2) return FTHE_ERR_ARG;
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    if (!k->xb.ready) return FTHE_ERR_ARG;
+    if (gamma) mpz_to_words(k->xb.gam[side][base], gamma, 2 * k->pq_w);
+    if (exp_words) *exp_words = k->pq_w;
+    return FTHE_OK;
+}
+
+static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *y,
+                           int y_words, uint64_t rng_seed, uint32_t *out, HostPipe *pipe) {
+    int rc = xb_ensure(k, c);
+    if (rc) return rc;
+    const fthe_key::ExactBase &X = k->xb;
+    const int pw = k->pq_w;
+    if (y && y_words != 6 * pw) return FTHE_ERR_ARG;         // y_{p,1..3}, y_{q,1..3}, pq_w words each
+    Launch Lc;
+    if ((rc = begin_call(c, k, count, Lc, nslots_for(k), k->spq))) return rc;
+    const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
+    const size_t dig_bytes = (size_t)3 * X.nwin * L * 2;    // per side: 3 exponents x nwin u16 digit rows
+    if ((rc = c->scratch.ensure(2 * dig_bytes + (size_t)L * pw * 4))) return rc;
+    uint8_t *dig[2] = {(uint8_t *)c->scratch.p, (uint8_t *)c->scratch.p + dig_bytes};
+    uint32_t *ytmp = (uint32_t *)((uint8_t *)c->scratch.p + 2 * dig_bytes);
+    RngKey rk{};
+    if (!y) {
+        uint64_t sd = rng_seed ? rng_seed : urandom64();
+        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(sd); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
+        rk.nonce = splitmix64(sd) ^ 0x6578616374626173ull;     // streams apart from k_rng_r's and k_rng_digits'
+    }
+    Lc.fill(SL_C1, k->c_nRp); Lc.fill(SL_C3, k->c_nRq);
+    Lc.fill(SL_T1, k->c_qinvRp2);
+    const size_t exp_bytes = (size_t)X.nwin * L * 2;
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        if (pipe && (rc = pipe->before(off, L, count))) return rc;
+        for (int side = 0; side < 2; side++)
+            for (int b = 0; b < 3; b++) {
+                uint8_t *dst = dig[side] + b * exp_bytes;
+                if (y) {
+                    hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream,
+                                       y + off * y_words + (size_t)(3 * side + b) * pw, y_words, pw, cnt, X.nwin, L, 2, dst);
+                } else {
+                    RngKey kb = rk;
+                    kb.nonce += (uint64_t)(3 * side + b + 1) << 56;           // one stream per (prime, base)
+                    hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords + side * pw, pw,
+                                       (int)(side ? k->q : k->p).bits(), kb, (uint64_t)off, cnt, ytmp);
+                    hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, ytmp, pw, pw, cnt, X.nwin,
+                                       L, 2, dst);
+                }
+            }
+        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+        const void *rp[2] = {X.d_tab[0], dig[0]};
+        const void *rq[2] = {X.d_tab[1], dig[1]};
+        if ((rc = Lc.prog_raw(X.d_prog + X.off[0], X.mm, k->mp2, rp, 2))) return rc;
+        if ((rc = Lc.prog_raw(X.d_prog + X.off[1], X.mm, k->mq2, rq, 2))) return rc;
+        hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
+                           k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+        if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+        hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
+        hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
+                           k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);
@@ -1910,7 +2128,8 @@ struct HostIO {
 extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
                                 int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
-    if (r && (r_words <= 0 || r_words > k->n_words + ((flags & FTHE_ENC_FIXED_BASE) ? 4 : 0))) return FTHE_ERR_ARG;
+    if (r && (r_words <= 0 || r_words > ((flags & FTHE_ENC_FIXED_BASE_EXACT) ? 3 * k->n_words
+                                         : k->n_words + ((flags & FTHE_ENC_FIXED_BASE) ? 4 : 0)))) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     size_t cw = 2 * (size_t)k->n_words;
     int rc;

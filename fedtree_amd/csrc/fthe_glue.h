@@ -25,7 +25,8 @@ __global__ void k_crt_dec_prep(uint32_t *mp, uint32_t *mq, const uint32_t *p, co
                                const uint32_t *two_p, uint32_t *d, int S, int L, int rb);
 __global__ void k_rng_r(const uint32_t *n_words, int nw, int nbits, RngKey key, uint64_t index0, size_t count, uint32_t *r);
 __global__ void k_rng_digits(RngKey key, uint64_t index0, size_t count, int nwin, int L, int bpd, int side, uint8_t *dig);
-__global__ void k_alpha_digits(const uint32_t *alpha, int aw, size_t count, int nwin, int L, int bpd, uint8_t *dig);
+__global__ void k_alpha_digits(const uint32_t *alpha, int stride, int aw, size_t count, int nwin, int L, int bpd,
+                               uint8_t *dig);
 __global__ void k_slot_to_entries(const uint32_t *slot, int S, int L, size_t count, int ew, uint32_t *out);
 // fthe_hist.hip: histogram CSR and the segmented-product planner
 __global__ void k_hist_count(const uint8_t *bin, int n_col, const int32_t *cut, int max_bin, const int32_t *inst,

@@ -180,9 +180,10 @@ class Paillier:
         return 2 * self.n_words
 
     @staticmethod
-    def _flags(public, fixed_base):
+    def _flags(public, fixed_base, fixed_base_exact=False):
         return (_lib.FTHE_ENC_PUBLIC if public else _lib.FTHE_ENC_DEFAULT) | \
-            (_lib.FTHE_ENC_FIXED_BASE if fixed_base else 0)
+            (_lib.FTHE_ENC_FIXED_BASE if fixed_base else 0) | \
+            (_lib.FTHE_ENC_FIXED_BASE_EXACT if fixed_base_exact else 0)
 
     def set_fixed_base(self, h=None):
         """(Re)build the fixed-base randomizer tables for base h (None: random h)."""
@@ -198,24 +199,45 @@ class Paillier:
                    "key_fixed_base_info")
         return ap.value, ac.value, int.from_bytes(hs.tobytes(), "little")
 
-    def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False):
+    def set_fixed_base_exact(self, seed=0):
+        """(Re)build the exact fixed-base tables (key holder; seed 0: bases from /dev/urandom)."""
+        _lib.check(self.lib.fthe_key_fixed_base_exact(self._key, self.dev.ctx, int(seed)), "key_fixed_base_exact")
+
+    def fixed_base_exact_info(self):
+        """([[gam_p1, gam_p2, gam_p3], [gam_q1, gam_q2, gam_q3]], words per exponent)."""
+        gam, ew = [[], []], ctypes.c_int()
+        buf = np.zeros(self.n_words, dtype=np.uint32)
+        for side in (0, 1):
+            for b in range(3):
+                _lib.check(self.lib.fthe_key_fixed_base_exact_info(self._key, side, b, _ptr(buf), ctypes.byref(ew)),
+                           "key_fixed_base_exact_info")
+                gam[side].append(int.from_bytes(buf.tobytes(), "little"))
+        return gam, ew.value
+
+    def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
         """c = g^m r^n mod n^2 for every m (paillier.cpp:134-137).
         r: None -> fresh uniform r per ciphertext from the device CSPRNG;
            else (count, n_words) uint32 words or a list of ints.
         fixed_base: r = h^alpha from the key's fixed-base tables (include/fthe.h);
-           r then injects alpha (ints or (count, words) uint32) instead of r."""
+           r then injects alpha (ints or (count, words) uint32) instead of r.
+        fixed_base_exact: r^n mod p^2, q^2 from the exact generator tables (key holder);
+           r then injects the six exponents (count, 6 * n_words/2) uint32 or 6-tuples of ints."""
         m = np.ascontiguousarray(m, dtype=np.uint64).reshape(-1)
         cnt = len(m)
         out = np.zeros((cnt, self._cw()), dtype=np.uint32)
         rw = None
         if r is not None:
+            if not isinstance(r, np.ndarray) and fixed_base_exact:
+                hw = self.n_words // 2
+                r = np.stack([np.concatenate([_words(int(x), hw) for x in t]) for t in r]) if cnt \
+                    else np.zeros((0, 6 * hw), np.uint32)
             if not isinstance(r, np.ndarray):
                 nw = self.n_words + (2 if fixed_base else 0)
                 if fixed_base and cnt:
                     nw = max(1, max((int(x).bit_length() + 31) // 32 for x in r))
                 r = np.stack([_words(int(x), nw) for x in r]) if cnt else np.zeros((0, nw), np.uint32)
             rw = np.ascontiguousarray(r, dtype=np.uint32).reshape(cnt, -1)
-        flags = self._flags(public, fixed_base)
+        flags = self._flags(public, fixed_base, fixed_base_exact)
         _lib.check(self.lib.fthe_encrypt_u64(self._key, self.dev.ctx, _ptr(m), cnt, _ptr(rw),
                                              rw.shape[1] if rw is not None else 0, int(seed), _ptr(out), flags),
                    "encrypt")
@@ -288,8 +310,8 @@ class Paillier:
         return out
 
     # ---- device-resident batch API (torch tensors on this device) -------------
-    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False, fixed_base=False):
-        flags = self._flags(public, fixed_base)
+    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
+        flags = self._flags(public, fixed_base, fixed_base_exact)
         rp = ctypes.c_void_p(r.data_ptr()) if r is not None else None
         rw = r.shape[-1] if r is not None else 0
         _lib.check(self.lib.fthe_encrypt_u64_dev(self._key, self.dev.ctx, ctypes.c_void_p(m.data_ptr()), m.numel(),

@@ -46,6 +46,7 @@ extern "C" {
 #define FTHE_ENC_DEFAULT      0   /* CRT when the private key is present */
 #define FTHE_ENC_PUBLIC       1   /* force the public-key (no CRT) formula */
 #define FTHE_ENC_FIXED_BASE   2   /* fixed-base randomizer r = h^alpha (see fthe_key_fixed_base) */
+#define FTHE_ENC_FIXED_BASE_EXACT 4  /* key holder: tables with the reference's r^n distribution (see fthe_key_fixed_base_exact) */
 
 typedef struct fthe_ctx fthe_ctx;
 typedef struct fthe_key fthe_key;
@@ -117,6 +118,29 @@ int fthe_encrypt_u64(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t cou
  *                            (2*n_words words, nullable), after a build. */
 int fthe_key_fixed_base(fthe_key *key, fthe_ctx *ctx, const uint32_t *h, int h_words);
 int fthe_key_fixed_base_info(fthe_key *key, int *alpha_bits_public, int *alpha_bits_crt, uint32_t *hs);
+
+/* ---- exact fixed-base randomizer (flag FTHE_ENC_FIXED_BASE_EXACT) -----------
+ * Key holder only (CRT; FTHE_ERR_NOPRIV without p, q).  The reference's r is
+ * uniform in Z_n^* (paillier.cpp:127-133); then r^n mod P^2 (P = p, q) is
+ * uniform over G_P = {x^P mod P^2}, cyclic of order P - 1, independently for p
+ * and q.  Here, per prime, three bases gam_i = t_i^P mod P^2 with
+ * <t_1, t_2, t_3> = Z_P^* (checked at every prime l < 2^24 dividing P - 1; a
+ * larger l escapes with probability < 2^-66 per key) and exponents y_i uniform
+ * in [1, P) from the device ChaCha20 stream give r^n mod P^2 = prod gam_i^y_i,
+ * exactly uniform over G_P: the reference's ciphertext distribution, computed as
+ * 3 * ceil(bits(P)/16) gathered products from 16-bit-window tables (~3.8 GB
+ * per prime at P-2048) instead of ~1.2 bits(P) squarings and products.
+ * Injected exponents (parity): r = y, r_words = 6 * (n_words / 2): per
+ * ciphertext y_{p,1}, y_{p,2}, y_{p,3}, y_{q,1}, y_{q,2}, y_{q,3}, n_words/2
+ * little-endian words each, each y < 2^(16 * ceil(bits(P)/16)).
+ * fthe_key_fixed_base_exact       (re)build bases and tables; seed 0 draws the
+ *                                 bases from /dev/urandom, else deterministic.
+ *                                 Built on first use otherwise.  Not concurrent
+ *                                 with calls that use the key.
+ * fthe_key_fixed_base_exact_info  gam_{side,base} (side 0 = p, 1 = q; n_words
+ *                                 words, nullable) and the words per exponent. */
+int fthe_key_fixed_base_exact(fthe_key *key, fthe_ctx *ctx, uint64_t seed);
+int fthe_key_fixed_base_exact_info(fthe_key *key, int side, int base, uint32_t *gamma, int *exp_words);
 
 /* ---- decrypt: m = L(c^lambda mod n^2) * mu mod n (paillier.cpp:153-156) ---
  * Computed with CRT over p^2, q^2 (identical canonical result).

@@ -468,3 +468,66 @@ def test_level_histogram_flow(dev, coracle):
         assert np.array_equal(arr_s, decode_fixed(per_bin))
         pref = np.concatenate([np.cumsum(per_bin[cut[f]:cut[f + 1]], dtype=np.uint64) for f in range(n_col)])
         assert np.array_equal(arr_p, decode_fixed(pref))
+
+
+def _next_prime(x):
+    """Smallest probable prime >= x (Miller-Rabin, 40 fixed bases; test keys only)."""
+    x |= 1
+    while True:
+        if all(x % sp for sp in (3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37)):
+            d, s = x - 1, 0
+            while d % 2 == 0:
+                d, s = d // 2, s + 1
+            for a in range(2, 42):
+                y = pow(a, d, x)
+                if y in (1, x - 1):
+                    continue
+                for _ in range(s - 1):
+                    y = y * y % x
+                    if y == x - 1:
+                        break
+                else:
+                    break
+            else:
+                return x
+        x += 2
+
+
+@pytest.mark.parametrize("shape", ["q_over_p_1.9", "p_over_q_1.9", "q_24_bits_longer"])
+def test_unbalanced_primes_vs_c_oracle(dev, coracle, shape):
+    """CRT recombination for any prime ratio: u = c_p + K - c_q needs K > q^2 (was 2 p^2,
+    wrong once q > sqrt(2) p) -- CRT/public encrypt and decrypt bit-exact vs the oracle."""
+    rng = np.random.default_rng(len(shape))
+    hw = 17
+    base = int.from_bytes(rng.bytes(62), "little") | (1 << 495) | (1 << 511)
+    base &= (1 << 512) - 1
+    if shape == "q_24_bits_longer":
+        p = _next_prime(base >> 12)                               # 500 bits
+        q = _next_prime(base << 12)                               # 524 bits
+    else:
+        a = _next_prime(base >> 1)                                # 511 bits
+        b = _next_prime(a * 19 // 10)                             # ~1.9 a, 512 bits
+        p, q = (a, b) if shape == "q_over_p_1.9" else (b, a)
+    pl = _pl(dev, p, q)
+    ok = coracle.key(pyoracle.to_words(p, hw), pyoracle.to_words(q, hw))
+    n = pl.modulus
+    cnt = 300
+    m = rng.integers(0, 2**64, cnt, dtype=np.uint64)
+    m[:3] = [0, 1, 2**64 - 1]
+    rs = [int.from_bytes(rng.bytes(pl.n_words * 4), "little") % (n - 1) + 1 for _ in range(cnt)]
+    rs[0], rs[1] = 1, n - 1
+    r = pyoracle.ints_to_words(rs, pl.n_words)
+    r_or = np.zeros((cnt, 2 * hw), np.uint32)                     # oracle rows: 2 * hw words
+    r_or[:, :pl.n_words] = r
+    want_or = ok.encrypt_batch(m, r_or)
+    assert not want_or[:, 2 * pl.n_words:].any()
+    want = np.ascontiguousarray(want_or[:, :2 * pl.n_words])
+    assert np.array_equal(pl.encrypt_u64(m, r=r), want)
+    if _public_supported(pl):
+        assert np.array_equal(pl.encrypt_u64(m, r=r, public=True), want)
+    low, full = pl.decrypt_u64(want, full=True)
+    assert np.array_equal(low, m)
+    assert np.array_equal(full, ok.decrypt_batch(want_or)[:, :pl.n_words])
+    c = pl.encrypt_u64(m, seed=4)                                 # device randomness (direct y)
+    assert np.array_equal(pl.decrypt_u64(c), m)
+    assert np.array_equal(pl.decrypt_u64(pl.encrypt_u64(m, seed=5, fixed_base_exact=True)), m)
