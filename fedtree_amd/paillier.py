@@ -425,8 +425,9 @@ class GHPairs:
     def __len__(self):
         return len(self.g)
 
-    def homo_encrypt(self, pl, r_g=None, r_h=None, seed=0):
-        """GHPair::homo_encrypt (common.h:125-134): encrypt g,h, zero them, set encrypted."""
+    def homo_encrypt(self, pl, r_g=None, r_h=None, seed=0, fixed_base_exact=False):
+        """GHPair::homo_encrypt (common.h:125-134): encrypt g,h, zero them, set encrypted.
+        fixed_base_exact: the key holder's table-driven randomizer (same distribution)."""
         if self.encrypted:
             return self
         m = np.concatenate([encode_fixed(self.g), encode_fixed(self.h)])
@@ -434,7 +435,7 @@ class GHPairs:
         if r_g is not None:
             r = np.concatenate([np.asarray(r_g, np.uint32).reshape(len(self), -1),
                                 np.asarray(r_h, np.uint32).reshape(len(self), -1)])
-        c = pl.encrypt_u64(m, r=r, seed=seed)
+        c = pl.encrypt_u64(m, r=r, seed=seed, fixed_base_exact=fixed_base_exact and r is None and pl.has_private)
         self.g_enc, self.h_enc = c[:len(self)], c[len(self):]
         self.paillier = pl
         self.g[:] = 0
@@ -523,9 +524,9 @@ class HEServer:
         """server.h:53-55: party.paillier = paillier (public part only)."""
         party.paillier = self.paillier.public()
 
-    def encrypt_gh_pairs(self, raw, seed=0):
+    def encrypt_gh_pairs(self, raw, seed=0, fixed_base_exact=False):
         """server.h:113-135."""
-        return raw.homo_encrypt(self.paillier, seed=seed)
+        return raw.homo_encrypt(self.paillier, seed=seed, fixed_base_exact=fixed_base_exact)
 
     def decrypt_gh_pairs(self, encrypted):
         """server.h:80-111."""

@@ -58,6 +58,10 @@ inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 
 
 class Paillier_HIP {
 public:
+    // Encryption mode of encrypt(): FTHE_ENC_DEFAULT (per-ciphertext exponentiation) or
+    // FTHE_ENC_FIXED_BASE_EXACT (precomputed generator tables, the same ciphertext
+    // distribution, ~4x the rate on the key holder; include/fthe.h).  Not in the reference.
+    int enc_flags = FTHE_ENC_DEFAULT;
     Paillier_HIP() : key_length(2048) {}
     Paillier_HIP(const Paillier_HIP &o) : key_length(o.key_length) { copy_public(o); }
     ~Paillier_HIP() { if (key_) fthe_key_destroy(key_); }
@@ -93,8 +97,10 @@ public:
         std::vector<uint64_t> m(2 * n);
         for (size_t i = 0; i < n; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
         std::vector<uint32_t> c(2 * n * (size_t)cw);
+        int flags = enc_flags;            // the exact fixed-base mode needs p, q: key holder only
+        if (!fthe_key_has_private(key_)) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
         fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
-                                          FTHE_ENC_DEFAULT), "encrypt");
+                                          flags), "encrypt");
         for (size_t i = 0; i < n; i++) {
             fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
             fthe_shim::from_words(d[i].h_enc, &c[(n + i) * cw], cw);

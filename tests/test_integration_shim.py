@@ -26,7 +26,8 @@ def test_shim_compiles_and_links(tmp_path):
 
 
 @pytest.mark.gpu
-def test_shim_runs_server_party_flow(tmp_path):
+@pytest.mark.parametrize("mode", ["default", "exact"])
+def test_shim_runs_server_party_flow(tmp_path, mode):
     exe = _build(str(tmp_path / "shim_test"))
-    r = subprocess.run([exe, "1024"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, "1024", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "shim OK" in r.stdout, r.stdout + r.stderr
