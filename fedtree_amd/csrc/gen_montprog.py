@@ -57,6 +57,10 @@ Q_VIA_MAD = not os.environ.get("FTHE_GEN_QLO")
 # four-lane kernel: accumulator window as a register ring (no window moves);
 # FTHE_GEN_NORING=1 restores the sliding window (A/B builds)
 QUAD_RING = not os.environ.get("FTHE_GEN_NORING")
+# four-lane kernel: every lane keeps the carry of its retiring column and hands
+# down only the low B bits (one DPP, no masks); FTHE_GEN_HANDOFF64=1 restores the
+# 64-bit hand-off with lane masks (A/B builds)
+QUAD_LOW_HANDOFF = not os.environ.get("FTHE_GEN_HANDOFF64")
 
 
 def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
@@ -960,6 +964,23 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
                 e(f'  v_mov_b32_dpp {q}, {q} quad_perm:[0,0,0,0] {DPP}')
             if j == 11:
                 e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * 64}')
+        if QUAD_LOW_HANDOFF:
+            # Every lane splits its lowest column c = lo + 2^B hi: hi stays in the lane's
+            # next column (absolute column c + 1 is the same lane's), lo moves to lane k-1
+            # as its new top column.  Lane 0's lo is 0 (the Montgomery step zeroed it), so
+            # the rotation [1,2,3,0] also hands lane 3 the zero its fresh column needs.
+            for j in range(Q):
+                e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {q}, {NV(j)}, {T(u + j)}')
+                if j == 3:
+                    e(f'  v_lshrrev_b64 {tmp}, {B}, {T(u)}')
+                if j == 9:
+                    e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
+                if j == 12:
+                    e(f'  v_and_b32_e32 {Tlo(u)}, {hex(MASK)}, {Tlo(u)}')
+            e(f'  v_mov_b32_dpp {Tlo(u + Q)}, {Tlo(u)} quad_perm:[1,2,3,0] {DPP}')
+            e(f'  v_mov_b32_e32 {Thi(u + Q)}, 0')
+            e('  s_waitcnt lgkmcnt(0)')
+            return
         for j in range(Q):
             e(f'  v_mad_u64_u32 {T(u + j)}, vcc, {q}, {NV(j)}, {T(u + j)}')
             if j == 3:
