@@ -68,6 +68,18 @@ size_t chunk_lanes() {
     return v;
 }
 
+// Launch size of the row-I/O ops (four-lane kernel, no slots but the R^k constant):
+// 4 chunks; FTHE_ROWIO_CHUNK overrides (A/B)
+size_t rowio_chunk_lanes() {
+    static size_t v = [] {
+        const char *e = getenv("FTHE_ROWIO_CHUNK");
+        size_t c = e ? (size_t)strtoull(e, nullptr, 10) : 4 * chunk_lanes();
+        c = (c + 1023) / 1024 * 1024;
+        return c < 1024 ? (size_t)1024 : c;
+    }();
+    return v;
+}
+
 // window width minimising table + multiplications for an e-bit exponent
 int best_window(size_t ebits) {
     int best = 1; double bc = 1e30;
@@ -781,12 +793,13 @@ struct Launch {
     }
 };
 
-int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots, Shape sh) {
+int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots, Shape sh,
+               size_t chunk = 0) {
     if (!c || !k) return FTHE_ERR_ARG;
     if (k->device != c->device) return FTHE_ERR_ARG;
     if (!sh.S) return FTHE_ERR_UNSUPPORTED;
     HIPOK(hipSetDevice(c->device));
-    size_t ch = chunk_lanes() / (size_t)sh.lanes;          // same slot footprint per chunk
+    size_t ch = (chunk ? chunk : chunk_lanes()) / (size_t)sh.lanes;    // same slot footprint per chunk
     ch = (ch + 255) / 256 * 256;
     size_t L = std::min(ch, (count + 255) / 256 * 256);
     if (L == 0) L = 256;
@@ -1642,7 +1655,10 @@ static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
+    // Row I/O reads and writes the AoS rows directly: the only slot is the R^2 constant, so
+    // device-resident calls take 4x larger launches (fewer launch tails) at no memory cost.
+    int rc = k->rowio ? begin_call(c, k, count, Lc, SL_C0 + 1, k->sn2, pipe ? 0 : rowio_chunk_lanes())
+                      : begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     Lc.fill(SL_C0, k->c_R2n2);
@@ -1688,13 +1704,14 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     if (!k || !c || kk <= 0 || kk > 64 || ((!x || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     const int base = nslots_for(k);               // inputs live after the standard slots
+    const bool rowio = k->rowio && kk + 1 <= 16;
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, base + kk, k->sn2);
+    int rc = rowio ? begin_call(c, k, count, Lc, SL_C0 + 1, k->sn2, rowio_chunk_lanes())   // constant slot only
+                   : begin_call(c, k, count, Lc, base + kk, k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
     std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
-    const bool rowio = k->rowio && kk + 1 <= 16;
     Prog p;
     if (rowio) {
         p.loadw(0);

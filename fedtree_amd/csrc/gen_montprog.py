@@ -61,6 +61,10 @@ QUAD_RING = not os.environ.get("FTHE_GEN_NORING")
 # down only the low B bits (one DPP, no masks); FTHE_GEN_HANDOFF64=1 restores the
 # 64-bit hand-off with lane masks (A/B builds)
 QUAD_LOW_HANDOFF = not os.environ.get("FTHE_GEN_HANDOFF64")
+# four-lane kernel: A-operand rows of 17 words (16 ciphertexts + 1 pad) so that the
+# four lanes of a quad, which write rows 38 apart, land in different LDS banks;
+# FTHE_GEN_LDS64=1 restores the unpadded 16-word rows (A/B builds)
+QUAD_ROWB = 64 if os.environ.get("FTHE_GEN_LDS64") else 68
 
 
 def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
@@ -568,7 +572,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
 
     o = []
     e = o.append
-    lds_per_wave = S * 64          # A[i][c]: 16 ciphertexts x 4 B per row
+    RB_ = QUAD_ROWB
+    lds_per_wave = S * RB_         # A[i][c]: 16 ciphertexts x 4 B per row (+ pad)
     lds_bytes = 4 * lds_per_wave
     DPP = "row_mask:0xf bank_mask:0xf"
     tmp = f"v[{V_TMP}:{V_TMP + 1}]"
@@ -607,7 +612,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e(f'  v_lshrrev_b32_e32 v{V_Q}, 2, v{V_TID}')
     e(f'  v_and_b32_e32 v{V_Q}, 15, v{V_Q}')
     e(f'  v_lshl_add_u32 v{V_LDSI}, v{V_Q}, 2, v{V_LDSI}')
-    e(f'  v_mul_u32_u24_e32 v{V_LDSW}, {Q * 64}, v{V_TMP}')        # k*Q*64 (tid dies here)
+    e(f'  v_mul_u32_u24_e32 v{V_LDSW}, {Q * RB_}, v{V_TMP}')       # k*Q*row (tid dies here)
     e(f'  v_add_u32_e32 v{V_LDSW}, v{V_LDSW}, v{V_LDSI}')
     e('  s_waitcnt vmcnt(0) lgkmcnt(0)')
 
@@ -714,7 +719,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
 
     def write_a(src):
         for k in range(Q):
-            e(f'  ds_write_b32 v{V_LDSW}, {src(k)} offset:{k * 64}')
+            e(f'  ds_write_b32 v{V_LDSW}, {src(k)} offset:{k * RB_}')
             if k % 8 == 7:
                 e('  s_waitcnt lgkmcnt(0)')
         e('  s_waitcnt lgkmcnt(0)')
@@ -963,7 +968,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
             if j == 9:
                 e(f'  v_mov_b32_dpp {q}, {q} quad_perm:[0,0,0,0] {DPP}')
             if j == 11:
-                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * 64}')
+                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * RB_}')
         if QUAD_LOW_HANDOFF:
             # Every lane splits its lowest column c = lo + 2^B hi: hi stays in the lane's
             # next column (absolute column c + 1 is the same lane's), lo moves to lane k-1
@@ -1016,14 +1021,14 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         if not QUAD_RING:
             for k in range(Q):
                 e(f'  v_mov_b64_e32 {T(k)}, {T(k + U)}')
-        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(STEP * 64)}, v{V_LDSI}')
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(STEP * RB_)}, v{V_LDSI}')
         e('  s_sub_u32 s18, s18, 1')
         e('  s_cmp_lg_u32 s18, 0')
         e('  s_cbranch_scc1 .Ltrip')
     for u in range(TL):
         iteration(u)
     TAIL = TL
-    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * STEP * 64)}, v{V_LDSI}')    # back to the column base
+    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * STEP * RB_)}, v{V_LDSI}')   # back to the column base
     # normalise T[TAIL .. TAIL+Q-1] (64-bit columns) into X, then across lanes
     e(f'  v_mov_b64_e32 {tmp}, 0')
     for k in range(Q):

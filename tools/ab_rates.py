@@ -42,6 +42,9 @@ def main():
         res["encrypt_public"] = best(lambda: pl.encrypt_u64_dev(m[:a.n // 4], c[:a.n // 4], seed=1, public=True), a.n // 4)
     k = a.n // 8
     res["sub"] = best(lambda: pl.sub_dev(c[:k], c[k:2 * k], o[:k]), k)
+    if os.environ.get("FTHE_AB_KWAY") == "1":          # 8-party merge, a.n // 8 bins: adds/s
+        x = c[:8 * k].reshape(8, k, cw)
+        res["kway_adds"] = best(lambda: pl.reduce_kway_dev(x, 8, o[:k]), 7 * k)
     print(json.dumps(res), flush=True)
 
 
