@@ -10,10 +10,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INTEG = os.path.join(ROOT, "integration")
 
 
-def _build(out):
-    cmd = ["g++", "-O2", "-std=c++17", "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
+def _build(out, src="shim_test.cpp"):
+    cmd = ["g++", "-O2", "-std=c++17", "-pthread", "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
            "-I" + os.path.join(ROOT, "include"), "-idirafter", "/opt/conda/include",
-           os.path.join(INTEG, "shim_test.cpp"), "-o", out, "-L" + os.path.join(ROOT, "fedtree_amd"), "-lfthe",
+           os.path.join(INTEG, src), "-o", out, "-L" + os.path.join(ROOT, "fedtree_amd"), "-lfthe",
            "-Wl,-rpath," + os.path.join(ROOT, "fedtree_amd"), "-l:libgmp.so.10"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
@@ -23,6 +23,7 @@ def _build(out):
 def test_shim_compiles_and_links(tmp_path):
     exe = _build(str(tmp_path / "shim_test"))
     assert os.path.exists(exe)
+    assert os.path.exists(_build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp"))
 
 
 @pytest.mark.gpu
@@ -31,3 +32,12 @@ def test_shim_runs_server_party_flow(tmp_path, mode):
     exe = _build(str(tmp_path / "shim_test"))
     r = subprocess.run([exe, "1024", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "shim OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["default", "exact"])
+def test_shim_concurrent_threads_share_one_key(tmp_path, mode):
+    """16 host threads, one shared key, a context per thread (the OpenMP call pattern)."""
+    exe = _build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp")
+    r = subprocess.run([exe, "1024", "16", "24", mode], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "concurrency OK" in r.stdout, r.stdout + r.stderr
