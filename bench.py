@@ -379,7 +379,30 @@ def main():
                              "decimal_bytes_per_ct": round(sum(len(x) for x in strs) / nw_, 1),
                              "binary_roundtrip_per_s": round(nw_ / t_bin), "binary_bytes_per_ct": sample.shape[1] * 4,
                              "roundtrip_ok": bool(np.array_equal(back, sample) and np.array_equal(g_, sample))}
-        del ch, strs, back, fr, g_
+        # the same decimal strings computed on the device (fthe_dec.hip), 1M device-resident ciphertexts
+        from fedtree_amd.paillier import ct_from_decimal_dev, ct_to_decimal_dev
+        nd_ = min(2 * P, 1 << 20)
+        ct_to_decimal_dev(dev, c[:4096])
+        dev.sync()
+        dbuf, doffs = ct_to_decimal_dev(dev, c[:nd_])
+        dev.sync()
+        t_denc = lib.fthe_last_kernel_ms(dev.ctx) * 1e-3
+        dback = ct_from_decimal_dev(dev, dbuf, doffs, c.shape[1])
+        dev.sync()
+        t_ddec = lib.fthe_last_kernel_ms(dev.ctx) * 1e-3
+        t0 = time.perf_counter()                                   # device ciphertexts -> host strings
+        hb_, ho_ = ct_to_decimal_dev(dev, c[:nd_])
+        ho_ = ho_.cpu()
+        hb_ = hb_[: int(ho_[-1])].cpu()
+        t_e2e = time.perf_counter() - t0
+        secondary["wire"].update({
+            "decimal_dev_ciphertexts": nd_, "decimal_encode_dev_per_s": round(nd_ / t_denc),
+            "decimal_decode_dev_per_s": round(nd_ / t_ddec),
+            "decimal_dev_to_host_strings_per_s": round(nd_ / t_e2e),
+            "decimal_dev_roundtrip_ok": bool(torch.equal(dback, c[:nd_])),
+            "decimal_dev_matches_host": bool(ct_to_decimal(c[:256].cpu().numpy().view(np.uint32)) == [
+                bytes(hb_[int(ho_[i]):int(ho_[i + 1])].numpy()).decode() for i in range(256)])})
+        del ch, strs, back, fr, g_, dbuf, doffs, dback, hb_, ho_
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_sample, a.cpu_threads)

@@ -74,6 +74,8 @@ _PROTOS = {
     "fthe_decimal_max_len": (_SZ, [_I]),
     "fthe_ct_to_decimal": (_I, [_P, _I, _SZ, _P, _SZ, _P, _I]),
     "fthe_ct_from_decimal": (_I, [_P, _P, _SZ, _I, _P, _I]),
+    "fthe_ct_to_decimal_dev": (_I, [_P, _P, _I, _SZ, _P, _SZ, _P]),
+    "fthe_ct_from_decimal_dev": (_I, [_P, _P, _P, _SZ, _I, _P]),
     "fthe_wire_size": (_SZ, [_SZ, _I, _I]),
     "fthe_wire_encode": (_I, [_P, _P, _SZ, _I, _P, _SZ, _P]),
     "fthe_wire_decode": (_I, [_P, _SZ, _I, _P, _P, _SZ, _P]),

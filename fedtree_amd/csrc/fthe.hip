@@ -130,6 +130,7 @@ struct fthe_ctx {
     hipFunction_t fn[MAX_VARIANTS] = {};
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
     DevBuf hb[6];                           // histogram CSR / segmented-product plan (device)
+    DevBuf dec[3];                          // decimal codec: 9-digit chunks, lengths, leading chunk / error flag
     void *cub_tmp = nullptr; size_t cub_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_mm = 0;
@@ -2237,6 +2238,56 @@ extern "C" int fthe_scalar_mul_u64(fthe_key *k, fthe_ctx *c, const uint32_t *x, 
 
 // ---------------------------------------------------------------------------
 // Codec
+// ---------------------------------------------------------------------------
+// Decimal wire strings on the device (fthe_dec.hip): the bytes of fthe_ct_to_decimal
+// (mpz_get_str, the reference's GHEncBatch text) without the host round trip.
+extern "C" int fthe_ct_to_decimal_dev(fthe_ctx *c, const uint32_t *ct, int words, size_t count, char *buf,
+                                      size_t buf_len, size_t *offsets) {
+    if (!c || (!ct && count) || words <= 0 || words > 128 || !offsets) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    const int nch = (int)((fthe_decimal_max_len(words) + 8) / 9);
+    int rc;
+    if ((rc = c->dec[0].ensure(std::max<size_t>(4, (size_t)nch * count * 4))) ||
+        (rc = c->dec[1].ensure((count + 1) * 8)) || (rc = c->dec[2].ensure(std::max<size_t>(4, count * 4))))
+        return rc;
+    hipStream_t st = c->stream;
+    HIPOK(hipEventRecord(c->ev0, st));
+    uint32_t *chunks = (uint32_t *)c->dec[0].p;
+    int64_t *len = (int64_t *)c->dec[1].p, *off = (int64_t *)offsets;
+    int32_t *top = (int32_t *)c->dec[2].p;
+    if (count && dec_launch_chunks(ct, words, count, nch, chunks, st)) return FTHE_ERR_UNSUPPORTED;
+    dec_launch_len_write(chunks, count, nch, len, top, 0, nullptr, nullptr, st);
+    if ((rc = exclusive_scan_i64(len, off, count + 1, c->cub_tmp, c->cub_bytes, st))) return FTHE_ERR_HIP;
+    int64_t total = 0;
+    HIPOK(hipMemcpyAsync(&total, off + count, 8, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    if ((size_t)total > buf_len || (!buf && total)) return FTHE_ERR_ARG;   // offsets[count]: bytes needed
+    if (count) dec_launch_len_write(chunks, count, nch, len, top, 1, off, buf, st);
+    HIPOK(hipEventRecord(c->ev1, st));
+    c->timed = true;
+    return hipGetLastError() == hipSuccess ? FTHE_OK : FTHE_ERR_HIP;
+}
+
+extern "C" int fthe_ct_from_decimal_dev(fthe_ctx *c, const char *buf, const size_t *offsets, size_t count, int words,
+                                        uint32_t *ct) {
+    if (!c || (!buf && count) || !offsets || words <= 0 || words > 128 || (!ct && count)) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    int rc;
+    if ((rc = c->dec[2].ensure(4))) return rc;
+    hipStream_t st = c->stream;
+    int *err = (int *)c->dec[2].p;
+    HIPOK(hipEventRecord(c->ev0, st));
+    HIPOK(hipMemsetAsync(err, 0, 4, st));
+    if (count && dec_launch_parse(buf, (const int64_t *)offsets, count, words, (int)fthe_decimal_max_len(words), ct,
+                                  err, st)) return FTHE_ERR_UNSUPPORTED;
+    HIPOK(hipEventRecord(c->ev1, st));
+    c->timed = true;
+    int h = 0;
+    HIPOK(hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    return h ? FTHE_ERR_ARG : FTHE_OK;
+}
+
 extern "C" int fthe_encode_fixed_dev(fthe_ctx *c, const float *x, size_t count, uint64_t *m) {
     if (!c) return FTHE_ERR_ARG;
     if (!count) return FTHE_OK;

@@ -39,6 +39,12 @@ __global__ void k_plan_groups(const int64_t *seg, const int64_t *members, size_t
                               int K, int64_t *gidx);
 __global__ void k_u64_to_i64(const unsigned long long *a, int64_t *b, size_t n);
 int exclusive_scan_i64(const int64_t *in, int64_t *out, size_t n, void *&tmp, size_t &tmp_bytes, hipStream_t st);
+// fthe_dec.hip: decimal wire strings on the device
+int dec_launch_chunks(const uint32_t *ct, int words, size_t count, int nch, uint32_t *chunks, hipStream_t st);
+int dec_launch_len_write(const uint32_t *chunks, size_t count, int nch, int64_t *len, int32_t *top, int pass,
+                         const int64_t *off, char *buf, hipStream_t st);
+int dec_launch_parse(const char *buf, const int64_t *off, size_t count, int words, int maxlen, uint32_t *ct, int *err,
+                     hipStream_t st);
 __global__ void k_encode_fixed(const float *x, size_t count, uint64_t *m);
 __global__ void k_decode_fixed(const uint64_t *m, size_t count, float *x);
 }  // namespace fthe

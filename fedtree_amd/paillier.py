@@ -633,6 +633,31 @@ def ct_from_decimal(strings, words, threads=0):
     return out
 
 
+def ct_to_decimal_dev(dev, ct):
+    """Device ciphertext rows (torch int32/uint32, (count, words)) -> (buf, offsets): the
+    strings of ct_to_decimal concatenated in a device uint8 tensor and count+1 int64
+    device offsets, computed on the GPU (fthe_ct_to_decimal_dev)."""
+    import torch
+    cnt, words = ct.shape
+    buf = torch.empty(max(1, cnt * dev.lib.fthe_decimal_max_len(words)), dtype=torch.uint8, device=ct.device)
+    offs = torch.empty(cnt + 1, dtype=torch.int64, device=ct.device)
+    _lib.check(dev.lib.fthe_ct_to_decimal_dev(dev.ctx, ctypes.c_void_p(ct.data_ptr()), words, cnt,
+                                              ctypes.c_void_p(buf.data_ptr()), buf.numel(),
+                                              ctypes.c_void_p(offs.data_ptr())), "to_decimal_dev")
+    return buf, offs
+
+
+def ct_from_decimal_dev(dev, buf, offs, words):
+    """(buf, offsets) device tensors of decimal strings -> (count, words) int32 device rows."""
+    import torch
+    cnt = offs.numel() - 1
+    out = torch.empty((cnt, words), dtype=torch.int32, device=buf.device)
+    _lib.check(dev.lib.fthe_ct_from_decimal_dev(dev.ctx, ctypes.c_void_p(buf.data_ptr()),
+                                                ctypes.c_void_p(offs.data_ptr()), cnt, words,
+                                                ctypes.c_void_p(out.data_ptr())), "from_decimal_dev")
+    return out
+
+
 def wire_encode(g, h=None):
     """Binary "FTHW" frame of raw little-endian words."""
     lib = _lib.load()

@@ -257,6 +257,15 @@ int fthe_ct_to_decimal(const uint32_t *ct, int words, size_t count, char *buf, s
                        size_t *offsets, int threads);
 int fthe_ct_from_decimal(const char *buf, const size_t *offsets, size_t count, int words,
                          uint32_t *ct, int threads);
+/* The same decimal strings computed on the GPU (fthe_dec.hip): ct, buf and offsets
+ * (count+1 entries, size_t) in device memory, words <= 128.  to: offsets[count] =
+ * bytes; buf_len too small -> FTHE_ERR_ARG with the offsets filled (size needed in
+ * offsets[count]).  from: FTHE_ERR_ARG on an empty, non-decimal or oversized string.
+ * Both synchronise the context stream once (the size / error flag). */
+int fthe_ct_to_decimal_dev(fthe_ctx *ctx, const uint32_t *ct, int words, size_t count, char *buf,
+                           size_t buf_len, size_t *offsets);
+int fthe_ct_from_decimal_dev(fthe_ctx *ctx, const char *buf, const size_t *offsets, size_t count,
+                             int words, uint32_t *ct);
 size_t fthe_wire_size(size_t count, int words, int with_h);
 int fthe_wire_encode(const uint32_t *g, const uint32_t *h, size_t count, int words,
                      uint8_t *out, size_t cap, size_t *len);
