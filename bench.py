@@ -201,6 +201,13 @@ def main():
         pmc = json.load(open(prof_hbm))
         roof["traffic"] = pmc.get("enc", {}).get("fthe_montprog_s74", {}).get("hbm_bytes_per_launch")
         roof["traffic_source"] = f"profiles/{PMC_FILE} (s74 full-chunk launch)"
+    # what the traffic is: SURVEY 8(d) algorithmic bytes (772 B per encrypt, half per prime launch) vs the
+    # operand reads of the one-lane design (each window multiplication reads a 296-B table entry per lane)
+    lanes = 393216
+    roof["algorithmic_bytes_per_launch"] = lanes * 772 // 2
+    roof["window_operand_bytes_per_launch_model"] = int(lanes * (190 + 16 + 4) * 296)
+    roof["traffic_note"] = ("HBM bytes are the per-lane window-table operand reads (~190 multiplications x 296 B "
+                            "per lane per exponentiation), 2.2% of HBM bandwidth in a VALU-bound kernel")
 
     secondary = {}
     if rank == 0 and not a.no_secondary:
