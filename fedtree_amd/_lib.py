@@ -22,6 +22,7 @@ FTHE_ENC_DEFAULT = 0
 FTHE_ENC_PUBLIC = 1
 FTHE_ENC_FIXED_BASE = 2
 FTHE_ENC_FIXED_BASE_EXACT = 4
+FTHE_KEYGEN_KNOWN_ORDER = 1
 
 
 class FtheError(RuntimeError):
@@ -48,6 +49,7 @@ _PROTOS = {
     "fthe_ctx_stream": (_P, [_P]),
     "fthe_ctx_device": (_I, [_P]),
     "fthe_key_generate": (_I, [_P, _I, _U64, _PP]),
+    "fthe_key_generate_ex": (_I, [_P, _I, _U64, _I, _PP]),
     "fthe_key_from_primes": (_I, [_P, _P, _P, _I, _PP]),
     "fthe_key_from_n": (_I, [_P, _P, _I, _PP]),
     "fthe_key_destroy": (None, [_P]),
@@ -59,6 +61,7 @@ _PROTOS = {
     "fthe_key_fixed_base_info": (_I, [_P, _P, _P, _P]),
     "fthe_key_fixed_base_exact": (_I, [_P, _P, _U64]),
     "fthe_key_fixed_base_exact_info": (_I, [_P, _I, _I, _P, _P]),
+    "fthe_key_fixed_base_exact_bases": (_I, [_P]),
     "fthe_encrypt_u64_dev": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_encrypt_u64": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_decrypt_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),

@@ -243,12 +243,16 @@ struct fthe_key {
     // for exponents y_i < P; r^n mod P^2 is drawn as prod_i gam[i]^y_i.
     struct ExactBase {
         bool ready = false;
+        int nb = 3;                       // bases per prime: 1 when P - 1 is factored (a generator), else 3
         int nwin = 0, ew = 0;             // 16-bit windows per exponent, words per entry
         Mpz gam[2][3];
         uint32_t *d_tab[2] = {nullptr, nullptr}, *d_prog = nullptr;
         size_t off[2] = {0, 0};
         double mm = 0;
     } xb;
+    // prime factors of p - 1 and q - 1 when the key generator recorded them (FTHE_KEYGEN_KNOWN_ORDER)
+    bool order_known = false;
+    std::vector<Mpz> pm1_factors, qm1_factors;
 };
 
 // slot numbering shared by all programs
@@ -654,6 +658,86 @@ extern "C" int fthe_key_from_primes(fthe_ctx *ctx, const uint32_t *p, const uint
     if (!ctx || !p || !q || w <= 0 || !out) return FTHE_ERR_ARG;
     Mpz P, Q; mpz_from_words(P, p, w); mpz_from_words(Q, q, w);
     return key_from_pq(ctx, P, Q, out);
+}
+
+// A prime P of hb bits (top two bits set) with P - 1 = 2 s P' fully factored: P' a random
+// prime of hb - 42 bits, s a product of random primes below 2^16; P found by trying s.
+// Returns the distinct prime factors of P - 1 in `factors`.
+static void known_order_prime(gmp_randstate_t st, int hb, Mpz &P, std::vector<Mpz> &factors) {
+    static const std::vector<uint32_t> sp = [] {
+        std::vector<uint32_t> v;
+        for (uint32_t i = 3; i < 65536; i += 2) {
+            bool pr = true;
+            for (uint32_t d = 3; d * d <= i; d += 2) if (i % d == 0) { pr = false; break; }
+            if (pr) v.push_back(i);
+        }
+        return v;
+    }();
+    Mpz Pp, lo, hi, s, t, r;
+    for (;;) {
+        mpz_urandomb(Pp, st, hb - 42); mpz_setbit(Pp, hb - 43); mpz_nextprime(Pp, Pp);
+        // 2 s P' + 1 in [3 * 2^(hb-2), 2^hb): s in [lo, hi)
+        mpz_set_ui(t, 3); mpz_mul_2exp(t, t, hb - 2); mpz_fdiv_q(lo, t, Pp); mpz_fdiv_q_2exp(lo, lo, 1);
+        mpz_set_ui(t, 1); mpz_mul_2exp(t, t, hb); mpz_fdiv_q(hi, t, Pp); mpz_fdiv_q_2exp(hi, hi, 1);
+        for (int tries = 0; tries < 20000; tries++) {
+            std::vector<uint32_t> used;
+            mpz_set_ui(s, 1);
+            for (;;) {                                    // random small primes while s * 2^16 < lo
+                mpz_mul_2exp(t, s, 16);
+                if (mpz_cmp(t, lo) >= 0) break;
+                mpz_urandomm(r, st, Mpz((unsigned long)sp.size()));
+                used.push_back(sp[mpz_get_ui(r)]);
+                mpz_mul_ui(s, s, used.back());
+            }
+            // the last factor: a random small prime in [ceil(lo / s), ceil(hi / s))
+            mpz_cdiv_q(t, lo, s);
+            const unsigned long a = mpz_get_ui(t);
+            mpz_cdiv_q(t, hi, s);
+            const unsigned long b = std::min(mpz_get_ui(t), 65536ul);
+            auto ia = std::lower_bound(sp.begin(), sp.end(), (uint32_t)a), ib = std::lower_bound(sp.begin(), sp.end(), (uint32_t)b);
+            if (ia >= ib) continue;
+            mpz_urandomm(r, st, Mpz((unsigned long)(ib - ia)));
+            used.push_back(*(ia + mpz_get_ui(r)));
+            mpz_mul_ui(s, s, used.back());
+            mpz_mul(P, s, Pp); mpz_mul_2exp(P, P, 1); mpz_add_ui(P, P, 1);
+            if (mpz_probab_prime_p(P, 30) == 0) continue;
+            factors.clear();
+            factors.emplace_back(2ul);
+            std::sort(used.begin(), used.end());
+            used.erase(std::unique(used.begin(), used.end()), used.end());
+            for (uint32_t l : used) factors.emplace_back((unsigned long)l);
+            factors.push_back(Pp);
+            return;
+        }
+    }
+}
+
+extern "C" int fthe_key_generate_ex(fthe_ctx *ctx, int n_bits, uint64_t seed, int flags, fthe_key **out) {
+    if (!(flags & FTHE_KEYGEN_KNOWN_ORDER)) return fthe_key_generate(ctx, n_bits, seed, out);
+    if (!ctx || !out || n_bits < 128 || (n_bits & 1)) return FTHE_ERR_ARG;
+    gmp_randstate_t st; gmp_randinit_mt(st);
+    uint64_t s = seed ? seed : urandom64();
+    Mpz sd; mpz_set_ui(sd, (unsigned long)splitmix64(s));
+    mpz_mul_2exp(sd, sd, 64); mpz_add_ui(sd, sd, (unsigned long)splitmix64(s) ^ 0x6b6e6f776e6f7264ull);
+    gmp_randseed(st, sd);
+    const int hb = n_bits / 2;
+    int rc = FTHE_ERR_KEY;
+    for (int tries = 0; tries < 64 && rc == FTHE_ERR_KEY; tries++) {
+        Mpz p, q;
+        std::vector<Mpz> fp, fq;
+        known_order_prime(st, hb, p, fp);
+        known_order_prime(st, hb, q, fq);
+        Mpz nn; mpz_mul(nn, p, q);
+        if (mpz_cmp(p, q) == 0 || nn.bits() != (size_t)n_bits) continue;
+        rc = key_from_pq(ctx, p, q, out);
+        if (rc == FTHE_OK) {
+            (*out)->order_known = true;
+            (*out)->pm1_factors = fp;
+            (*out)->qm1_factors = fq;
+        }
+    }
+    gmp_randclear(st);
+    return rc;
 }
 
 extern "C" int fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out) {
@@ -1438,6 +1522,24 @@ void xb_pick_bases(gmp_randstate_t st, const mpz_t P, Mpz t[3]) {
     }
 }
 
+// P - 1 fully factored (factors = its distinct primes): a primitive root t mod P, so gam = t^P
+// generates G_P by itself and one base with a uniform exponent is exactly uniform over G_P
+void xb_pick_generator(gmp_randstate_t st, const mpz_t P, const std::vector<Mpz> &factors, Mpz &t) {
+    Mpz Pm1, e, x, span;
+    mpz_sub_ui(Pm1, P, 1);
+    mpz_sub_ui(span, P, 3);
+    for (;;) {
+        mpz_urandomm(t, st, span); mpz_add_ui(t, t, 2);
+        bool gen = true;
+        for (const Mpz &l : factors) {
+            mpz_divexact(e, Pm1, l);
+            mpz_powm(x, t, e, P);
+            if (mpz_cmp_ui(x, 1) == 0) { gen = false; break; }
+        }
+        if (gen) return;
+    }
+}
+
 int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
     fthe_key::ExactBase &X = k->xb;
     if (!k->priv) return FTHE_ERR_NOPRIV;
@@ -1455,27 +1557,29 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
     gmp_randseed(st, sd);
     X.nwin = (int)((std::max(k->p.bits(), k->q.bits()) + 15) / 16);
     X.ew = 4 * ((k->spq.S + 3) / 4);
+    X.nb = k->order_known ? 1 : 3;
     std::vector<uint32_t> progs;
     int rc = FTHE_OK;
     for (int side = 0; side < 2 && rc == FTHE_OK; side++) {
         const Mpz &P = side ? k->q : k->p;
         const DevMod &D = side ? k->mq2 : k->mp2;
         Mpz t[3];
-        xb_pick_bases(st, P, t);
+        if (k->order_known) xb_pick_generator(st, P, side ? k->qm1_factors : k->pm1_factors, t[0]);
+        else xb_pick_bases(st, P, t);
         std::vector<uint32_t> tab;                        // 8-bit windows, base after base
-        for (int b = 0; b < 3; b++) {
+        for (int b = 0; b < X.nb; b++) {
             mpz_powm(X.gam[side][b], t[b], P, D.m.N);
             std::vector<uint32_t> tb = fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, fb_store_limbs(D.m));
             tab.insert(tab.end(), tb.begin(), tb.end());
         }
         uint32_t *d8 = nullptr;
         if ((rc = fb_upload(tab, &d8))) break;
-        rc = fb_widen(k, c, D, k->spq, d8, 3 * X.nwin, X.ew, false, &X.d_tab[side]);
+        rc = fb_widen(k, c, D, k->spq, d8, X.nb * X.nwin, X.ew, false, &X.d_tab[side]);
         hipFree(d8);
         if (rc) break;
         Prog e;                                           // X = prod_j entry(j, digit j), then (1 + m n) X
         e.loadgd16(0);
-        for (int j = 1; j < 3 * X.nwin; j++) e.mulgd16(j);
+        for (int j = 1; j < X.nb * X.nwin; j++) e.mulgd16(j);
         e.storex(SL_SAVED);
         e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
         e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
@@ -1505,12 +1609,18 @@ extern "C" int fthe_key_fixed_base_exact(fthe_key *k, fthe_ctx *c, uint64_t seed
 }
 
 extern "C" int fthe_key_fixed_base_exact_info(fthe_key *k, int side, int base, uint32_t *gamma, int *exp_words) {
-    if (!k || side < 0 || side > 1 || base < 0 || base > 2) return FTHE_ERR_ARG;
+    if (!k || side < 0 || side > 1 || base < 0) return FTHE_ERR_ARG;
     std::lock_guard<std::mutex> g(k->fb_mu);
-    if (!k->xb.ready) return FTHE_ERR_ARG;
+    if (!k->xb.ready || base >= k->xb.nb) return FTHE_ERR_ARG;
     if (gamma) mpz_to_words(k->xb.gam[side][base], gamma, 2 * k->pq_w);
     if (exp_words) *exp_words = k->pq_w;
     return FTHE_OK;
+}
+
+extern "C" int fthe_key_fixed_base_exact_bases(fthe_key *k) {
+    if (!k) return 0;
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    return k->xb.ready ? k->xb.nb : 0;
 }
 
 static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *y,
@@ -1519,11 +1629,12 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
     if (rc) return rc;
     const fthe_key::ExactBase &X = k->xb;
     const int pw = k->pq_w;
-    if (y && y_words != 6 * pw) return FTHE_ERR_ARG;         // y_{p,1..3}, y_{q,1..3}, pq_w words each
+    const int nb = X.nb;
+    if (y && y_words != 2 * nb * pw) return FTHE_ERR_ARG;    // y_{p,1..nb}, y_{q,1..nb}, pq_w words each
     Launch Lc;
     if ((rc = begin_call(c, k, count, Lc, nslots_for(k), k->spq))) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
-    const size_t dig_bytes = (size_t)3 * X.nwin * L * 2;    // per side: 3 exponents x nwin u16 digit rows
+    const size_t dig_bytes = (size_t)nb * X.nwin * L * 2;   // per side: nb exponents x nwin u16 digit rows
     if ((rc = c->scratch.ensure(2 * dig_bytes + (size_t)L * pw * 4))) return rc;
     uint8_t *dig[2] = {(uint8_t *)c->scratch.p, (uint8_t *)c->scratch.p + dig_bytes};
     uint32_t *ytmp = (uint32_t *)((uint8_t *)c->scratch.p + 2 * dig_bytes);
@@ -1541,11 +1652,12 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
         Lc.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         for (int side = 0; side < 2; side++)
-            for (int b = 0; b < 3; b++) {
+            for (int b = 0; b < nb; b++) {
                 uint8_t *dst = dig[side] + b * exp_bytes;
                 if (y) {
                     hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream,
-                                       y + off * y_words + (size_t)(3 * side + b) * pw, y_words, pw, cnt, X.nwin, L, 2, dst);
+                                       y + off * y_words + (size_t)(nb * side + b) * pw, y_words, pw, cnt, X.nwin, L, 2,
+                                       dst);
                 } else {
                     RngKey kb = rk;
                     kb.nonce += (uint64_t)(3 * side + b + 1) << 56;           // one stream per (prime, base)

@@ -135,10 +135,14 @@ class Paillier:
         self.n2 = self.modulus * self.modulus
         return self
 
-    def keygen(self, keyLength, seed=0):
-        """Paillier::keygen(int keyLength) (paillier.cpp:66-90)."""
+    def keygen(self, keyLength, seed=0, known_order=False):
+        """Paillier::keygen(int keyLength) (paillier.cpp:66-90).  known_order: primes with a
+        factored P - 1 (FTHE_KEYGEN_KNOWN_ORDER: one generator per prime in the exact
+        fixed-base mode; not the reference's prime distribution)."""
         key = ctypes.c_void_p()
-        _lib.check(self.lib.fthe_key_generate(self.dev.ctx, int(keyLength), int(seed), ctypes.byref(key)), "keygen")
+        flags = _lib.FTHE_KEYGEN_KNOWN_ORDER if known_order else 0
+        _lib.check(self.lib.fthe_key_generate_ex(self.dev.ctx, int(keyLength), int(seed), flags, ctypes.byref(key)),
+                   "keygen")
         return self._adopt(key)
 
     @classmethod
@@ -204,11 +208,13 @@ class Paillier:
         _lib.check(self.lib.fthe_key_fixed_base_exact(self._key, self.dev.ctx, int(seed)), "key_fixed_base_exact")
 
     def fixed_base_exact_info(self):
-        """([[gam_p1, gam_p2, gam_p3], [gam_q1, gam_q2, gam_q3]], words per exponent)."""
+        """([[gam_p1, ...], [gam_q1, ...]], words per exponent): 3 bases per prime, or 1 (a
+        generator) for known-order keys."""
         gam, ew = [[], []], ctypes.c_int()
         buf = np.zeros(self.n_words, dtype=np.uint32)
+        nb = self.lib.fthe_key_fixed_base_exact_bases(self._key)
         for side in (0, 1):
-            for b in range(3):
+            for b in range(nb):
                 _lib.check(self.lib.fthe_key_fixed_base_exact_info(self._key, side, b, _ptr(buf), ctypes.byref(ew)),
                            "key_fixed_base_exact_info")
                 gam[side].append(int.from_bytes(buf.tobytes(), "little"))
@@ -221,14 +227,15 @@ class Paillier:
         fixed_base: r = h^alpha from the key's fixed-base tables (include/fthe.h);
            r then injects alpha (ints or (count, words) uint32) instead of r.
         fixed_base_exact: r^n mod p^2, q^2 from the exact generator tables (key holder);
-           r then injects the six exponents (count, 6 * n_words/2) uint32 or 6-tuples of ints."""
+           r then injects the 2 * bases exponents per ciphertext ((count, 2 * bases * n_words/2)
+           uint32 or tuples of ints; bases from fixed_base_exact_info)."""
         m = np.ascontiguousarray(m, dtype=np.uint64).reshape(-1)
         cnt = len(m)
         out = np.zeros((cnt, self._cw()), dtype=np.uint32)
         rw = None
         if r is not None:
             if not isinstance(r, np.ndarray) and fixed_base_exact:
-                hw = self.n_words // 2
+                hw = self.n_words // 2             # tuples of 2 * bases exponents (fixed_base_exact_info)
                 r = np.stack([np.concatenate([_words(int(x), hw) for x in t]) for t in r]) if cnt \
                     else np.zeros((0, 6 * hw), np.uint32)
             if not isinstance(r, np.ndarray):

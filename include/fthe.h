@@ -72,6 +72,16 @@ int   fthe_ctx_device(fthe_ctx *ctx);
  *                        (copies modulus/generator/keyLength only).
  */
 int  fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out);
+/* fthe_key_generate_ex   flags 0: fthe_key_generate.  FTHE_KEYGEN_KNOWN_ORDER: p and q
+ *                        (top two bits set, n of n_bits bits) of the form 2 s P' + 1 with
+ *                        P' a random prime and s a product of random primes < 2^16, the
+ *                        factorisation of p - 1, q - 1 kept with the key, so that the exact
+ *                        fixed-base mode uses one generator per prime (64 instead of 192
+ *                        gathered products at P-2048) and is exact without a probability
+ *                        bound.  Not the reference's prime distribution (paillier.cpp:43-62
+ *                        draws unconstrained random primes); opt-in. */
+#define FTHE_KEYGEN_KNOWN_ORDER 1
+int  fthe_key_generate_ex(fthe_ctx *ctx, int n_bits, uint64_t seed, int flags, fthe_key **out);
 int  fthe_key_from_primes(fthe_ctx *ctx, const uint32_t *p, const uint32_t *q,
                           int pq_words, fthe_key **out);
 int  fthe_key_from_n(fthe_ctx *ctx, const uint32_t *n, int n_words, fthe_key **out);
@@ -131,8 +141,9 @@ int fthe_key_fixed_base_info(fthe_key *key, int *alpha_bits_public, int *alpha_b
  * 3 * ceil(bits(P)/16) gathered products from 16-bit-window tables (~3.8 GB
  * per prime at P-2048) instead of ~1.2 bits(P) squarings and products.
  * Injected exponents (parity): r = y, r_words = 6 * (n_words / 2): per
- * ciphertext y_{p,1}, y_{p,2}, y_{p,3}, y_{q,1}, y_{q,2}, y_{q,3}, n_words/2
- * little-endian words each, each y < 2^(16 * ceil(bits(P)/16)).
+ * ciphertext y_{p,1}, y_{p,2}, y_{q,1}, ... (see fthe_key_fixed_base_exact_bases;
+ * 3 bases, or 1 for FTHE_KEYGEN_KNOWN_ORDER keys), n_words/2 little-endian words
+ * each, each y < 2^(16 * ceil(bits(P)/16)).
  * fthe_key_fixed_base_exact       (re)build bases and tables; seed 0 draws the
  *                                 bases from /dev/urandom, else deterministic.
  *                                 Built on first use otherwise.  Not concurrent
@@ -141,6 +152,10 @@ int fthe_key_fixed_base_info(fthe_key *key, int *alpha_bits_public, int *alpha_b
  *                                 words, nullable) and the words per exponent. */
 int fthe_key_fixed_base_exact(fthe_key *key, fthe_ctx *ctx, uint64_t seed);
 int fthe_key_fixed_base_exact_info(fthe_key *key, int side, int base, uint32_t *gamma, int *exp_words);
+/* bases per prime of the built exact tables: 3, or 1 for FTHE_KEYGEN_KNOWN_ORDER keys
+ * (one generator); 0 before a build.  Injected exponents then take 2 * bases * (n_words/2)
+ * words per ciphertext (y_{p,1..bases}, y_{q,1..bases}). */
+int fthe_key_fixed_base_exact_bases(fthe_key *key);
 
 /* ---- decrypt: m = L(c^lambda mod n^2) * mu mod n (paillier.cpp:153-156) ---
  * Computed with CRT over p^2, q^2 (identical canonical result).

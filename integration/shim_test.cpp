@@ -9,10 +9,11 @@
 int main(int argc, char **argv) {
     int bits = argc > 1 ? std::atoi(argv[1]) : 1024;
     Paillier_HIP server;                 // Server::paillier
+    if (argc > 2 && std::string(argv[2]) == "exact_known_order") server.keygen_flags = FTHE_KEYGEN_KNOWN_ORDER;
     server.keygen(bits);                 // homo_init (NTL semantics: n of `bits` bits)
     Paillier_HIP party;                  // Party::paillier
     party = server;                      // Server::send_key: public part only
-    if (argc > 2 && std::string(argv[2]) == "exact")      // table-driven randomizer; the party (no p, q)
+    if (argc > 2 && std::string(argv[2]).rfind("exact", 0) == 0)   // table-driven randomizer; the party (no p, q)
         server.enc_flags = party.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;   // falls back to the default
     const float g[5] = {0.4f, 1.2f, 0.1f, 0.8f, -0.7f}, h[5] = {0.6f, 1.4f, 0.2f, 1.0f, 0.8f};
     SyncArray<GHPair> gh(5), hist(5);

@@ -55,8 +55,9 @@ def _check_bases(gam, P):
 
 def _crt_want(p, q, m, ys, gam):
     n = p * q
+    nb = len(gam[0])
     parts = []
-    for P, yy, gg in ((p, ys[:3], gam[0]), (q, ys[3:], gam[1])):
+    for P, yy, gg in ((p, ys[:nb], gam[0]), (q, ys[nb:], gam[1])):
         P2 = P * P
         v = (1 + int(m) * n) % P2
         for y, g in zip(yy, gg):
@@ -87,6 +88,7 @@ def test_exact_injected_exponents(dev, name):
     ys[1] = (1,) * 6
     ys[2] = ((1 << ebits) - 1,) * 6
     ys[3] = (p - 1, 0, 0, q - 1, 0, 0)                      # gam^(P-1) = 1
+    assert len(gam[0]) == 3
     c = pl.encrypt_u64(m, r=ys, fixed_base_exact=True)
     want = [_crt_want(p, q, x, y, gam) for x, y in zip(m, ys)]
     assert pyoracle.words_to_ints(c) == want
@@ -188,3 +190,49 @@ def test_exact_needs_private_key(dev):
     with pytest.raises(RuntimeError):
         pub.set_fixed_base_exact(seed=1)
     assert _lib.FTHE_ENC_FIXED_BASE_EXACT == 4
+
+
+def _factor_small(x):
+    """x = prod(primes < 2^16)^e * rest; returns (distinct small primes, rest)."""
+    fs = []
+    for l in SMALL:
+        if x % l == 0:
+            fs.append(l)
+            while x % l == 0:
+                x //= l
+    return fs, x
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_known_order_keygen_single_generator(dev, coracle, bits):
+    """FTHE_KEYGEN_KNOWN_ORDER: P - 1 = 2 s P' with s smooth and P' prime, so the engine
+    picks one generator per prime; verified here at every prime factor of P - 1, with
+    injected exponents bit-exact and device-drawn round trips."""
+    from fedtree_amd.paillier import Paillier
+    pl = Paillier(dev).keygen(bits, seed=77, known_order=True)
+    p, q, n = pl.p, pl.q, pl.modulus
+    assert n.bit_length() == bits and p * q == n
+    assert pl.p >= 3 << (bits // 2 - 2) and pl.q >= 3 << (bits // 2 - 2)
+    pl.set_fixed_base_exact(seed=5)
+    gam, ew = pl.fixed_base_exact_info()
+    assert [len(g) for g in gam] == [1, 1]
+    for P, (g,) in ((p, gam[0]), (q, gam[1])):
+        fs, rest = _factor_small(P - 1)
+        assert 2 in fs and rest > 2**64 and pow(3, rest - 1, rest) == 1      # P' a large (probable) prime
+        for l in fs + [rest]:
+            assert pow(g % P, (P - 1) // l, P) != 1, l                       # a generator of Z_P^*
+        assert pow(g, P - 1, P * P) == 1                                       # in G_P
+    rng = np.random.default_rng(bits)
+    ebits = 16 * ((max(p.bit_length(), q.bit_length()) + 15) // 16)
+    m = rng.integers(0, 2**64, 16, dtype=np.uint64)
+    ys = [(int.from_bytes(rng.bytes(ebits // 8), "little"), int.from_bytes(rng.bytes(ebits // 8), "little"))
+          for _ in range(16)]
+    ys[0] = (0, 0)
+    c = pl.encrypt_u64(m, r=ys, fixed_base_exact=True)
+    assert pyoracle.words_to_ints(c) == [_crt_want(p, q, x, y, gam) for x, y in zip(m, ys)]
+    mm = rng.integers(0, 2**64, 100_000, dtype=np.uint64)
+    cc = pl.encrypt_u64(mm, seed=9, fixed_base_exact=True)
+    assert np.array_equal(pl.decrypt_u64(cc), mm)
+    ok = coracle.key(pyoracle.to_words(p, pl.n_words // 2), pyoracle.to_words(q, pl.n_words // 2))
+    dec = ok.decrypt_batch(cc[:16])
+    assert [pyoracle.from_words(d) for d in dec] == [int(x) for x in mm[:16]]

@@ -34,6 +34,23 @@ def main():
         pl.decrypt_u64_dev(c, low)
         dev.sync()
         out[name + "_roundtrip_ok"] = bool(torch.equal(low, m))
+    # one-generator exact mode: a key with factored P - 1 (FTHE_KEYGEN_KNOWN_ORDER)
+    t0 = time.perf_counter()
+    pk = Paillier(dev).keygen(2048, seed=20261016, known_order=True)
+    out["known_order_keygen_s"] = round(time.perf_counter() - t0, 3)
+    t0 = time.perf_counter()
+    pk.set_fixed_base_exact(seed=0)
+    dev.sync()
+    out["known_order_table_build_s"] = round(time.perf_counter() - t0, 3)
+    pk.encrypt_u64_dev(m[:4096], c[:4096], seed=1, fixed_base_exact=True)
+    dev.sync()
+    pk.encrypt_u64_dev(m, c, seed=2, fixed_base_exact=True)
+    dev.sync()
+    out["exact_known_order_per_s"] = round(n / (dev.last_kernel_ms() * 1e-3))
+    low = torch.empty_like(m)
+    pk.decrypt_u64_dev(c, low)
+    dev.sync()
+    out["exact_known_order_roundtrip_ok"] = bool(torch.equal(low, m))
     print(json.dumps(out), flush=True)
 
 
