@@ -14,6 +14,7 @@ little-endian word order of mpz_export(order=-1) (paillier_gpu.cu:7,18); batch
 calls also accept torch tensors resident on the device (the *_dev paths).
 """
 import ctypes
+import functools
 import threading
 
 import numpy as np
@@ -81,6 +82,26 @@ class Device:
     def sync(self):
         _lib.check(self.lib.fthe_ctx_sync(self.ctx), "sync")
 
+    # Stream order with torch: the engine runs on its own HIP stream, so a device-resident
+    # call first waits for the work torch has queued on its current stream (the producers of
+    # the inputs, e.g. a torch.zeros fill of the output), and torch's stream then waits for
+    # the engine, so consumers of the outputs see them -- no host synchronisation.
+    def _ext_stream(self):
+        import torch
+        st = getattr(self, "_ext", None)
+        if st is None:
+            st = self._ext = torch.cuda.ExternalStream(self.lib.fthe_ctx_stream(self.ctx),
+                                                       device=torch.device("cuda", self.device))
+        return st
+
+    def order_in(self):
+        import torch
+        self._ext_stream().wait_stream(torch.cuda.current_stream(self.device))
+
+    def order_out(self):
+        import torch
+        torch.cuda.current_stream(self.device).wait_stream(self._ext_stream())
+
     def last_kernel_ms(self):
         return self.lib.fthe_last_kernel_ms(self.ctx)
 
@@ -97,6 +118,18 @@ class Device:
             self.close()
         except Exception:
             pass
+
+
+def _stream_ordered(fn):
+    """Device-resident method: ordered after torch's queued work, torch ordered after it."""
+    @functools.wraps(fn)
+    def wrap(self, *a, **k):
+        self.dev.order_in()
+        try:
+            return fn(self, *a, **k)
+        finally:
+            self.dev.order_out()
+    return wrap
 
 
 class Paillier:
@@ -317,6 +350,7 @@ class Paillier:
         return out
 
     # ---- device-resident batch API (torch tensors on this device) -------------
+    @_stream_ordered
     def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
         flags = self._flags(public, fixed_base, fixed_base_exact)
         rp = ctypes.c_void_p(r.data_ptr()) if r is not None else None
@@ -326,6 +360,7 @@ class Paillier:
                    "encrypt_dev")
         return out
 
+    @_stream_ordered
     def decrypt_u64_dev(self, c, out_low, short=False):
         cnt = c.numel() // self._cw()
         fn = self.lib.fthe_decrypt_short_dev if short else self.lib.fthe_decrypt_dev
@@ -333,6 +368,7 @@ class Paillier:
                       ctypes.c_void_p(out_low.data_ptr()), None), "decrypt_dev")
         return out_low
 
+    @_stream_ordered
     def add_dev(self, a, b, out):
         cnt = a.numel() // self._cw()
         _lib.check(self.lib.fthe_add_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),
@@ -340,6 +376,7 @@ class Paillier:
                    "add_dev")
         return out
 
+    @_stream_ordered
     def sub_dev(self, a, b, out):
         cnt = a.numel() // self._cw()
         _lib.check(self.lib.fthe_sub_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),
@@ -347,18 +384,21 @@ class Paillier:
                    "sub_dev")
         return out
 
+    @_stream_ordered
     def scan_segments_dev(self, x, seg_ptr, out):
         seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
         _lib.check(self.lib.fthe_scan_segments_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), _ptr(seg),
                                                    len(seg) - 1, ctypes.c_void_p(out.data_ptr())), "scan_segments_dev")
         return out
 
+    @_stream_ordered
     def reduce_kway_dev(self, x, k, out):
         cnt = out.numel() // self._cw()
         _lib.check(self.lib.fthe_reduce_kway_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), int(k),
                                                  cnt, ctypes.c_void_p(out.data_ptr())), "reduce_kway_dev")
         return out
 
+    @_stream_ordered
     def reduce_segments_dev(self, x, seg_ptr, out, idx=None):
         """Device tensors x (count, 2nw) and out (nseg, 2nw); host seg_ptr / idx."""
         seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
@@ -369,6 +409,7 @@ class Paillier:
                                                      ctypes.c_void_p(out.data_ptr())), "reduce_segments_dev")
         return out
 
+    @_stream_ordered
     def reduce_segments_csr_dev(self, x, seg_ptr, out, idx=None):
         """Segmented product with the CSR (int64 seg_ptr, optional int64 idx) on the device."""
         cnt = x.numel() // self._cw()
@@ -378,6 +419,7 @@ class Paillier:
             ctypes.c_void_p(out.data_ptr())), "reduce_segments_csr_dev")
         return out
 
+    @_stream_ordered
     def histogram_dev(self, x, count, planes, bin_ids, cut_col_ptr, max_num_bin, out, inst=None):
         """Node histogram on the device (hist_tree_builder.cpp:565-595, :640-664).
         x: device (planes*count, 2nw) ciphertexts (g plane, h plane); bin_ids: device
@@ -641,6 +683,14 @@ def ct_from_decimal(strings, words, threads=0):
 
 
 def ct_to_decimal_dev(dev, ct):
+    dev.order_in()
+    try:
+        return _ct_to_decimal_dev(dev, ct)
+    finally:
+        dev.order_out()
+
+
+def _ct_to_decimal_dev(dev, ct):
     """Device ciphertext rows (torch int32/uint32, (count, words)) -> (buf, offsets): the
     strings of ct_to_decimal concatenated in a device uint8 tensor and count+1 int64
     device offsets, computed on the GPU (fthe_ct_to_decimal_dev)."""
@@ -655,6 +705,14 @@ def ct_to_decimal_dev(dev, ct):
 
 
 def ct_from_decimal_dev(dev, buf, offs, words):
+    dev.order_in()
+    try:
+        return _ct_from_decimal_dev(dev, buf, offs, words)
+    finally:
+        dev.order_out()
+
+
+def _ct_from_decimal_dev(dev, buf, offs, words):
     """(buf, offsets) device tensors of decimal strings -> (count, words) int32 device rows."""
     import torch
     cnt = offs.numel() - 1

@@ -67,6 +67,7 @@ def test_config2_p2048_10M_pairs_roundtrip(dev, coracle):
     gh = np.concatenate([g, h])
     x = torch.from_numpy(gh).to("cuda:0")
     m = torch.empty(2 * pairs, dtype=torch.int64, device="cuda:0")
+    dev.order_in()                   # direct C-ABI call: after torch's copy of x
     _lib.check(dev.lib.fthe_encode_fixed_dev(dev.ctx, ctypes.c_void_p(x.data_ptr()), 2 * pairs,
                                              ctypes.c_void_p(m.data_ptr())), "encode")
     dev.sync()

@@ -224,6 +224,7 @@ def test_device_codec_and_dev_api(dev, coracle):
     lib = dev.lib
     tf = torch.from_numpy(f).cuda()
     tm = torch.zeros(len(f), dtype=torch.int64, device="cuda")
+    dev.order_in()                   # direct C-ABI calls: order after torch's fills and copies
     _lib.check(lib.fthe_encode_fixed_dev(dev.ctx, ctypes.c_void_p(tf.data_ptr()), len(f),
                                          ctypes.c_void_p(tm.data_ptr())))
     dev.sync()
@@ -233,6 +234,7 @@ def test_device_codec_and_dev_api(dev, coracle):
     allin = np.concatenate([din, m])
     tin = torch.from_numpy(allin.view(np.int64)).cuda()
     tout = torch.zeros(len(allin), dtype=torch.float32, device="cuda")
+    dev.order_in()
     _lib.check(lib.fthe_decode_fixed_dev(dev.ctx, ctypes.c_void_p(tin.data_ptr()), len(allin),
                                          ctypes.c_void_p(tout.data_ptr())))
     dev.sync()

@@ -84,6 +84,7 @@ def test_decimal_dev_errors(dev):
     buf = torch.empty(10, dtype=torch.uint8, device="cuda:0")
     offs = torch.empty(4, dtype=torch.int64, device="cuda:0")
     import ctypes
+    dev.order_in()                   # direct C-ABI call: after torch's fill of ct
     rc = dev.lib.fthe_ct_to_decimal_dev(dev.ctx, ctypes.c_void_p(ct.data_ptr()), words, 3,
                                         ctypes.c_void_p(buf.data_ptr()), 10, ctypes.c_void_p(offs.data_ptr()))
     assert rc == _lib.FTHE_ERR_ARG and int(offs[-1]) == 3 * len(str(2**128 - 1))

@@ -132,14 +132,17 @@ def pmc_round(tag, out):
                 d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
             wr[kn] = d
         res[w] = wr
-    # launch durations of the s152 row-I/O kernels (ops trace: add launches first, then kway)
+    # launch durations of the s152 row-I/O kernels (ops trace: add launches first, then as many
+    # kway launches); full launches = within 10% of the longest of their op
     tr = glob.glob(f"gpurun_out/{tag}_ops_trace/*kernel_trace.csv")
     if tr:
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
                 for r in csv.DictReader(open(tr[0])) if r["Kernel_Name"] == "fthe_montprog_s152"]
-        # prof_ops --n 1048576 --ops add,kway: 11 add chunks (98,304 rows) then 11 kway chunks
-        add, kway = durs[:10], durs[11:21]
-        for w, ds, units in (("add", add, 98304), ("kway", kway, 98304)):
+        h = len(durs) // 2
+        full = lambda ds: [d for d in ds if d >= 0.9 * max(ds)] if ds else []
+        add, kway = full(durs[:h]), full(durs[h:])
+        rows = int(os.environ.get("FTHE_ROWIO_ROWS", "393216"))    # rows per full row-I/O launch
+        for w, ds, units in (("add", add, rows), ("kway", kway, rows)):
             if ds and "fthe_montprog_s152" in res[w]:
                 k = res[w]["fthe_montprog_s152"]
                 ms = sum(ds) / len(ds)
