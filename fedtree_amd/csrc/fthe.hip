@@ -217,7 +217,7 @@ struct fthe_key {
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
-    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_crt_h, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
@@ -263,6 +263,10 @@ enum Slot : int {
 };
 
 static int nslots_for(const fthe_key *k) { return SL_TAB + k->tabn_max; }
+
+// The p half of every CRT encrypt program ends here: X = cp (< 2p^2) -> (cp + v) (q^2)^-1 mod p^2
+// into T2, with v = K - cq in T0 (k_crt_prep_q, run after the q half) and Mont((q^2)^-1) in T1.
+static void crt_tail(Prog &e) { e.addslot(SL_T0); e.mul(SL_T1); e.storex(SL_T2); }
 
 // One-lane kernels prefetch multipliers into LDS (PREFA/MULA); FTHE_NO_LDSDMA=1 turns it off (A/B).
 static bool lds_prefetch(const Shape &sh) {
@@ -489,12 +493,12 @@ static int key_finish(fthe_key *k) {
         k->c_R3q = k->add_const(L_(k->mq2.m.R3));
         k->c_p2 = k->add_const(L_(p2));
         k->c_q2 = k->add_const(L_(q2));
-        // u = cp + K - cq (k_crt_enc_prep) with K = p^2 (floor(q^2 / p^2) + 1) > q^2 > cq:
-        // u >= 0 and u = cp - cq (mod p^2) whatever the ratio q / p (K = 2 p^2 failed for
-        // q > sqrt(2) p).  u < K + p^2 must stay a valid Montgomery operand: < R / 2.
+        // u = cp + (K - cq) (k_crt_prep_q + the p program's CRT tail) with K = p^2 (floor(q^2/p^2) + 1)
+        // > q^2 > cq: u >= 0 and u = cp - cq (mod p^2) whatever the ratio q / p (K = 2 p^2 failed
+        // for q > sqrt(2) p).  u < K + 2 p^2 must stay a valid Montgomery operand: < R / 2.
         mpz_fdiv_q(t, q2, p2); mpz_add_ui(t, t, 1); mpz_mul(t, t, p2);
         {
-            Mpz lim; mpz_add(lim, t, p2); mpz_mul_2exp(lim, lim, 1);
+            Mpz lim; mpz_add(lim, t, p2); mpz_add(lim, lim, p2); mpz_mul_2exp(lim, lim, 1);   // cp + v < K + 2p^2
             if (mpz_cmp(lim, k->mp2.m.R) >= 0) return FTHE_ERR_UNSUPPORTED;
         }
         k->c_2p2 = k->add_const(L_(t));
@@ -543,13 +547,10 @@ static int key_finish(fthe_key *k) {
                 e.storex(SL_SAVED);
                 e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);    // m (n mod P^2)
                 e.addsmall(1); e.mul(SL_SAVED);                  // (1 + m n) r^n mod P^2
-                e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+                if (side) e.storex(SL_OUTQ); else crt_tail(e);
+                e.end();
                 (side ? k->pr_enc_q : k->pr_enc_p) = k->add_prog(e);
             }
-        }
-        {   // h = (cp - cq) (q^2)^-1 mod p^2
-            Prog h; h.loadx(SL_T0); h.mul(SL_T1); h.storex(SL_T2); h.end();
-            k->pr_crt_h = k->add_prog(h);
         }
         // --- CRT decrypt constants
         k->c_p = k->add_const(L_(k->p));
@@ -1122,14 +1123,13 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
             hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
             pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lc.slot(SL_T3), S, L, Lc.B);
             pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lc.slot(SL_T4), S, L, Lc.B);
-            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;
             if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
-            hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
-                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+            hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
+                               k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;          // ends with h = (cp - cq) q^-2 in T2
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
-            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
-                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+            mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
+                        k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
             if (pipe && (rc = pipe->after(off, cnt))) return rc;
             continue;
         }
@@ -1152,15 +1152,14 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
                                Lc.slot(SL_T3), S, L);
             hipLaunchKernelGGL(k_copy_limbs, Lc.grid(), dim3(256), 0, c->stream, L1.slot(SL_OUTQ), L1.S,
                                Lc.slot(SL_T4), S, L);
-            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;
             if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
-            hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
-                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+            hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
+                               k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;          // ends with h = (cp - cq) q^-2 in T2
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
-            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
-                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+            mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
+                        k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else {
             pack_rows(c->stream, rw, rwn, cnt, 0,
                                Lc.slot(SL_IN0), S, L, Lc.B);
@@ -1352,7 +1351,8 @@ int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
             expo(e, F.nwin_crt);
             e.storex(SL_SAVED);
             e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
-            e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+            if (side) e.storex(SL_OUTQ); else crt_tail(e);
+            e.end();
             double mm;
             add(e, side ? F.off_q : F.off_p, mm);
             F.mm_crt = mm;
@@ -1449,14 +1449,13 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
         if (crt) {
             const void *rp[2] = {F.d_tab_p, dig_p};
             const void *rq[2] = {F.d_tab_q, sides == 2 ? dig_q : dig_p};
-            if ((rc = Lc.prog_raw(prog + F.off_p, F.mm_crt, k->mp2, rp, 2))) return rc;
             if ((rc = Lc.prog_raw(prog + F.off_q, F.mm_crt, k->mq2, rq, 2))) return rc;
-            hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
-                               k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+            hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
+                               k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+            if ((rc = Lc.prog_raw(prog + F.off_p, F.mm_crt, k->mp2, rp, 2))) return rc;
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
-            hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
-                               k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+            mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
+                        k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else if (F.pub_rows) {
             const void *rows[3] = {F.d_tab_pub, dig_p, out + off * cw};
             if ((rc = Lc.prog_raw(prog + F.off_pub, F.mm_pub, k->mn2, rows, 3))) return rc;
@@ -1582,8 +1581,9 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
         for (int j = 1; j < X.nb * X.nwin; j++) e.mulgd16(j);
         e.storex(SL_SAVED);
         e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
-        e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
-        X.off[side] = progs.size(); X.mm = e.montmuls;
+        if (side) e.storex(SL_OUTQ); else crt_tail(e);
+        e.end();
+        X.off[side] = progs.size(); X.mm = std::max(X.mm, e.montmuls);
         progs.insert(progs.end(), e.w.begin(), e.w.end());
     }
     gmp_randclear(st);
@@ -1670,14 +1670,13 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
         hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         const void *rp[2] = {X.d_tab[0], dig[0]};
         const void *rq[2] = {X.d_tab[1], dig[1]};
-        if ((rc = Lc.prog_raw(X.d_prog + X.off[0], X.mm, k->mp2, rp, 2))) return rc;
         if ((rc = Lc.prog_raw(X.d_prog + X.off[1], X.mm, k->mq2, rq, 2))) return rc;
-        hipLaunchKernelGGL(k_crt_enc_prep, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), Lc.slot(SL_OUTQ),
-                           k->cst(k->c_p2), k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-        if ((rc = Lc.prog(k->pr_crt_h, k->mp2))) return rc;
+        hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
+                           k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+        if ((rc = Lc.prog_raw(X.d_prog + X.off[0], X.mm, k->mp2, rp, 2))) return rc;
         hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
-        hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S,
-                           k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+        mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
+                    k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
     return end_call(c, Lc);

@@ -16,10 +16,13 @@ __global__ void k_pack_u64(const uint64_t *m, size_t count, uint32_t *slot, int 
 __global__ void k_copy_limbs(const uint32_t *src, int Ssrc, uint32_t *dst, int Sdst, int L);
 __global__ void k_fill_const(const uint32_t *limbs, uint32_t *slot, int S, int L);
 __global__ void k_canon(uint32_t *x, const uint32_t *N, int S, int L, int rb);
-__global__ void k_crt_enc_prep(uint32_t *cp, uint32_t *cq, const uint32_t *p2, const uint32_t *q2,
-                               const uint32_t *two_p2, uint32_t *u, int S, int L, int rb);
+__global__ void k_crt_prep_q(uint32_t *cq, const uint32_t *q2, const uint32_t *kconst, uint32_t *v, int S, int L,
+                             int rb);
 __global__ void k_mul_add_out(const uint32_t *a, int na, const uint32_t *B, int nb, const uint32_t *h, int nh,
                               int L, size_t count, uint32_t *out, int wout, uint64_t *out_low, int rb);
+// out = a + B h; the na = nb = nh = 37 / 74 forms on the register kernel (CRT recombination)
+void mul_add_out(hipStream_t st, dim3 grid, const uint32_t *a, int na, const uint32_t *B, int nb, const uint32_t *h,
+                 int nh, int L, size_t count, uint32_t *out, int wout, uint64_t *out_low, int rb);
 __global__ void k_dec_lfunc(uint32_t *x, const uint32_t *P2, int S, const uint32_t *Pinv, int ky, uint32_t *y, int L, int rb);
 __global__ void k_crt_dec_prep(uint32_t *mp, uint32_t *mq, const uint32_t *p, const uint32_t *q,
                                const uint32_t *two_p, uint32_t *d, int S, int L, int rb);
