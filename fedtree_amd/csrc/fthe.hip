@@ -1739,9 +1739,9 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         if ((rc = Lc.prog(k->pr_dec_t, k->mp))) return rc;
         hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T4), k->cst(k->c_p), S, L, Lc.B);
         // m = mq + q t   (< n)
-        hipLaunchKernelGGL(k_mul_add_out, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), S, k->cst(k->c_q),
-                           k->kq, Lc.slot(SL_T4), k->kp, L, cnt, m_full ? m_full + off * nw : (uint32_t *)nullptr, nw,
-                           m_low ? m_low + off : (uint64_t *)nullptr, Lc.B);
+        mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S, k->cst(k->c_q), k->kq, Lc.slot(SL_T4), k->kp, L, cnt,
+                    m_full ? m_full + off * nw : (uint32_t *)nullptr, nw, m_low ? m_low + off : (uint64_t *)nullptr,
+                    Lc.B);
         if (off + L < count) {   // restore the exponentiation constants for the next chunk
             Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p); Lc.fill(SL_C2, k->c_R2q);
         }
