@@ -18,10 +18,13 @@
 //     exit(1) / CHECK aborts.
 #pragma once
 #include <gmp.h>
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <exception>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fthe.h"
@@ -51,6 +54,26 @@ inline void to_words(const mpz_t x, uint32_t *w, int nw) {
     mpz_export(w, &cnt, -1, 4, 0, 0, x);
 }
 inline void from_words(mpz_t x, const uint32_t *w, int nw) { mpz_import(x, (size_t)nw, -1, 4, 0, 0, w); }
+// The per-element mpz marshalling of a large batch on several host threads (a few hundred ns
+// per ciphertext; at the engine's rates it would otherwise dominate a batch call).  Small batches
+// stay on the calling thread, which may itself be one of FedTree's OpenMP workers.
+template <class F>
+inline void parallel_for(size_t n, F f) {
+    const size_t grain = 1 << 16;
+    unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < 2 * grain || nt < 2) { f(0, n); return; }
+    nt = (unsigned)std::min<size_t>(nt, n / grain);
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(nt);                // a worker's exception resurfaces here
+    const size_t per = (n + nt - 1) / nt;
+    for (unsigned t = 1; t < nt; t++) {
+        const size_t b = t * per, e = std::min(n, b + per);
+        if (b < e) th.emplace_back([=, &f, &err] { try { f(b, e); } catch (...) { err[t] = std::current_exception(); } });
+    }
+    try { f(0, std::min(n, per)); } catch (...) { err[0] = std::current_exception(); }
+    for (auto &x : th) x.join();
+    for (auto &e : err) if (e) std::rethrow_exception(e);
+}
 // codec of common.h:81-86 and paillier_gpu.cu:487
 inline uint64_t encode(float_type v) { long l = (long)(v * 1e6); return (uint64_t)l; }
 inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 1e6; }
@@ -99,16 +122,20 @@ public:
         size_t n = message.size();
         int nw = fthe_key_n_words(key_), cw = 2 * nw;
         std::vector<uint64_t> m(2 * n);
-        for (size_t i = 0; i < n; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
+        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
+        });
         std::vector<uint32_t> c(2 * n * (size_t)cw);
         int flags = enc_flags;            // the exact fixed-base mode needs p, q: key holder only
         if (!fthe_key_has_private(key_)) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
         fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
                                           flags), "encrypt");
-        for (size_t i = 0; i < n; i++) {
-            fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
-            fthe_shim::from_words(d[i].h_enc, &c[(n + i) * cw], cw);
-        }
+        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; i++) {
+                fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
+                fthe_shim::from_words(d[i].h_enc, &c[(n + i) * cw], cw);
+            }
+        });
     }
 
     // Paillier_GPU::decrypt(SyncArray<GHPair>&) (paillier_gpu.cu:448-494)
@@ -117,15 +144,19 @@ public:
         size_t n = message.size();
         int nw = fthe_key_n_words(key_), cw = 2 * nw;
         std::vector<uint32_t> c(2 * n * (size_t)cw, 0);
-        for (size_t i = 0; i < n; i++) {
-            if (!d[i].encrypted) continue;
-            fthe_shim::to_words(d[i].g_enc, &c[i * cw], cw);
-            fthe_shim::to_words(d[i].h_enc, &c[(n + i) * cw], cw);
-        }
+        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {      // to_words throws only on oversize input
+            for (size_t i = b; i < e; i++) {
+                if (!d[i].encrypted) continue;
+                fthe_shim::to_words(d[i].g_enc, &c[i * cw], cw);
+                fthe_shim::to_words(d[i].h_enc, &c[(n + i) * cw], cw);
+            }
+        });
         std::vector<uint64_t> m(2 * n);
         fthe_shim::check(fthe_decrypt(key_, fthe_shim::thread_ctx(), c.data(), 2 * n, m.data(), nullptr), "decrypt");
-        for (size_t i = 0; i < n; i++)
-            if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }
+        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; i++)
+                if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }
+        });
     }
 
     // Paillier_GPU::decrypt(GHPair&) (paillier_gpu.cu:497-542)

@@ -34,6 +34,19 @@ int main(int argc, char **argv) {
         if (std::fabs(p.g - 2 * g[i]) > 3e-6 || std::fabs(p.h - 2 * h[i]) > 3e-6) bad++;
         printf("%d: g %.6f (want %.6f)  h %.6f (want %.6f)\n", i, p.g, 2 * g[i], p.h, 2 * h[i]);
     }
+    if (argc > 2 && std::string(argv[2]) == "big") {            // the multi-threaded marshalling path
+        const size_t N = 300000;
+        SyncArray<GHPair> big(N);
+        for (size_t i = 0; i < N; i++) big.host_data()[i] = GHPair(1e-6f * (float)(i % 100000), -0.5f);
+        server.encrypt(big);
+        for (size_t i = 0; i < N; i++) big.host_data()[i].encrypted = true;
+        server.decrypt(big);
+        for (size_t i = 0; i < N; i += 997) {
+            const auto &p = big.host_data()[i];
+            if (std::fabs(p.g - 1e-6f * (float)(i % 100000)) > 2e-6 || std::fabs(p.h + 0.5f) > 2e-6) bad++;
+        }
+        printf("big batch of %zu checked\n", N);
+    }
     GHPair one = gh.host_data()[0];
     server.decrypt(one);                                         // decrypt_gh
     if (std::fabs(one.g - g[0]) > 2e-6) bad++;
