@@ -97,13 +97,13 @@ struct DevBuf {
     void *p = nullptr; size_t n = 0;
     int ensure(size_t bytes) {
         if (bytes <= n) return FTHE_OK;
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr; n = 0;
         if (hipMalloc(&p, bytes) != hipSuccess) return FTHE_ERR_NOMEM;
         n = bytes;
         return FTHE_OK;
     }
-    ~DevBuf() { if (p) hipFree(p); }
+    ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
 // Pinned host staging buffer (page-locked: truly asynchronous DMA).
@@ -111,13 +111,13 @@ struct PinBuf {
     void *p = nullptr; size_t n = 0;
     int ensure(size_t bytes) {
         if (bytes <= n) return FTHE_OK;
-        if (p) hipHostFree(p);
+        if (p) (void)hipHostFree(p);
         p = nullptr; n = 0;
         if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return FTHE_ERR_NOMEM;
         n = bytes;
         return FTHE_OK;
     }
-    ~PinBuf() { if (p) hipHostFree(p); }
+    ~PinBuf() { if (p) (void)hipHostFree(p); }
 };
 
 struct fthe_ctx {
@@ -182,13 +182,13 @@ struct fthe_key {
     uint32_t *d_pqwords = nullptr;  // p then q as pq_w u32 words each (device-drawn y_p, y_q)
     int pq_w = 0;
     ~fthe_key() {
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1}) if (d->d_ctx) hipFree(d->d_ctx);
-        if (d_consts) hipFree(d_consts);
-        if (d_progs) hipFree(d_progs);
-        if (d_nwords) hipFree(d_nwords);
-        if (d_pqwords) hipFree(d_pqwords);
-        for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) hipFree(p);
-        for (uint32_t *p : {xb.d_tab[0], xb.d_tab[1], xb.d_prog}) if (p) hipFree(p);
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1}) if (d->d_ctx) (void)hipFree(d->d_ctx);
+        if (d_consts) (void)hipFree(d_consts);
+        if (d_progs) (void)hipFree(d_progs);
+        if (d_nwords) (void)hipFree(d_nwords);
+        if (d_pqwords) (void)hipFree(d_pqwords);
+        for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) (void)hipFree(p);
+        for (uint32_t *p : {xb.d_tab[0], xb.d_tab[1], xb.d_prog}) if (p) (void)hipFree(p);
     }
     // constant handles
     int add_const(const std::vector<uint32_t> &limbs) {
@@ -323,20 +323,20 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
 
 extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->copy) hipStreamSynchronize(c->copy);
-    for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) hipModuleUnload(c->mod[i]);
-    if (c->cub_tmp) hipFree(c->cub_tmp);
-    for (auto &e : c->prof_ev) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
-    if (c->stream) hipStreamDestroy(c->stream);
-    if (c->copy) hipStreamDestroy(c->copy);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
+    for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) (void)hipModuleUnload(c->mod[i]);
+    if (c->cub_tmp) (void)hipFree(c->cub_tmp);
+    for (auto &e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
     for (int i = 0; i < 2; i++) {
-        if (c->ev_done[i]) hipEventDestroy(c->ev_done[i]);
-        if (c->ev_copied[i]) hipEventDestroy(c->ev_copied[i]);
-        if (c->ev_in[i]) hipEventDestroy(c->ev_in[i]);
+        if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
+        if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+        if (c->ev_in[i]) (void)hipEventDestroy(c->ev_in[i]);
     }
     delete c;
 }
@@ -1278,7 +1278,7 @@ int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipStreamSynchronize(c->stream));
     for (uint32_t **p : {&F.d_tab_pub, &F.d_tab_p, &F.d_tab_q, &F.d_prog})
-        if (*p) { hipFree(*p); *p = nullptr; }
+        if (*p) { (void)hipFree(*p); *p = nullptr; }
     F.ready = false;
     F.window = fb_window();
     const bool wide = F.window == 16;
@@ -1318,7 +1318,7 @@ int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
         if (wide) {
             uint32_t *t16 = nullptr;
             rc = fb_widen(k, c, k->mn2, k->sn2, F.d_tab_pub, nwin16, F.ew_pub, F.pub_rows, &t16);
-            hipFree(F.d_tab_pub);
+            (void)hipFree(F.d_tab_pub);
             F.d_tab_pub = t16;
             if (rc) return rc;
         }
@@ -1343,7 +1343,7 @@ int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
             if (wide) {
                 uint32_t *t16 = nullptr;
                 rc = fb_widen(k, c, D, k->spq, *dt, nwin16, F.ew_crt, false, &t16);
-                hipFree(*dt);
+                (void)hipFree(*dt);
                 *dt = t16;
                 if (rc) return rc;
             }
@@ -1545,7 +1545,7 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipStreamSynchronize(c->stream));
     for (uint32_t **p : {&X.d_tab[0], &X.d_tab[1], &X.d_prog})
-        if (*p) { hipFree(*p); *p = nullptr; }
+        if (*p) { (void)hipFree(*p); *p = nullptr; }
     X.ready = false;
     gmp_randstate_t st;
     gmp_randinit_default(st);
@@ -1574,7 +1574,7 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
         uint32_t *d8 = nullptr;
         if ((rc = fb_upload(tab, &d8))) break;
         rc = fb_widen(k, c, D, k->spq, d8, X.nb * X.nwin, X.ew, false, &X.d_tab[side]);
-        hipFree(d8);
+        (void)hipFree(d8);
         if (rc) break;
         Prog e;                                           // X = prod_j entry(j, digit j), then (1 + m n) X
         e.loadgd16(0);
