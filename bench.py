@@ -304,9 +304,15 @@ def main():
         # the add kernel's HBM side (north star): algorithmic bytes (2 rows in, 1 out, 512 B each)
         # over the live launch time, and the PMC-measured bytes of a full-chunk launch
         pk = pmc.get("add", {}).get("fthe_montprog_s152", {})
+        rate = na / add_s
         secondary["p2048_add_hbm"] = {"algorithmic_GBps": round(na * 1536 / add_s / 1e9, 1),
                                       "pmc_GBps": pk.get("hbm_GBps"), "pmc_VALUBusy": pk.get("VALUBusy"),
-                                      "peak_GBps": 8000, "bound": "valu (2 Montgomery products of 4096 bits per add)"}
+                                      "peak_GBps": 8000, "bound": "valu (2 Montgomery products of 4096 bits per add)",
+                                      # VALU roofline in three units: executed MADs (2 products of
+                                      # 2*152^2 at radix 2^27), two products at W(128), the survey's one W(128)
+                                      "valu_frac_executed": round(rate * 2 * 2 * 152 * 152 / PEAK_MAC_S, 4),
+                                      "valu_frac_two_products": round(rate * 2 * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4),
+                                      "valu_frac_survey_unit": round(rate * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4)}
         del o
         # configs[1]: Paillier-1024, 100k gradient pairs (200k ciphertexts), device-resident
         p1k = Paillier(dev).keygen(1024, seed=SEED + 1)
