@@ -64,6 +64,8 @@ _PROTOS = {
     "fthe_key_fixed_base_exact_bases": (_I, [_P]),
     "fthe_encrypt_u64_dev": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_encrypt_u64": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
+    "fthe_encrypt_words_dev": (_I, [_P, _P, _P, _I, _SZ, _P, _I, _U64, _P, _I]),
+    "fthe_encrypt_words": (_I, [_P, _P, _P, _I, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_decrypt_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_decrypt": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_decrypt_short_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),

@@ -1053,13 +1053,28 @@ int launch_dyn(Launch &Lc, const void *prog, double mm, const DevMod &mod, const
 
 // ---------------------------------------------------------------------------
 // Encrypt
-static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *alpha,
+// Plaintexts of an encrypt call: the u64 codec values of FedTree (m64), or general plaintexts
+// m < n as little-endian words (mw, mww words each: Paillier::encrypt(const ZZ&), paillier.cpp:122).
+struct MsgSrc {
+    const uint64_t *m64 = nullptr;
+    const uint32_t *mw = nullptr;
+    int mww = 0;
+    bool null() const { return !m64 && !mw; }
+    // plaintexts [off, off + cnt) -> the IN1 slot (radix-2^B limbs); g^m = 1 + m n follows in the programs
+    void pack(hipStream_t st, dim3 grid, size_t off, size_t cnt, uint32_t *slot, int S, int L, int B) const {
+        if (m64) hipLaunchKernelGGL(k_pack_u64, grid, dim3(256), 0, st, m64 + off, cnt, slot, S, L, B);
+        else pack_rows(st, mw + off * (size_t)mww, mww, cnt, 0, slot, S, L, B);
+    }
+};
+
+static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *alpha,
                            int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe);
-static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *y,
+static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y,
                            int y_words, uint64_t rng_seed, uint32_t *out, HostPipe *pipe);
-static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r, int r_words,
+static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *r, int r_words,
                         uint64_t rng_seed, uint32_t *out, int flags, HostPipe *pipe) {
-    if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
+    if (!k || !c || (m.null() && count) || (!out && count)) return FTHE_ERR_ARG;
+    if (m.mw && (m.mww <= 0 || m.mww > k->n_words)) return FTHE_ERR_ARG;
     if (r && !(flags & (FTHE_ENC_FIXED_BASE | FTHE_ENC_FIXED_BASE_EXACT)) && (r_words <= 0 || r_words > k->n_words))
         return FTHE_ERR_ARG;
     bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
@@ -1120,7 +1135,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
                                rk, (uint64_t)off, cnt, yp);
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords + k->pq_w, k->pq_w,
                                (int)k->q.bits(), rq, (uint64_t)off, cnt, yq);
-            hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+            m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
             pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lc.slot(SL_T3), S, L, Lc.B);
             pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lc.slot(SL_T4), S, L, Lc.B);
             if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
@@ -1138,7 +1153,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t coun
                                (uint64_t)off, cnt, (uint32_t *)c->scratch.p);
             rw = (const uint32_t *)c->scratch.p; rwn = nw;
         }
-        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+        m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (crt) {
             // r (< n) -> low / high halves in the small layout
             pack_rows(c->stream, rw, rwn, cnt, 0,
@@ -1405,7 +1420,7 @@ extern "C" int fthe_key_fixed_base_info(fthe_key *k, int *alpha_bits_public, int
     return FTHE_OK;
 }
 
-static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *alpha,
+static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *alpha,
                            int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe) {
     int rc = fb_ensure(k, c);
     if (rc) return rc;
@@ -1445,7 +1460,7 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
                 hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, rk, (uint64_t)off, cnt, nwin, L,
                                    bpd, sd, sd ? dig_q : dig_p);
         }
-        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+        m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (crt) {
             const void *rp[2] = {F.d_tab_p, dig_p};
             const void *rq[2] = {F.d_tab_q, sides == 2 ? dig_q : dig_p};
@@ -1623,7 +1638,7 @@ extern "C" int fthe_key_fixed_base_exact_bases(fthe_key *k) {
     return k->xb.ready ? k->xb.nb : 0;
 }
 
-static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *y,
+static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y,
                            int y_words, uint64_t rng_seed, uint32_t *out, HostPipe *pipe) {
     int rc = xb_ensure(k, c);
     if (rc) return rc;
@@ -1667,7 +1682,7 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
                                        L, 2, dst);
                 }
             }
-        hipLaunchKernelGGL(k_pack_u64, Lc.grid(), dim3(256), 0, c->stream, m + off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+        m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         const void *rp[2] = {X.d_tab[0], dig[0]};
         const void *rq[2] = {X.d_tab[1], dig[1]};
         if ((rc = Lc.prog_raw(X.d_prog + X.off[1], X.mm, k->mq2, rq, 2))) return rc;
@@ -1685,7 +1700,14 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t c
 extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count,
                                     const uint32_t *r, int r_words, uint64_t rng_seed,
                                     uint32_t *out, int flags) {
-    return encrypt_impl(k, c, m, count, r, r_words, rng_seed, out, flags, nullptr);
+    MsgSrc ms; ms.m64 = m;
+    return encrypt_impl(k, c, ms, count, r, r_words, rng_seed, out, flags, nullptr);
+}
+
+extern "C" int fthe_encrypt_words_dev(fthe_key *k, fthe_ctx *c, const uint32_t *m, int m_words, size_t count,
+                                      const uint32_t *r, int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
+    MsgSrc ms; ms.mw = m; ms.mww = m_words;
+    return encrypt_impl(k, c, ms, count, r, r_words, rng_seed, out, flags, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -2254,24 +2276,40 @@ struct HostIO {
 };
 }  // namespace
 
-extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
-                                int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
+// Host-resident encrypt: inputs staged and outputs drained chunk by chunk through pinned buffers
+// (HostPipe); m is either u64 codec values or general plaintexts of mww words.
+static int encrypt_host(fthe_key *k, fthe_ctx *c, const void *m, int mww, size_t count, const uint32_t *r,
+                        int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
+    if (mww && (mww < 0 || mww > k->n_words)) return FTHE_ERR_ARG;
     if (r && (r_words <= 0 || r_words > ((flags & FTHE_ENC_FIXED_BASE_EXACT) ? 3 * k->n_words
                                          : k->n_words + ((flags & FTHE_ENC_FIXED_BASE) ? 4 : 0)))) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
-    size_t cw = 2 * (size_t)k->n_words;
+    size_t cw = 2 * (size_t)k->n_words, mb = mww ? (size_t)mww * 4 : 8;
     int rc;
-    if ((rc = c->io[0].ensure(std::max<size_t>(4, count * 8))) || (rc = c->io[2].ensure(std::max<size_t>(4, count * cw * 4))))
+    if ((rc = c->io[0].ensure(std::max<size_t>(4, count * mb))) || (rc = c->io[2].ensure(std::max<size_t>(4, count * cw * 4))))
         return rc;
     if (r && (rc = c->io[1].ensure(std::max<size_t>(4, count * r_words * 4)))) return rc;
     HostPipe pipe{c};
-    pipe.add_in(m, c->io[0].p, 8);
+    pipe.add_in(m, c->io[0].p, mb);
     if (r) pipe.add_in(r, c->io[1].p, (size_t)r_words * 4);
     pipe.add_out(out, c->io[2].p, cw * 4);
-    if ((rc = encrypt_impl(k, c, (const uint64_t *)c->io[0].p, count, r ? (const uint32_t *)c->io[1].p : nullptr, r_words,
+    MsgSrc ms;
+    if (mww) { ms.mw = (const uint32_t *)c->io[0].p; ms.mww = mww; } else ms.m64 = (const uint64_t *)c->io[0].p;
+    if ((rc = encrypt_impl(k, c, ms, count, r ? (const uint32_t *)c->io[1].p : nullptr, r_words,
                            rng_seed, (uint32_t *)c->io[2].p, flags, count ? &pipe : nullptr))) return rc;
     return pipe.finish();
+}
+
+extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
+                                int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
+    return encrypt_host(k, c, m, 0, count, r, r_words, rng_seed, out, flags);
+}
+
+extern "C" int fthe_encrypt_words(fthe_key *k, fthe_ctx *c, const uint32_t *m, int m_words, size_t count,
+                                  const uint32_t *r, int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
+    if (m_words <= 0) return FTHE_ERR_ARG;
+    return encrypt_host(k, c, m, m_words, count, r, r_words, rng_seed, out, flags);
 }
 
 static int decrypt_host(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full,

@@ -435,10 +435,33 @@ class Paillier:
             ctypes.c_void_p(out.data_ptr())), "histogram_dev")
         return out
 
+    def encrypt_words(self, m, r=None, seed=0, public=False):
+        """General plaintexts (Paillier::encrypt(const ZZ&), paillier.cpp:122-139): m is a list of
+        ints (any size up to n_words words) or a (count, words) uint32 array; r as encrypt_u64."""
+        if not isinstance(m, np.ndarray):
+            m = np.stack([_words(int(x), self.n_words) for x in m]) if len(m) else np.zeros((0, self.n_words), np.uint32)
+        m = np.ascontiguousarray(m, dtype=np.uint32)
+        cnt, mw = m.shape
+        out = np.zeros((cnt, self._cw()), dtype=np.uint32)
+        rw = None
+        if r is not None:
+            rw = r if isinstance(r, np.ndarray) else np.stack([_words(int(x), self.n_words) for x in r])
+            rw = np.ascontiguousarray(rw, dtype=np.uint32).reshape(cnt, -1)
+        _lib.check(self.lib.fthe_encrypt_words(self._key, self.dev.ctx, _ptr(m), mw, cnt, _ptr(rw),
+                                               rw.shape[1] if rw is not None else 0, int(seed), _ptr(out),
+                                               self._flags(public, False)), "encrypt_words")
+        return out
+
     # ---- reference single-value signatures (batch of one) ------------------
     def encrypt(self, message, r=None):
-        """Paillier::encrypt(const ZZ&) (paillier.cpp:122).  message < 2^64."""
-        c = self.encrypt_u64(np.array([int(message) % 2**64], np.uint64), None if r is None else [int(r)])
+        """Paillier::encrypt(const ZZ&) (paillier.cpp:122): any plaintext that fits in n_words."""
+        message = int(message)
+        if 0 <= message < 2**64:
+            c = self.encrypt_u64(np.array([message], np.uint64), None if r is None else [int(r)])
+        else:
+            if message < 0 or message.bit_length() > 32 * self.n_words:
+                raise ValueError("plaintext must be a non-negative integer of at most n_words words")
+            c = self.encrypt_words([message], None if r is None else [int(r)])
         return _int(c[0])
 
     def decrypt(self, ciphertext):

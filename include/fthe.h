@@ -107,6 +107,13 @@ int fthe_encrypt_u64_dev(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t
 int fthe_encrypt_u64(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
                      const uint32_t *r, int r_words, uint64_t rng_seed,
                      uint32_t *c, int flags);
+/* General plaintexts (Paillier::encrypt(const ZZ&), paillier.cpp:122-139): m_words little-
+ * endian words per plaintext (m_words <= n_words); otherwise as fthe_encrypt_u64.  Any m that
+ * fits is encrypted exactly as PowerMod(g, m, n^2) r^n (g^m = 1 + m n mod n^2 for every m). */
+int fthe_encrypt_words_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *m, int m_words, size_t count,
+                           const uint32_t *r, int r_words, uint64_t rng_seed, uint32_t *c, int flags);
+int fthe_encrypt_words(fthe_key *key, fthe_ctx *ctx, const uint32_t *m, int m_words, size_t count,
+                       const uint32_t *r, int r_words, uint64_t rng_seed, uint32_t *c, int flags);
 
 /* ---- fixed-base randomizer (flag FTHE_ENC_FIXED_BASE) -----------------------
  * Not in the reference: an opt-in encryption mode for throughput.  One random
