@@ -74,6 +74,8 @@ _PROTOS = {
     "fthe_add": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_scalar_mul_u64_dev": (_I, [_P, _P, _P, _U64, _SZ, _P]),
     "fthe_scalar_mul_u64": (_I, [_P, _P, _P, _U64, _SZ, _P]),
+    "fthe_scalar_mul_words_dev": (_I, [_P, _P, _P, _P, _I, _SZ, _P]),
+    "fthe_scalar_mul_words": (_I, [_P, _P, _P, _P, _I, _SZ, _P]),
     "fthe_reduce_kway_dev": (_I, [_P, _P, _P, _I, _SZ, _P]),
     "fthe_reduce_kway": (_I, [_P, _P, _P, _I, _SZ, _P]),
     "fthe_decimal_max_len": (_SZ, [_I]),

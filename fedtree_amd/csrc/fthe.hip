@@ -2209,7 +2209,8 @@ extern "C" int fthe_scan_segments(fthe_key *k, fthe_ctx *c, const uint32_t *x, c
 }
 
 // out[i] = x[i]^e mod n^2 (Paillier::mul, paillier.cpp:118), e uniform.
-extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, uint64_t e, size_t count, uint32_t *out) {
+// x^e mod n^2 for one exponent e shared by the batch (Paillier::mul, paillier.cpp:107-120)
+static int scalar_mul_impl(fthe_key *k, fthe_ctx *c, const uint32_t *x, const mpz_t ez, size_t count, uint32_t *out) {
     if (!k || !c || ((!x || !out) && count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     Launch Lc;
@@ -2219,13 +2220,12 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
     const bool rowio = k->rowio;
     Prog p;
     p.lds_a = lds_prefetch(k->sn2);
-    if (e == 0) {
+    if (mpz_sgn(ez) == 0) {
         p.loadx(SL_C1);                 // x^0 = 1
     } else {
-        Mpz ez; mpz_import(ez, 1, -1, 8, 0, 0, &e);
         if (rowio) p.loadw(0); else p.loadx(SL_IN0);
         p.mul(SL_C0);                    // Montgomery form
-        p.pow(ez, SL_TAB, SL_SQ, std::min(best_window(ez.bits()), 5));
+        p.pow(ez, SL_TAB, SL_SQ, std::min(best_window(mpz_sizeinbase(ez, 2)), 5));
         p.mul(SL_C1);                    // * 1 -> out of Montgomery
     }
     if (rowio) p.storew(1); else p.storex(SL_OUTP);
@@ -2248,6 +2248,18 @@ extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t 
                            cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
+}
+
+extern "C" int fthe_scalar_mul_u64_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, uint64_t e, size_t count, uint32_t *out) {
+    Mpz ez; mpz_import(ez, 1, -1, 8, 0, 0, &e);
+    return scalar_mul_impl(k, c, x, ez, count, out);
+}
+
+extern "C" int fthe_scalar_mul_words_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, const uint32_t *e, int e_words,
+                                         size_t count, uint32_t *out) {
+    if (!e || e_words <= 0) return FTHE_ERR_ARG;
+    Mpz ez; mpz_from_words(ez, e, e_words);
+    return scalar_mul_impl(k, c, x, ez, count, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -2382,6 +2394,18 @@ extern "C" int fthe_scalar_mul_u64(fthe_key *k, fthe_ctx *c, const uint32_t *x, 
     if ((rc = io.in(0, x, bytes, &dx))) return rc;
     if ((rc = io.outbuf(2, bytes, &dout))) return rc;
     if ((rc = fthe_scalar_mul_u64_dev(k, c, (const uint32_t *)dx, e, count, (uint32_t *)dout))) return rc;
+    return io.back(out, dout, bytes);
+}
+
+extern "C" int fthe_scalar_mul_words(fthe_key *k, fthe_ctx *c, const uint32_t *x, const uint32_t *e, int e_words,
+                                     size_t count, uint32_t *out) {
+    if (!k || !c) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HostIO io{c}; void *dx, *dout; int rc;
+    size_t bytes = count * 2 * (size_t)k->n_words * 4;
+    if ((rc = io.in(0, x, bytes, &dx))) return rc;
+    if ((rc = io.outbuf(2, bytes, &dout))) return rc;
+    if ((rc = fthe_scalar_mul_words_dev(k, c, (const uint32_t *)dx, e, e_words, count, (uint32_t *)dout))) return rc;
     return io.back(out, dout, bytes);
 }
 

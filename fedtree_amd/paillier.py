@@ -475,10 +475,18 @@ class Paillier:
         return _int(self.add_batch(_words(int(x), self._cw())[None], _words(int(y), self._cw())[None])[0])
 
     def mul(self, x, y):
-        """Paillier::mul (paillier.cpp:107), exponent y < 2^64."""
-        if not 0 <= int(y) < 2**64:
-            raise ValueError("exponent must fit in 64 bits (the reference only uses (unsigned long)-1)")
-        return _int(self.scalar_mul(_words(int(x), self._cw())[None], int(y))[0])
+        """Paillier::mul (paillier.cpp:107): x^y mod n^2 for any y >= 0."""
+        y = int(y)
+        if y < 0:
+            raise ValueError("exponent must be non-negative")
+        xw = _words(int(x), self._cw())[None]
+        if y < 2**64:
+            return _int(self.scalar_mul(xw, y)[0])
+        ew = _words(y, (y.bit_length() + 31) // 32)
+        out = np.zeros_like(xw)
+        _lib.check(self.lib.fthe_scalar_mul_words(self._key, self.dev.ctx, _ptr(xw), _ptr(ew), len(ew), 1, _ptr(out)),
+                   "scalar_mul_words")
+        return _int(out[0])
 
 
 # --------------------------------------------------------------------------

@@ -212,6 +212,12 @@ int fthe_scalar_mul_u64_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, uin
                             size_t count, uint32_t *out);
 int fthe_scalar_mul_u64(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, uint64_t k,
                         size_t count, uint32_t *out);
+/* x^e mod n^2 with an exponent of e_words little-endian words (Paillier::mul(x, ZZ y),
+ * paillier.cpp:107-120, any y), one exponent for the batch. */
+int fthe_scalar_mul_words_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, const uint32_t *e, int e_words,
+                              size_t count, uint32_t *out);
+int fthe_scalar_mul_words(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, const uint32_t *e, int e_words,
+                          size_t count, uint32_t *out);
 
 /* ---- k-way product (k-party histogram merge) ---------------------------
  * out[i] = prod_{j<k} x[j*count + i] mod n^2.

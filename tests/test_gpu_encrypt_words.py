@@ -42,3 +42,17 @@ def test_encrypt_words_vs_oracle(dev, name):
     _, full = pl.decrypt_u64(cd, full=True)
     assert [pyoracle.from_words(w) for w in full] == ms[:10]
     assert pl.decrypt(pl.encrypt(ms[0])) == ms[0]
+
+
+@pytest.mark.parametrize("name", GOLDEN_KEYS)
+def test_mul_any_exponent_vs_oracle(dev, name):
+    """Paillier::mul(x, y) = PowerMod(x, y, n^2) for exponents above 64 bits."""
+    from fedtree_amd.paillier import Paillier
+    p, q = golden_key(load_golden(name))
+    pl = Paillier.from_primes(p, q, dev)
+    key = pyoracle.keygen_from_primes(p, q)
+    n, n2 = pl.modulus, pl.modulus ** 2
+    x = pyoracle.encrypt(key, 12345, 777)
+    for y in (2**64, 2**64 + 1, n - 1, 3 * n + 17, 2**(32 * pl.n_words) - 1):
+        assert pl.mul(x, y) == pow(x, y, n2)
+    assert pl.decrypt(pl.mul(x, 2**70 + 3)) == 12345 * (2**70 + 3) % n
