@@ -186,10 +186,17 @@ public:
         int cw = 2 * fthe_key_n_words(key_);
         std::vector<uint32_t> a(cw), o(cw);
         fthe_shim::to_words(x, a.data(), cw);
-        uint64_t k = 0;
-        if (mpz_sizeinbase(y, 2) > 64) throw std::runtime_error("mul: exponent > 64 bits");
-        mpz_export(&k, nullptr, -1, 8, 0, 0, y);
-        fthe_shim::check(fthe_scalar_mul_u64(key_, fthe_shim::thread_ctx(), a.data(), k, 1, o.data()), "mul");
+        if (mpz_sgn(y) < 0) throw std::runtime_error("mul: negative exponent");
+        if (mpz_sizeinbase(y, 2) <= 64) {
+            uint64_t k = 0;
+            mpz_export(&k, nullptr, -1, 8, 0, 0, y);
+            fthe_shim::check(fthe_scalar_mul_u64(key_, fthe_shim::thread_ctx(), a.data(), k, 1, o.data()), "mul");
+        } else {                                        // any exponent (Paillier::mul(x, ZZ y))
+            std::vector<uint32_t> e(words(y));
+            fthe_shim::to_words(y, e.data(), (int)e.size());
+            fthe_shim::check(fthe_scalar_mul_words(key_, fthe_shim::thread_ctx(), a.data(), e.data(), (int)e.size(), 1,
+                                                   o.data()), "mul");
+        }
         fthe_shim::from_words(result, o.data(), cw);
     }
 
