@@ -13,11 +13,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <cmath>
 #include <functional>
 #include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 #include <fcntl.h>
 #include <unistd.h>
@@ -189,6 +191,7 @@ struct fthe_key {
         if (d_pqwords) (void)hipFree(d_pqwords);
         for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) (void)hipFree(p);
         for (uint32_t *p : {xb.d_tab[0], xb.d_tab[1], xb.d_prog}) if (p) (void)hipFree(p);
+        for (uint32_t *p : {pb.d_tab, pb.d_prog}) if (p) (void)hipFree(p);
     }
     // constant handles
     int add_const(const std::vector<uint32_t> &limbs) {
@@ -250,6 +253,16 @@ struct fthe_key {
         size_t off[2] = {0, 0};
         double mm = 0;
     } xb;
+    // ---- public exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT, public form) ----
+    // Bases hs_i = t_i^n mod n^2 published by the key holder, <t_1 .. t_nb> = Z_n^*;
+    // r^n = prod hs_i^y_i with y_i uniform below 2^(16 nwin) >= n 2^64.
+    struct PublicBase {
+        bool ready = false, rows = false;
+        int nb = 0, nwin = 0, ew = 0;     // bases, 16-bit windows per exponent, words per entry
+        Mpz hs[3];
+        uint32_t *d_tab = nullptr, *d_prog = nullptr;
+        double mm = 0;
+    } pb;
     // prime factors of p - 1 and q - 1 when the key generator recorded them (FTHE_KEYGEN_KNOWN_ORDER)
     bool order_known = false;
     std::vector<Mpz> pm1_factors, qm1_factors;
@@ -1071,6 +1084,8 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
                            int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe);
 static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y,
                            int y_words, uint64_t rng_seed, uint32_t *out, HostPipe *pipe);
+static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y, int y_words,
+                           uint64_t rng_seed, uint32_t *out, HostPipe *pipe);
 static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *r, int r_words,
                         uint64_t rng_seed, uint32_t *out, int flags, HostPipe *pipe) {
     if (!k || !c || (m.null() && count) || (!out && count)) return FTHE_ERR_ARG;
@@ -1079,8 +1094,11 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         return FTHE_ERR_ARG;
     bool crt = k->priv && !(flags & FTHE_ENC_PUBLIC);
     if (flags & FTHE_ENC_FIXED_BASE_EXACT) {
-        if (!crt) return k->priv ? FTHE_ERR_UNSUPPORTED : FTHE_ERR_NOPRIV;
-        return encrypt_xb_impl(k, c, m, count, r, r_words, rng_seed, out, pipe);
+        if (crt) return encrypt_xb_impl(k, c, m, count, r, r_words, rng_seed, out, pipe);
+        bool pb_ready;
+        { std::lock_guard<std::mutex> g(k->fb_mu); pb_ready = k->pb.ready; }
+        if (!pb_ready) return k->priv ? FTHE_ERR_UNSUPPORTED : FTHE_ERR_NOPRIV;
+        return encrypt_pb_impl(k, c, m, count, r, r_words, rng_seed, out, pipe);
     }
     if (!crt && !k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     if (flags & FTHE_ENC_FIXED_BASE) return encrypt_fb_impl(k, c, m, count, r, r_words, rng_seed, out, crt, pipe);
@@ -1280,6 +1298,36 @@ int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32
     return end_call(c, Lc);
 }
 
+// Public-form (mod n^2) fixed-base tables for bases hs[0 .. nb), nwin16 16-bit windows each,
+// base after base: one-lane n^2 kernels store radix-2^B limb entries, the four-lane kernel
+// canonical 2 n_words-word rows (k->sn2.lanes == 4).  wide = false keeps 8-bit windows.
+int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, int nwin16, bool wide, uint32_t **d_tab, int *ew) {
+    const MontMod &M = k->mn2.m;
+    const bool rows = k->sn2.lanes == 4;
+    const int cw = 2 * k->n_words;
+    *ew = rows ? cw : 4 * ((M.S + 3) / 4);
+    std::vector<uint32_t> tab;
+    for (int b = 0; b < nb; b++) {
+        std::vector<uint32_t> tb;
+        if (rows)
+            tb = fb_table(hs[b], k->n2, 2 * nwin16, cw, [&M, cw](const mpz_t x, uint32_t *dst) {
+                Mpz t; mpz_mul(t, x, M.R); mpz_mod(t, t, M.N);
+                mpz_to_words(t, dst, cw);
+            });
+        else
+            tb = fb_table(hs[b], k->n2, 2 * nwin16, *ew, fb_store_limbs(M));
+        if (nb == 1) tab.swap(tb);
+        else tab.insert(tab.end(), tb.begin(), tb.end());
+    }
+    int rc;
+    uint32_t *d8 = nullptr;
+    if ((rc = fb_upload(tab, &d8))) return rc;
+    if (!wide) { *d_tab = d8; return FTHE_OK; }
+    rc = fb_widen(k, c, k->mn2, k->sn2, d8, nb * nwin16, *ew, rows, d_tab);
+    (void)hipFree(d8);
+    return rc;
+}
+
 // FTHE_FB_WINDOW=8 keeps the host-built 8-bit tables; the default widens them to 16 bits
 // on the device (2x fewer products per encryption, 65536 entries per window).
 int fb_window() {
@@ -1316,27 +1364,7 @@ int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
         const int nwin16 = (k->n_bits + 64 + 15) / 16;          // alpha: n_bits + 64 bits
         F.nwin_pub = wide ? nwin16 : 2 * nwin16;
         F.pub_rows = k->sn2.lanes == 4;
-        const MontMod &M = k->mn2.m;
-        std::vector<uint32_t> tab;
-        if (F.pub_rows) {
-            F.ew_pub = 2 * k->n_words;
-            const int cw = F.ew_pub;
-            tab = fb_table(F.hs, k->n2, 2 * nwin16, cw, [&M, cw](const mpz_t x, uint32_t *dst) {
-                Mpz t; mpz_mul(t, x, M.R); mpz_mod(t, t, M.N);
-                mpz_to_words(t, dst, cw);
-            });
-        } else {
-            F.ew_pub = 4 * ((M.S + 3) / 4);
-            tab = fb_table(F.hs, k->n2, 2 * nwin16, F.ew_pub, fb_store_limbs(M));
-        }
-        if ((rc = fb_upload(tab, &F.d_tab_pub))) return rc;
-        if (wide) {
-            uint32_t *t16 = nullptr;
-            rc = fb_widen(k, c, k->mn2, k->sn2, F.d_tab_pub, nwin16, F.ew_pub, F.pub_rows, &t16);
-            (void)hipFree(F.d_tab_pub);
-            F.d_tab_pub = t16;
-            if (rc) return rc;
-        }
+        if ((rc = pub_tables(k, c, &F.hs, 1, nwin16, wide, &F.d_tab_pub, &F.ew_pub))) return rc;
         Prog e;
         expo(e, F.nwin_pub);
         e.storex(SL_SAVED);
@@ -1636,6 +1664,235 @@ extern "C" int fthe_key_fixed_base_exact_bases(fthe_key *k) {
     if (!k) return 0;
     std::lock_guard<std::mutex> g(k->fb_mu);
     return k->xb.ready ? k->xb.nb : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Public exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT, public form).
+//
+// Parties hold only n (party.h:181-185) and encrypt their histograms with the
+// public formula (Party::encrypt_histogram, party.h:118-142), r uniform in Z_n^*.
+// r -> r^n mod n^2 is a homomorphism of Z_n^* (r^n depends on r mod n only), so
+// with published bases hs_i = t_i^n mod n^2 for t_1 .. t_nb generating Z_n^*, a
+// uniform r^n is prod hs_i^y_i for y uniform modulo the group order.  The party
+// does not know the order (it is phi(n)); it draws y_i uniform below 2^(16 nwin)
+// >= n 2^64, which is within nb 2^-64 (statistical distance) of uniform modulo
+// any order <= n.  The key holder picks and checks the t_i: Z_n^* = Z_p^* x Z_q^*
+// needs, at every prime l | (p-1)(q-1), images spanning (Z_p^*/l-th powers) x
+// (Z_q^*/l-th powers): one non-l-th power when l divides one of p-1, q-1, rank 2
+// over GF(l) when it divides both (2 always does).  Checked exactly at every
+// l < 2^24 (discrete logs in mu_l by baby-step giant-step), and at every l for
+// FTHE_KEYGEN_KNOWN_ORDER keys (nb = 2); with 3 bases a larger l escapes with
+// probability < 2^-65 per key (l^-3 per l dividing one side, as for the CRT mode).
+namespace {
+
+uint64_t mpz_low64(const mpz_t x) { return mpz_sgn(x) == 0 ? 0 : (uint64_t)mpz_getlimbn(x, 0); }
+
+// d with z^d = a mod P, z of prime order l (< 2^24); -1 when a is not in <z>
+long dlog_mu(const mpz_t z, const mpz_t a, uint32_t l, const mpz_t P) {
+    const uint32_t m = (uint32_t)std::ceil(std::sqrt((double)l));
+    std::unordered_map<uint64_t, uint32_t> baby;
+    baby.reserve(2 * m);
+    Mpz x(1), y, t, zm, chk;
+    for (uint32_t j = 0; j < m; j++) {
+        baby.emplace(mpz_low64(x), j);
+        mpz_mul(t, x, z); mpz_mod(x, t, P);
+    }
+    mpz_powm_ui(zm, z, (unsigned long)(l - (m % l)) % l, P);     // z^-m (z has order l)
+    mpz_set(y, a);
+    for (uint32_t i = 0; i <= m; i++) {
+        auto it = baby.find(mpz_low64(y));
+        if (it != baby.end()) {
+            const unsigned long d = ((unsigned long)i * m + it->second) % l;
+            mpz_powm_ui(chk, z, d, P);
+            if (mpz_cmp(chk, a) == 0) return (long)d;
+        }
+        mpz_mul(t, y, zm); mpz_mod(y, t, P);
+    }
+    return -1;
+}
+
+// do t[0 .. nb) generate Z_n^* at the primes l of `ls` (each dividing p-1 or q-1)?
+bool pb_generates(const Mpz *t, int nb, const mpz_t p, const mpz_t q, const std::vector<Mpz> &ls) {
+    Mpz pm1, qm1, e, a[3], b[3], bd;
+    mpz_sub_ui(pm1, p, 1); mpz_sub_ui(qm1, q, 1);
+    for (const Mpz &l : ls) {
+        const bool inp = mpz_divisible_p(pm1, l), inq = mpz_divisible_p(qm1, l);
+        if (inp) { mpz_divexact(e, pm1, l); for (int i = 0; i < nb; i++) mpz_powm(a[i], t[i], e, p); }
+        if (inq) { mpz_divexact(e, qm1, l); for (int i = 0; i < nb; i++) mpz_powm(b[i], t[i], e, q); }
+        int ia = -1, ib = -1;
+        for (int i = 0; i < nb; i++) {
+            if (inp && ia < 0 && mpz_cmp_ui(a[i], 1) != 0) ia = i;
+            if (inq && ib < 0 && mpz_cmp_ui(b[i], 1) != 0) ib = i;
+        }
+        if ((inp && ia < 0) || (inq && ib < 0)) return false;
+        if (!(inp && inq)) continue;
+        if (mpz_sizeinbase(l, 2) > 24) continue;        // no small discrete logs: see the bound above
+        // rank 2: some j with (log a_j, log b_j) not a multiple of (log a_ia, log b_ia) = (1, beta)
+        const uint32_t lu = (uint32_t)mpz_get_ui(l);
+        bool rank2 = false;
+        for (int j = 0; j < nb && !rank2; j++) {
+            if (j == ia) continue;
+            const long d = dlog_mu(a[ia], a[j], lu, p);  // a_j = a_ia^d
+            if (d < 0) return false;                     // cannot happen (mu_l is cyclic): refuse
+            mpz_powm_ui(bd, b[ia], (unsigned long)d, q);
+            rank2 = mpz_cmp(bd, b[j]) != 0;
+        }
+        if (!rank2) return false;
+    }
+    return true;
+}
+
+// the primes l to check: l < 2^24 dividing p-1 or q-1, plus the recorded factors of known-order keys
+std::vector<Mpz> pb_primes(const fthe_key *k) {
+    std::vector<Mpz> ls;
+    if (k->order_known) {
+        for (const std::vector<Mpz> *f : {&k->pm1_factors, &k->qm1_factors})
+            for (const Mpz &l : *f) {
+                bool dup = false;
+                for (const Mpz &x : ls) dup = dup || mpz_cmp(x, l) == 0;
+                if (!dup) ls.push_back(l);
+            }
+        return ls;
+    }
+    Mpz pm1, qm1;
+    mpz_sub_ui(pm1, k->p, 1); mpz_sub_ui(qm1, k->q, 1);
+    for (uint32_t l : small_primes())
+        if (mpz_fdiv_ui(pm1, l) == 0 || mpz_fdiv_ui(qm1, l) == 0) ls.push_back(Mpz(l));
+    return ls;
+}
+
+int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
+    fthe_key::PublicBase &B = k->pb;
+    if (!k->pub_ok || (k->sn2.lanes == 4 && !k->rowio)) return FTHE_ERR_UNSUPPORTED;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipDeviceSynchronize());                       // no call may still read the old tables
+    for (uint32_t **p : {&B.d_tab, &B.d_prog})
+        if (*p) { (void)hipFree(*p); *p = nullptr; }
+    B.ready = false;
+    B.nb = nb;
+    B.nwin = (int)((k->n_bits + 64 + 15) / 16);
+    B.rows = k->sn2.lanes == 4;
+    for (int i = 0; i < nb; i++) mpz_set(B.hs[i], hs[i]);
+    int rc;
+    if ((rc = pub_tables(k, c, B.hs, nb, B.nwin, true, &B.d_tab, &B.ew))) return rc;
+    Prog e;                                              // X = prod_j entry(j, digit j), then (1 + m n) X
+    e.loadgd16(0);
+    for (int j = 1; j < nb * B.nwin; j++) e.mulgd16(j);
+    e.storex(SL_SAVED);
+    e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);
+    if (B.rows) e.storew(2); else e.storex(SL_OUTP);
+    e.end();
+    B.mm = e.montmuls;
+    if ((rc = fb_upload(e.w, &B.d_prog))) return rc;
+    B.ready = true;
+    return FTHE_OK;
+}
+
+}  // namespace
+
+extern "C" int fthe_key_public_bases(fthe_key *k, uint64_t seed, uint32_t *hs, int *nb) {
+    if (!k) return FTHE_ERR_ARG;
+    if (!k->priv) return FTHE_ERR_NOPRIV;
+    const int nbases = k->order_known ? 2 : 3;
+    if (nb) *nb = nbases;
+    if (!hs) return FTHE_OK;
+    gmp_randstate_t st;
+    gmp_randinit_default(st);
+    Mpz sd;
+    mpz_set_ui(sd, seed ? seed : urandom64());
+    mpz_mul_2exp(sd, sd, 64);
+    mpz_add_ui(sd, sd, seed ? 0x5055424241534553ull : urandom64());
+    gmp_randseed(st, sd);
+    const std::vector<Mpz> ls = pb_primes(k);
+    Mpz t[3], span, g;
+    mpz_sub_ui(span, k->n, 3);
+    for (;;) {
+        bool unit = true;
+        for (int i = 0; i < nbases; i++) {
+            mpz_urandomm(t[i], st, span); mpz_add_ui(t[i], t[i], 2);
+            mpz_gcd(g, t[i], k->n);
+            unit = unit && mpz_cmp_ui(g, 1) == 0;
+        }
+        if (unit && pb_generates(t, nbases, k->p, k->q, ls)) break;
+    }
+    gmp_randclear(st);
+    const int cw = 2 * k->n_words;
+    for (int i = 0; i < nbases; i++) {
+        mpz_powm(g, t[i], k->n, k->n2);
+        mpz_to_words(g, hs + (size_t)i * cw, cw);
+    }
+    return FTHE_OK;
+}
+
+extern "C" int fthe_key_set_public_bases(fthe_key *k, fthe_ctx *c, const uint32_t *hs, int nb) {
+    if (!k || !c || !hs || k->device != c->device || nb < 1 || nb > 3) return FTHE_ERR_ARG;
+    const int cw = 2 * k->n_words;
+    Mpz h[3], g;
+    for (int i = 0; i < nb; i++) {
+        mpz_from_words(h[i], hs + (size_t)i * cw, cw);
+        mpz_gcd(g, h[i], k->n);
+        if (mpz_sgn(h[i]) <= 0 || mpz_cmp(h[i], k->n2) >= 0 || mpz_cmp_ui(g, 1) != 0) return FTHE_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(k->fb_mu);
+    return pb_build(k, c, h, nb);
+}
+
+extern "C" int fthe_key_public_bases_info(fthe_key *k, int *nb, int *exp_words) {
+    if (!k) return FTHE_ERR_ARG;
+    std::lock_guard<std::mutex> lk(k->fb_mu);
+    if (!k->pb.ready) return FTHE_ERR_ARG;
+    if (nb) *nb = k->pb.nb;
+    if (exp_words) *exp_words = (k->pb.nwin + 1) / 2;
+    return FTHE_OK;
+}
+
+static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y, int y_words,
+                           uint64_t rng_seed, uint32_t *out, HostPipe *pipe) {
+    const fthe_key::PublicBase &B = k->pb;
+    const int nb = B.nb, ewd = (B.nwin + 1) / 2;          // words per injected exponent
+    if (y && y_words != nb * ewd) return FTHE_ERR_ARG;
+    Launch Lc;
+    int rc;
+    if ((rc = begin_call(c, k, count, Lc, nslots_for(k), k->sn2))) return rc;
+    const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
+    const size_t exp_bytes = (size_t)B.nwin * L * 2, dig_bytes = nb * exp_bytes;
+    if ((rc = c->scratch.ensure(dig_bytes))) return rc;
+    uint8_t *dig = (uint8_t *)c->scratch.p;
+    RngKey rk{};
+    if (!y) {
+        uint64_t sd = rng_seed ? rng_seed : urandom64();
+        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(sd); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
+        rk.nonce = splitmix64(sd) ^ 0x7075626c69636273ull;     // streams apart from the other modes'
+    }
+    Lc.fill(SL_C1, k->c_nRn2);
+    for (size_t off = 0; off < count; off += L) {
+        size_t cnt = std::min((size_t)L, count - off);
+        Lc.live = cnt;
+        if (pipe && (rc = pipe->before(off, L, count))) return rc;
+        for (int b = 0; b < nb; b++) {
+            uint8_t *dst = dig + b * exp_bytes;
+            if (y) {
+                hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, y + off * y_words + (size_t)b * ewd,
+                                   y_words, ewd, cnt, B.nwin, L, 2, dst);
+            } else {
+                RngKey kb = rk;
+                kb.nonce += (uint64_t)(b + 1) << 56;                       // one stream per base
+                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, kb, (uint64_t)off, cnt, B.nwin, L,
+                                   2, 0, dst);
+            }
+        }
+        m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
+        if (B.rows) {
+            const void *rows[3] = {B.d_tab, dig, out + off * cw};
+            if ((rc = Lc.prog_raw(B.d_prog, B.mm, k->mn2, rows, 3))) return rc;
+        } else {
+            const void *rows[2] = {B.d_tab, dig};
+            if ((rc = Lc.prog_raw(B.d_prog, B.mm, k->mn2, rows, 2))) return rc;
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L, cnt, out + off * cw, cw, Lc.B);
+        }
+        if (pipe && (rc = pipe->after(off, cnt))) return rc;
+    }
+    return end_call(c, Lc);
 }
 
 static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y,
@@ -2294,7 +2551,7 @@ static int encrypt_host(fthe_key *k, fthe_ctx *c, const void *m, int mww, size_t
                         int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
     if (mww && (mww < 0 || mww > k->n_words)) return FTHE_ERR_ARG;
-    if (r && (r_words <= 0 || r_words > ((flags & FTHE_ENC_FIXED_BASE_EXACT) ? 3 * k->n_words
+    if (r && (r_words <= 0 || r_words > ((flags & FTHE_ENC_FIXED_BASE_EXACT) ? 3 * (k->n_words + 2)
                                          : k->n_words + ((flags & FTHE_ENC_FIXED_BASE) ? 4 : 0)))) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     size_t cw = 2 * (size_t)k->n_words, mb = mww ? (size_t)mww * 4 : 8;

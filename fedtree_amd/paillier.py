@@ -197,9 +197,13 @@ class Paillier:
         _lib.check(self.lib.fthe_key_from_n(self.dev.ctx, _ptr(w), nw, ctypes.byref(key)), "key_from_n")
         return self._adopt(key)
 
-    def public(self):
-        """Paillier::operator= (paillier.h:12-18): copies modulus, generator, keyLength only."""
-        return Paillier.from_public(self.modulus, self.dev)
+    def public(self, bases=None):
+        """Paillier::operator= (paillier.h:12-18): copies modulus, generator, keyLength only.
+        bases: published public_bases() to build the party's exact fixed-base tables with."""
+        pub = Paillier.from_public(self.modulus, self.dev)
+        if bases is not None:
+            pub.set_public_bases(bases)
+        return pub
 
     @property
     def has_private(self):
@@ -253,6 +257,33 @@ class Paillier:
                 gam[side].append(int.from_bytes(buf.tobytes(), "little"))
         return gam, ew.value
 
+    def public_bases(self, seed=0):
+        """Key holder: bases hs_i = t_i^n mod n^2 with <t_i> = Z_n^* (checked), to publish with n
+        (fthe_key_public_bases).  Returns a list of 3 ints (2 for known-order keys)."""
+        nb = ctypes.c_int()
+        _lib.check(self.lib.fthe_key_public_bases(self._key, int(seed), None, ctypes.byref(nb)), "key_public_bases")
+        hs = np.zeros((nb.value, self._cw()), dtype=np.uint32)
+        _lib.check(self.lib.fthe_key_public_bases(self._key, int(seed), _ptr(hs), ctypes.byref(nb)),
+                   "key_public_bases")
+        return [int.from_bytes(row.tobytes(), "little") for row in hs]
+
+    def set_public_bases(self, hs):
+        """Build the public exact fixed-base tables for published bases (any key)."""
+        arr = np.stack([_words(int(h), self._cw()) for h in hs])
+        _lib.check(self.lib.fthe_key_set_public_bases(self._key, self.dev.ctx, _ptr(arr), len(hs)),
+                   "key_set_public_bases")
+
+    @property
+    def has_public_bases(self):
+        return bool(self._key) and self.lib.fthe_key_public_bases_info(self._key, None, None) == 0
+
+    def public_bases_info(self):
+        """(bases, words per injected exponent) of the built public tables."""
+        nb, ew = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.fthe_key_public_bases_info(self._key, ctypes.byref(nb), ctypes.byref(ew)),
+                   "key_public_bases_info")
+        return nb.value, ew.value
+
     def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
         """c = g^m r^n mod n^2 for every m (paillier.cpp:134-137).
         r: None -> fresh uniform r per ciphertext from the device CSPRNG;
@@ -261,16 +292,23 @@ class Paillier:
            r then injects alpha (ints or (count, words) uint32) instead of r.
         fixed_base_exact: r^n mod p^2, q^2 from the exact generator tables (key holder);
            r then injects the 2 * bases exponents per ciphertext ((count, 2 * bases * n_words/2)
-           uint32 or tuples of ints; bases from fixed_base_exact_info)."""
+           uint32 or tuples of ints; bases from fixed_base_exact_info).  On a public key (or
+           with public=True): r^n = prod hs_i^y_i from the published bases (set_public_bases);
+           r injects the `bases` exponents y_i (tuples of ints, see public_bases_info)."""
         m = np.ascontiguousarray(m, dtype=np.uint64).reshape(-1)
         cnt = len(m)
         out = np.zeros((cnt, self._cw()), dtype=np.uint32)
         rw = None
         if r is not None:
             if not isinstance(r, np.ndarray) and fixed_base_exact:
-                hw = self.n_words // 2             # tuples of 2 * bases exponents (fixed_base_exact_info)
+                if public or not self.has_private:  # tuples of `bases` exponents (public_bases_info)
+                    nb, hw = self.public_bases_info()
+                    tot = nb * hw
+                else:                               # tuples of 2 * bases exponents (fixed_base_exact_info)
+                    hw = self.n_words // 2
+                    tot = 6 * hw
                 r = np.stack([np.concatenate([_words(int(x), hw) for x in t]) for t in r]) if cnt \
-                    else np.zeros((0, 6 * hw), np.uint32)
+                    else np.zeros((0, tot), np.uint32)
             if not isinstance(r, np.ndarray):
                 nw = self.n_words + (2 if fixed_base else 0)
                 if fixed_base and cnt:
@@ -507,7 +545,8 @@ class GHPairs:
 
     def homo_encrypt(self, pl, r_g=None, r_h=None, seed=0, fixed_base_exact=False):
         """GHPair::homo_encrypt (common.h:125-134): encrypt g,h, zero them, set encrypted.
-        fixed_base_exact: the key holder's table-driven randomizer (same distribution)."""
+        fixed_base_exact: the table-driven randomizer (key holder: same distribution; public
+        key with published bases: within 2^-62 of it; otherwise the default path)."""
         if self.encrypted:
             return self
         m = np.concatenate([encode_fixed(self.g), encode_fixed(self.h)])
@@ -515,7 +554,8 @@ class GHPairs:
         if r_g is not None:
             r = np.concatenate([np.asarray(r_g, np.uint32).reshape(len(self), -1),
                                 np.asarray(r_h, np.uint32).reshape(len(self), -1)])
-        c = pl.encrypt_u64(m, r=r, seed=seed, fixed_base_exact=fixed_base_exact and r is None and pl.has_private)
+        fbx = fixed_base_exact and r is None and (pl.has_private or pl.has_public_bases)
+        c = pl.encrypt_u64(m, r=r, seed=seed, fixed_base_exact=fbx)
         self.g_enc, self.h_enc = c[:len(self)], c[len(self):]
         self.paillier = pl
         self.g[:] = 0
@@ -600,9 +640,13 @@ class HEServer:
         """server.h:58-67 (NTL build: keygen(keylength))."""
         self.paillier.keygen(keylength, seed)
 
-    def send_key(self, party):
-        """server.h:53-55: party.paillier = paillier (public part only)."""
-        party.paillier = self.paillier.public()
+    def send_key(self, party, bases=False):
+        """server.h:53-55: party.paillier = paillier (public part only).
+        bases: also publish checked fixed-base bases (Paillier.public_bases) for the
+        parties' FTHE_ENC_FIXED_BASE_EXACT histogram encryption."""
+        if bases and not hasattr(self, "_bases"):
+            self._bases = self.paillier.public_bases()
+        party.paillier = self.paillier.public(self._bases if bases else None)
 
     def encrypt_gh_pairs(self, raw, seed=0, fixed_base_exact=False):
         """server.h:113-135."""
@@ -623,9 +667,9 @@ class HEParty:
     def __init__(self, paillier=None):
         self.paillier = paillier
 
-    def encrypt_histogram(self, hist, seed=0):
-        """party.h:118-142."""
-        return hist.homo_encrypt(self.paillier, seed=seed)
+    def encrypt_histogram(self, hist, seed=0, fixed_base_exact=False):
+        """party.h:118-142.  fixed_base_exact: the published-bases randomizer (send_key(bases=True))."""
+        return hist.homo_encrypt(self.paillier, seed=seed, fixed_base_exact=fixed_base_exact)
 
     def compute_histogram(self, gh, bin_ids, cut_col_ptr, max_num_bin):
         """Histogram of one node (hist_tree_builder.cpp:565-595, n_nodes_in_level == 1):

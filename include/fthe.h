@@ -137,7 +137,7 @@ int fthe_key_fixed_base(fthe_key *key, fthe_ctx *ctx, const uint32_t *h, int h_w
 int fthe_key_fixed_base_info(fthe_key *key, int *alpha_bits_public, int *alpha_bits_crt, uint32_t *hs);
 
 /* ---- exact fixed-base randomizer (flag FTHE_ENC_FIXED_BASE_EXACT) -----------
- * Key holder only (CRT; FTHE_ERR_NOPRIV without p, q).  The reference's r is
+ * Key holder (CRT; public keys: see fthe_key_set_public_bases).  The reference's r is
  * uniform in Z_n^* (paillier.cpp:127-133); then r^n mod P^2 (P = p, q) is
  * uniform over G_P = {x^P mod P^2}, cyclic of order P - 1, independently for p
  * and q.  Here, per prime, three bases gam_i = t_i^P mod P^2 with
@@ -163,6 +163,35 @@ int fthe_key_fixed_base_exact_info(fthe_key *key, int side, int base, uint32_t *
  * (one generator); 0 before a build.  Injected exponents then take 2 * bases * (n_words/2)
  * words per ciphertext (y_{p,1..bases}, y_{q,1..bases}). */
 int fthe_key_fixed_base_exact_bases(fthe_key *key);
+
+/* ---- public exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT, public form) ----
+ * Parties hold only n (party.h:181-185) and encrypt with the public formula
+ * (Party::encrypt_histogram, party.h:118-142; paillier.cpp:122-139), r uniform in
+ * Z_n^*.  r^n mod n^2 depends on r mod n only and is multiplicative, so with bases
+ * hs_i = t_i^n mod n^2 for t_1 .. t_nb generating Z_n^*, r^n = prod hs_i^y_i for
+ * exponents y_i uniform modulo the group order.  Holding n alone, the encrypting
+ * side draws y_i uniform below 2^(16 nwin), nwin = ceil((bits(n) + 64) / 16): the
+ * ciphertext distribution is within nb * 2^-64 (statistical distance) of the
+ * reference's, from nb * nwin gathered products of 16-bit-window tables (~13 GB
+ * at P-2048 with 3 bases) instead of ~1.2 bits(n) products mod n^2.
+ * fthe_key_public_bases      key holder (FTHE_ERR_NOPRIV otherwise): draws t_i and
+ *                            checks <t_i> = Z_n^* at every prime l < 2^24 dividing
+ *                            p-1 or q-1 (rank 2 over GF(l) where l divides both;
+ *                            a larger l escapes with probability < 2^-65), at every
+ *                            l for FTHE_KEYGEN_KNOWN_ORDER keys; writes hs_i (nb *
+ *                            2*n_words words; hs NULL: *nb only).  nb = 3, or 2
+ *                            for known-order keys.  seed 0: /dev/urandom.  Host only.
+ * fthe_key_set_public_bases  any key with the public form: builds the tables for the
+ *                            published hs (nb * 2*n_words words, 1 <= nb <= 3); then
+ *                            FTHE_ENC_FIXED_BASE_EXACT on a public key (or with
+ *                            FTHE_ENC_PUBLIC) uses them.  Not concurrent with calls
+ *                            that use the key.
+ * fthe_key_public_bases_info nb and the words per injected exponent (exp_words) of
+ *                            the built tables; injected exponents (parity): r = y,
+ *                            r_words = nb * exp_words, y_i < 2^(16 nwin). */
+int fthe_key_public_bases(fthe_key *key, uint64_t seed, uint32_t *hs, int *nb);
+int fthe_key_set_public_bases(fthe_key *key, fthe_ctx *ctx, const uint32_t *hs, int nb);
+int fthe_key_public_bases_info(fthe_key *key, int *nb, int *exp_words);
 
 /* ---- decrypt: m = L(c^lambda mod n^2) * mu mod n (paillier.cpp:153-156) ---
  * Computed with CRT over p^2, q^2 (identical canonical result).

@@ -1,0 +1,215 @@
+"""Public exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT on a public key,
+include/fthe.h fthe_key_public_bases / fthe_key_set_public_bases) on the GPU.
+
+Parties encrypt their histograms with n alone (Party::encrypt_histogram,
+party.h:118-142; public formula paillier.cpp:122-139, r uniform in Z_n^*).  The
+key holder publishes bases hs_i = t_i^n mod n^2 with <t_i> = Z_n^*; a party draws
+r^n as prod hs_i^y_i with y_i uniform below 2^(16 nwin) >= n 2^64.  Checked here:
+
+* the published bases: each hs_i is an n-th residue mod n^2 (hs^phi(n) = 1), and
+  hs_i mod p, mod q span every quotient Z_P^*/l-th powers for the small primes l
+  dividing p-1 or q-1 (one non-l-th power where l divides one of them, rank 2 over
+  GF(l) where it divides both) -- recomputed in Python from hs alone (t -> t^n is a
+  bijection of Z_P^*, so the images carry the t_i's span);
+* injected exponents: bit-exact against (1 + m n) prod hs_i^y_i mod n^2 (Python
+  pow) at the three golden key sizes (one-lane n^2 kernels at 512/1023 bits, the
+  four-lane row form at 2048), incl. y = 0, 1 and the largest exponent covered;
+* device-drawn exponents: round trips, seeded determinism, fresh ciphertexts, the
+  Server/Party histogram flow, known-order keys (2 bases);
+* refusals: no bases (public key: FTHE_ERR_NOPRIV), bad bases, bases without p, q.
+Integer work: every comparison is exact.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import GOLDEN_KEYS, golden_key, load_golden
+from fedtree_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from fedtree_amd.paillier import Device
+    return Device(0)
+
+
+def _primes_below(n):
+    s = np.ones(n, bool)
+    s[:2] = False
+    for i in range(2, int(n ** 0.5) + 1):
+        if s[i]:
+            s[i * i::i] = False
+    return [int(x) for x in np.nonzero(s)[0]]
+
+
+SMALL = _primes_below(1 << 12)
+
+
+def _dlog(z, a, l, P):
+    x = 1
+    for d in range(l):
+        if x == a:
+            return d
+        x = x * z % P
+    raise AssertionError("not in <z>")
+
+
+def _check_public_bases(hs, p, q, ls=SMALL):
+    n = p * q
+    n2 = n * n
+    phi = (p - 1) * (q - 1)
+    for h in hs:
+        assert 1 < h < n2 and math.gcd(h, n) == 1 and pow(h, phi, n2) == 1
+    for l in ls:
+        inp, inq = (p - 1) % l == 0, (q - 1) % l == 0
+        if not (inp or inq):
+            continue
+        a = [pow(h % p, (p - 1) // l, p) for h in hs] if inp else None
+        b = [pow(h % q, (q - 1) // l, q) for h in hs] if inq else None
+        if inp:
+            assert any(x != 1 for x in a), l
+        if inq:
+            assert any(x != 1 for x in b), l
+        if inp and inq and l < 1 << 12:
+            i = next(i for i, x in enumerate(a) if x != 1)
+            # rank 2: some j whose (log a_j, log b_j) is not a multiple of base i's
+            assert any(pow(b[i], _dlog(a[i], a[j], l, p), q) != b[j] for j in range(len(hs)) if j != i), l
+
+
+def _want(n, m, ys, hs):
+    n2 = n * n
+    v = (1 + int(m) * n) % n2
+    for y, h in zip(ys, hs):
+        v = v * pow(h, y, n2) % n2
+    return v
+
+
+@pytest.mark.parametrize("name", GOLDEN_KEYS)
+def test_public_exact_injected_exponents(dev, name):
+    from fedtree_amd.paillier import Paillier
+    p, q = golden_key(load_golden(name))
+    n = p * q
+    server = Paillier.from_primes(p, q, dev)
+    hs = server.public_bases(seed=7)
+    assert len(hs) == 3
+    _check_public_bases(hs, p, q)
+    assert server.public_bases(seed=7) == hs and server.public_bases(seed=8) != hs
+    party = server.public(bases=hs)
+    assert not party.has_private and party.has_public_bases
+    nb, ew = party.public_bases_info()
+    nwin = (n.bit_length() + 64 + 15) // 16
+    assert nb == 3 and ew == (nwin + 1) // 2
+    ebits = 16 * nwin
+    rng = np.random.default_rng(len(name) + 300)
+    cnt = 24
+    m = rng.integers(0, 2**64, cnt, dtype=np.uint64)
+    m[:3] = [0, 1, 2**64 - 1]
+    ys = [tuple(int.from_bytes(rng.bytes(ebits // 8), "little") for _ in range(nb)) for _ in range(cnt)]
+    ys[0] = (0,) * nb
+    ys[1] = (1,) * nb
+    ys[2] = ((1 << ebits) - 1,) * nb
+    ys[3] = ((p - 1) * (q - 1), 0, 0)                        # hs^phi(n) = 1
+    c = party.encrypt_u64(m, r=ys, fixed_base_exact=True)
+    want = [_want(n, x, y, hs) for x, y in zip(m, ys)]
+    assert pyoracle.words_to_ints(c) == want
+    assert pyoracle.from_words(c[0]) == 1 and pyoracle.from_words(c[3]) == (1 + int(m[3]) * n) % (n * n)
+    assert np.array_equal(server.decrypt_u64(c), m)
+    # the key holder with the same bases, public form: identical ciphertexts
+    server.set_public_bases(hs)
+    assert np.array_equal(server.encrypt_u64(m, r=ys, public=True, fixed_base_exact=True), c)
+
+
+@pytest.mark.parametrize("name", ["ref_gmp_L2048.json", "ref_gmp_L4096.json"])
+def test_public_exact_random_roundtrip(dev, coracle, name):
+    from fedtree_amd.paillier import Paillier
+    p, q = golden_key(load_golden(name))
+    server = Paillier.from_primes(p, q, dev)
+    party = server.public(bases=server.public_bases())
+    cnt = 200003
+    m = np.random.default_rng(9).integers(0, 2**64, cnt, dtype=np.uint64)
+    c = party.encrypt_u64(m, seed=31, fixed_base_exact=True)
+    assert np.array_equal(server.decrypt_u64(c), m)
+    idx = np.arange(0, cnt, 997)
+    assert len({bytes(c[i]) for i in idx}) == len(idx)
+    assert np.array_equal(party.encrypt_u64(m[:3000], seed=31, fixed_base_exact=True), c[:3000])
+    assert not np.array_equal(party.encrypt_u64(m[:3000], seed=32, fixed_base_exact=True), c[:3000])
+    same = party.encrypt_u64(np.full(64, 77, np.uint64), seed=4, fixed_base_exact=True)
+    assert len({bytes(x) for x in same}) == 64
+    ok = coracle.key(pyoracle.to_words(p, server.n_words // 2), pyoracle.to_words(q, server.n_words // 2))
+    dec = ok.decrypt_batch(c[idx[:16]])
+    assert [pyoracle.from_words(d) for d in dec] == [int(x) for x in m[idx[:16]]]
+    s = party.add_batch(c[:1000], c[1000:2000])
+    assert np.array_equal(server.decrypt_u64(s), m[:1000] + m[1000:2000])
+
+
+def test_public_exact_known_order_two_bases(dev):
+    """FTHE_KEYGEN_KNOWN_ORDER: every prime factor of p-1, q-1 is checked, two bases."""
+    from fedtree_amd.paillier import Paillier
+    server = Paillier(dev)
+    server.keygen(1024, seed=77, known_order=True)
+    hs = server.public_bases(seed=3)
+    assert len(hs) == 2
+    p, q = server.p, server.q
+    _check_public_bases(hs, p, q)
+    party = server.public(bases=hs)
+    m = np.arange(20000, dtype=np.uint64) * np.uint64(1000003)
+    c = party.encrypt_u64(m, seed=2, fixed_base_exact=True)
+    assert np.array_equal(server.decrypt_u64(c), m)
+    ys = [(5, 7), (0, 1), (2**1000 + 3, 2**900)]
+    c = party.encrypt_u64(m[:3], r=ys, fixed_base_exact=True)
+    assert pyoracle.words_to_ints(c) == [_want(p * q, x, y, hs) for x, y in zip(m[:3], ys)]
+
+
+def test_public_exact_histogram_flow(dev):
+    """HEServer.send_key(bases=True) -> HEParty.encrypt_histogram(fixed_base_exact=True)
+    -> merged by the party -> decrypted by the server (party.h:118-142, server.h:80-111)."""
+    from fedtree_amd.paillier import GHPairs, HEParty, HEServer, Paillier
+    srv = HEServer(dev)
+    srv.paillier = Paillier.from_primes(*golden_key(load_golden("ref_gmp_L4096.json")), dev)
+    parties = [HEParty(), HEParty()]
+    for pt in parties:
+        srv.send_key(pt, bases=True)
+        assert pt.paillier.has_public_bases
+    rng = np.random.default_rng(12)
+    g = [rng.normal(size=300) for _ in parties]
+    h = [rng.uniform(0.1, 1, size=300) for _ in parties]
+    hists = [pt.encrypt_histogram(GHPairs(gg, hh), seed=i + 1, fixed_base_exact=True)
+             for i, (pt, gg, hh) in enumerate(zip(parties, g, h))]
+    total = (hists[0] + hists[1]).homo_decrypt(srv.paillier)
+    want_g = (np.round(g[0] * 1e6).astype(np.int64) + np.round(g[1] * 1e6).astype(np.int64)) / 1e6
+    assert np.allclose(total.g, want_g, atol=2e-6)
+    # without published bases the flag falls back to the default public path
+    plain = HEParty()
+    srv.send_key(plain)
+    enc = plain.encrypt_histogram(GHPairs(g[0], h[0]), seed=5, fixed_base_exact=True)
+    assert np.allclose(enc.homo_decrypt(srv.paillier).g, np.round(g[0] * 1e6) / 1e6, atol=2e-6)
+
+
+def test_public_exact_refusals(dev):
+    from fedtree_amd.paillier import Paillier
+    p, q = golden_key(load_golden("ref_gmp_L2048.json"))
+    n = p * q
+    server = Paillier.from_primes(p, q, dev)
+    pub = Paillier.from_public(n, dev)
+    with pytest.raises(RuntimeError):                        # no bases: FTHE_ERR_NOPRIV
+        pub.encrypt_u64(np.arange(4, dtype=np.uint64), fixed_base_exact=True)
+    with pytest.raises(RuntimeError):                        # key holder, public form, no bases
+        server.encrypt_u64(np.arange(4, dtype=np.uint64), public=True, fixed_base_exact=True)
+    with pytest.raises(RuntimeError):                        # bases need p, q
+        pub.public_bases()
+    with pytest.raises(RuntimeError):
+        pub.public_bases_info()
+    for bad in ([n], [0], [n * n], [2, 3, 5, 7]):             # not a unit / out of range / nb > 3
+        with pytest.raises(RuntimeError):
+            pub.set_public_bases(bad)
+    assert pub.lib.fthe_key_set_public_bases(pub._key, pub.dev.ctx, None, 0) == _lib.FTHE_ERR_ARG
+    hs = server.public_bases(seed=1)
+    pub.set_public_bases(hs)
+    with pytest.raises(RuntimeError):                        # wrong injected exponent width
+        pub.encrypt_u64(np.arange(2, dtype=np.uint64), r=np.zeros((2, 5), np.uint32), fixed_base_exact=True)
+    c = pub.encrypt_u64(np.arange(4, dtype=np.uint64), seed=1, fixed_base_exact=True)
+    assert np.array_equal(server.decrypt_u64(c), np.arange(4, dtype=np.uint64))
