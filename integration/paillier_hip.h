@@ -99,12 +99,26 @@ public:
         return *this;
     }
 
+    // Key holder: publish checked fixed-base bases with the public key (fthe_key_public_bases).
+    // Parties that receive this key by operator= build their tables from them, and their
+    // encrypt() with enc_flags = FTHE_ENC_FIXED_BASE_EXACT (Party::encrypt_histogram) then draws
+    // r^n from the tables (~5.6x the per-ciphertext rate at P-2048).  Not in the reference.
+    void publish_bases() {
+        int nb = 0;
+        fthe_shim::check(fthe_key_public_bases(key_, 0, nullptr, &nb), "public_bases");
+        bases_.assign((size_t)nb * 2 * fthe_key_n_words(key_), 0);
+        fthe_shim::check(fthe_key_public_bases(key_, 0, bases_.data(), &nb), "public_bases");
+        nbases_ = nb;
+    }
+
     // Paillier_GPU::keygen (paillier_gpu.cu:119-121); key_length = bits of n.
     void keygen() { keygen((int)key_length); }
     void keygen(int keyLength) {
         key_length = (uint32_t)keyLength;
         if (key_) fthe_key_destroy(key_);
         key_ = nullptr;
+        bases_.clear();
+        nbases_ = 0;
         fthe_shim::check(fthe_key_generate_ex(fthe_shim::thread_ctx(), keyLength, 0, keygen_flags, &key_), "keygen");
         export_cpu();
     }
@@ -126,8 +140,8 @@ public:
             for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
         });
         std::vector<uint32_t> c(2 * n * (size_t)cw);
-        int flags = enc_flags;            // the exact fixed-base mode needs p, q: key holder only
-        if (!fthe_key_has_private(key_)) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
+        int flags = enc_flags;            // exact fixed-base: p, q (key holder) or published bases (party)
+        if (!fthe_key_has_private(key_) && !nbases_) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
         fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
                                           flags), "encrypt");
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
@@ -206,12 +220,19 @@ public:
 
 private:
     fthe_key *key_ = nullptr;
+    std::vector<uint32_t> bases_;          // published fixed-base bases (nbases_ x 2 n_words words)
+    int nbases_ = 0;
     static size_t words(const mpz_t x) { return (mpz_sizeinbase(x, 2) + 31) / 32; }
     void copy_public(const Paillier_HIP &o) {
         if (key_) fthe_key_destroy(key_);
         key_ = nullptr;
         paillier_cpu = o.paillier_cpu;                                    // public part only
         parameters_cpu_to_gpu();
+        bases_ = o.bases_;                                                // published with n (publish_bases)
+        nbases_ = o.nbases_;
+        if (nbases_)
+            fthe_shim::check(fthe_key_set_public_bases(key_, fthe_shim::thread_ctx(), bases_.data(), nbases_),
+                             "set_public_bases");
     }
     void export_cpu() {
         int nw = fthe_key_n_words(key_), hw = (nw + 1) / 2;

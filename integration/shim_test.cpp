@@ -11,10 +11,12 @@ int main(int argc, char **argv) {
     Paillier_HIP server;                 // Server::paillier
     if (argc > 2 && std::string(argv[2]) == "exact_known_order") server.keygen_flags = FTHE_KEYGEN_KNOWN_ORDER;
     server.keygen(bits);                 // homo_init (NTL semantics: n of `bits` bits)
+    const std::string mode = argc > 2 ? argv[2] : "default";
+    if (mode == "public_exact") server.publish_bases();          // bases travel with the public key
     Paillier_HIP party;                  // Party::paillier
     party = server;                      // Server::send_key: public part only
-    if (argc > 2 && std::string(argv[2]).rfind("exact", 0) == 0)   // table-driven randomizer; the party (no p, q)
-        server.enc_flags = party.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;   // falls back to the default
+    if (mode.rfind("exact", 0) == 0 || mode == "public_exact")  // table-driven randomizer; the party (no p, q)
+        server.enc_flags = party.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;   // uses published bases, else the default
     const float g[5] = {0.4f, 1.2f, 0.1f, 0.8f, -0.7f}, h[5] = {0.6f, 1.4f, 0.2f, 1.0f, 0.8f};
     SyncArray<GHPair> gh(5), hist(5);
     for (int i = 0; i < 5; i++) { gh.host_data()[i] = GHPair(g[i], h[i]); hist.host_data()[i] = GHPair(g[i], h[i]); }
