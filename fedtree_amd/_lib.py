@@ -74,6 +74,9 @@ _PROTOS = {
     "fthe_decrypt_short_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_decrypt_short": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_add_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
+    "fthe_to_mont_dev": (_I, [_P, _P, _P, _SZ, _P]),
+    "fthe_from_mont_dev": (_I, [_P, _P, _P, _SZ, _P]),
+    "fthe_add_mont_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_add": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_scalar_mul_u64_dev": (_I, [_P, _P, _P, _U64, _SZ, _P]),
     "fthe_scalar_mul_u64": (_I, [_P, _P, _P, _U64, _SZ, _P]),

@@ -2089,10 +2089,17 @@ namespace {
 // Launch with an explicit (dynamic) program pointer.
 }  // namespace
 
-// out[i] = prod_j x[j*count + i] mod n^2.
-// X = x_0;  X <- x_j X R^-1 (j = 1..k-1);  X <- X (R^k mod n^2) R^-1  = prod x_j.
-extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, int kk, size_t count, uint32_t *out) {
-    if (!k || !c || kk <= 0 || kk > 64 || ((!x || !out) && count)) return FTHE_ERR_ARG;
+// Row products with a closing constant: out[i] = prod_j xs[j][i] * K R^-kk mod n^2 (X = x_0;
+// X <- x_j X R^-1; X <- X K R^-1), or without it (cst = nullptr): prod_j xs[j][i] R^-(kk-1).
+//   k-way product:  K = R^kk mod n^2       -> prod x_j
+//   to Montgomery:  kk = 1, K = R^2         -> x R
+//   from Montgomery: kk = 1, K = 1          -> x R^-1
+//   Montgomery add: kk = 2, no constant     -> (aR)(bR)R^-1 = (ab)R
+static int rowprod_impl(fthe_key *k, fthe_ctx *c, const uint32_t *const *xs, int kk, size_t count, uint32_t *out,
+                        const mpz_t cst) {
+    if (!k || !c || kk <= 0 || kk > 64 || (!out && count)) return FTHE_ERR_ARG;
+    for (int j = 0; j < kk; j++)
+        if (!xs[j] && count) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     const int base = nslots_for(k);               // inputs live after the standard slots
     const bool rowio = k->rowio && kk + 1 <= 16;
@@ -2101,18 +2108,19 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
                    : begin_call(c, k, count, Lc, base + kk, k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
-    Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
-    std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
+    std::vector<uint32_t> rl;
+    if (cst) rl = k->mn2.m.limbs(cst);
+    else rl.assign(1, 0u);
     Prog p;
     if (rowio) {
         p.loadw(0);
         for (int j = 1; j < kk; j++) p.mulw(j);
-        p.mul(SL_C0);
+        if (cst) p.mul(SL_C0);
         p.storew(kk); p.end();
     } else {
         p.loadx(base);
         for (int j = 1; j < kk; j++) p.mul(base + j);
-        p.mul(SL_C0);
+        if (cst) p.mul(SL_C0);
         p.storex(SL_OUTP); p.end();
     }
     std::vector<uint32_t> blob(p.w);
@@ -2123,25 +2131,53 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     if ((rc = upload_dyn_prog(c, tmp, ph, c->io[3]))) return rc;
     HIPOK(hipEventRecord(c->ev0, c->stream));
     const uint32_t *dconst = (const uint32_t *)c->io[3].p + prog_words;
-    hipLaunchKernelGGL(k_fill_const, Lc.grid(), dim3(256), 0, c->stream, dconst, Lc.slot(SL_C0), S, L);
+    if (cst) hipLaunchKernelGGL(k_fill_const, Lc.grid(), dim3(256), 0, c->stream, dconst, Lc.slot(SL_C0), S, L);
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
         if (rowio) {
             const void *rows[16];
-            for (int j = 0; j < kk; j++) rows[j] = x + ((size_t)j * count + off) * cw;
+            for (int j = 0; j < kk; j++) rows[j] = xs[j] + off * cw;
             rows[kk] = out + off * cw;
             if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2, rows, kk + 1))) return rc;
             continue;
         }
         for (int j = 0; j < kk; j++)
-            pack_rows(c->stream, x + ((size_t)j * count + off) * cw, cw,
-                               cnt, 0, Lc.slot(base + j), S, L, Lc.B);
+            pack_rows(c->stream, xs[j] + off * cw, cw, cnt, 0, Lc.slot(base + j), S, L, Lc.B);
         if ((rc = launch_dyn(Lc, c->io[3].p, p.montmuls, k->mn2))) return rc;
         unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L,
                            cnt, out + off * cw, cw, Lc.B);
     }
     return end_call(c, Lc);
+}
+
+// out[i] = prod_j x[j*count + i] mod n^2.
+extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, int kk, size_t count, uint32_t *out) {
+    if (!k || kk <= 0 || kk > 64 || (!x && count)) return FTHE_ERR_ARG;
+    std::vector<const uint32_t *> xs(kk);
+    for (int j = 0; j < kk; j++) xs[j] = x + (size_t)j * count * 2 * k->n_words;
+    Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
+    return rowprod_impl(k, c, xs.data(), kk, count, out, Rk);
+}
+
+// Montgomery-resident rows: x R mod n^2 in the same 2 n_words-word row layout.  Products of
+// resident rows need one Montgomery product instead of two (fthe_add_mont_dev).
+extern "C" int fthe_to_mont_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, uint32_t *out) {
+    if (!k) return FTHE_ERR_ARG;
+    Mpz R2; mpz_mul(R2, k->mn2.m.R, k->mn2.m.R); mpz_mod(R2, R2, k->n2);
+    return rowprod_impl(k, c, &x, 1, count, out, R2);
+}
+
+extern "C" int fthe_from_mont_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, uint32_t *out) {
+    if (!k) return FTHE_ERR_ARG;
+    Mpz one(1);
+    return rowprod_impl(k, c, &x, 1, count, out, one);
+}
+
+extern "C" int fthe_add_mont_dev(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count,
+                                 uint32_t *out) {
+    const uint32_t *xs[2] = {a, b};
+    return rowprod_impl(k, c, xs, 2, count, out, nullptr);
 }
 
 // Gathered K-way products: out[g] = prod_{j<K} x[idx[j*G + g]] mod n^2 (idx < 0 -> 1),

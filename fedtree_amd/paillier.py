@@ -407,6 +407,29 @@ class Paillier:
         return out_low
 
     @_stream_ordered
+    def to_mont_dev(self, x, out):
+        """Montgomery-resident rows: out = x R mod n^2 (fthe_to_mont_dev)."""
+        _lib.check(self.lib.fthe_to_mont_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()),
+                                             x.numel() // self._cw(), ctypes.c_void_p(out.data_ptr())), "to_mont_dev")
+        return out
+
+    @_stream_ordered
+    def from_mont_dev(self, x, out):
+        """Montgomery-resident rows back to ciphertexts: out = x R^-1 mod n^2."""
+        _lib.check(self.lib.fthe_from_mont_dev(self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()),
+                                               x.numel() // self._cw(), ctypes.c_void_p(out.data_ptr())),
+                   "from_mont_dev")
+        return out
+
+    @_stream_ordered
+    def add_mont_dev(self, a, b, out):
+        """Homomorphic add of Montgomery-resident rows, one product: (aR)(bR)R^-1 = (ab)R."""
+        _lib.check(self.lib.fthe_add_mont_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),
+                                              ctypes.c_void_p(b.data_ptr()), a.numel() // self._cw(),
+                                              ctypes.c_void_p(out.data_ptr())), "add_mont_dev")
+        return out
+
+    @_stream_ordered
     def add_dev(self, a, b, out):
         cnt = a.numel() // self._cw()
         _lib.check(self.lib.fthe_add_dev(self._key, self.dev.ctx, ctypes.c_void_p(a.data_ptr()),

@@ -224,6 +224,21 @@ int fthe_add_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t
 int fthe_add(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
              size_t count, uint32_t *out);
 
+/* ---- Montgomery-resident rows (device; not in the reference) ---------------
+ * A fresh add costs two Montgomery products (x y R^-1, then a product by R^2
+ * mod n^2).  Rows kept resident in Montgomery form, x R mod n^2 (same 2 n_words
+ * layout, canonical < n^2), multiply with one: (aR)(bR)R^-1 = (ab)R.  For
+ * device-resident chains of adds (tree sums, repeated merges): convert once,
+ * add many times, convert back; the converted-back rows are bit-identical to
+ * fthe_add_dev's.  Alias-safe.
+ * fthe_to_mont_dev    out = x R mod n^2   (one product)
+ * fthe_from_mont_dev  out = x R^-1 mod n^2 (one product): canonical ciphertexts
+ * fthe_add_mont_dev   out = a b R^-1 mod n^2 (one product): Mont(a) Mont(b) -> Mont(ab) */
+int fthe_to_mont_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count, uint32_t *out);
+int fthe_from_mont_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count, uint32_t *out);
+int fthe_add_mont_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
+                      size_t count, uint32_t *out);
+
 /* out[i] = a[i] * b[i]^(2^64-1) mod n^2: GHPair::operator- with both sides
  * encrypted (common.h:253-337 -- Paillier::add(a, Paillier::mul(b, (unsigned
  * long)-1))), fused into one program (all-ones addition chain).  The sibling
