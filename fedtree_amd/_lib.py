@@ -62,6 +62,7 @@ _PROTOS = {
     "fthe_key_fixed_base_exact": (_I, [_P, _P, _U64]),
     "fthe_key_fixed_base_exact_info": (_I, [_P, _I, _I, _P, _P]),
     "fthe_key_fixed_base_exact_bases": (_I, [_P]),
+    "fthe_next_prime": (_I, [_P, _I, _P, _I]),
     "fthe_key_public_bases": (_I, [_P, _U64, _P, _P]),
     "fthe_key_set_public_bases": (_I, [_P, _P, _P, _I]),
     "fthe_key_public_bases_info": (_I, [_P, _P, _P]),

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <functional>
 #include <memory>
@@ -754,6 +755,77 @@ extern "C" int fthe_key_generate_ex(fthe_ctx *ctx, int n_bits, uint64_t seed, in
     return rc;
 }
 
+// Smallest prime > start, the result of mpz_nextprime(start), searched on up to 16 host
+// threads: windows of 2^14 odd candidates sieved by the odd primes below 2^16, survivors
+// tested (mpz_probab_prime_p: BPSW + 1 Miller-Rabin round) in index order from a shared
+// counter; a thread stops once its index passes the smallest prime found, so every
+// smaller survivor has been tested when the threads join.  Prime generation is a
+// per-round cost in FedTree's vertical simulation (FLtrainer.cpp:556).
+static void next_prime_par(mpz_t out, const mpz_t start) {
+    static const std::vector<uint32_t> sieve_primes = [] {      // odd primes below 2^16
+        std::vector<uint8_t> c(65536, 0);
+        std::vector<uint32_t> v;
+        for (uint32_t i = 3; i < 65536; i += 2) {
+            if (c[i]) continue;
+            v.push_back(i);
+            for (uint32_t j = i * i; j < 65536; j += 2 * i) c[j] = 1;
+        }
+        return v;
+    }();
+    if (mpz_cmp_ui(start, 1u << 20) < 0) { mpz_nextprime(out, start); return; }
+    const int W = 1 << 14;
+    const unsigned nt = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    Mpz base;
+    mpz_add_ui(base, start, 1);
+    if (mpz_even_p(base)) mpz_add_ui(base, base, 1);           // odd candidates base + 2i
+    std::vector<uint8_t> comp(W);
+    std::vector<uint32_t> surv;
+    for (;;) {
+        std::fill(comp.begin(), comp.end(), 0);
+        for (uint32_t l : sieve_primes) {
+            const uint64_t r = mpz_fdiv_ui(base, l);           // base + 2i = 0 mod l  <=>  i = -r / 2 mod l
+            uint64_t i0 = (uint64_t)((l - r) % l) * ((l + 1) / 2) % l;
+            for (uint64_t i = i0; i < (uint64_t)W; i += l) comp[i] = 1;
+        }
+        surv.clear();
+        for (int i = 0; i < W; i++)
+            if (!comp[i]) surv.push_back((uint32_t)i);
+        std::atomic<size_t> next{0}, best{SIZE_MAX};
+        auto work = [&] {
+            Mpz cand;
+            for (;;) {
+                const size_t idx = next.fetch_add(1);
+                if (idx >= surv.size() || idx > best.load()) return;
+                mpz_add_ui(cand, base, 2u * surv[idx]);
+                if (mpz_probab_prime_p(cand, 25)) {
+                    size_t b = best.load();
+                    while (idx < b && !best.compare_exchange_weak(b, idx)) {}
+                    return;
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+        work();
+        for (auto &x : th) x.join();
+        if (best.load() != SIZE_MAX) {
+            mpz_add_ui(out, base, 2u * surv[best.load()]);
+            return;
+        }
+        mpz_add_ui(base, base, 2u * W);
+    }
+}
+
+extern "C" int fthe_next_prime(const uint32_t *start, int words, uint32_t *out, int out_words) {
+    if (!start || !out || words <= 0 || out_words <= 0) return FTHE_ERR_ARG;
+    Mpz s, r;
+    mpz_from_words(s, start, words);
+    next_prime_par(r, s);
+    if (r.bits() > (size_t)out_words * 32) return FTHE_ERR_ARG;
+    mpz_to_words(r, out, out_words);
+    return FTHE_OK;
+}
+
 extern "C" int fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out) {
     if (!ctx || !out || n_bits < 64 || (n_bits & 1)) return FTHE_ERR_ARG;
     gmp_randstate_t st; gmp_randinit_mt(st);
@@ -766,8 +838,8 @@ extern "C" int fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_
     for (int tries = 0; tries < 64 && rc == FTHE_ERR_KEY; tries++) {
         Mpz p, q;
         // top two bits set -> p*q has exactly n_bits bits (GenPrimePair, paillier.cpp:51-61)
-        mpz_urandomb(p, st, hb); mpz_setbit(p, hb - 1); mpz_setbit(p, hb - 2); mpz_nextprime(p, p);
-        mpz_urandomb(q, st, hb); mpz_setbit(q, hb - 1); mpz_setbit(q, hb - 2); mpz_nextprime(q, q);
+        mpz_urandomb(p, st, hb); mpz_setbit(p, hb - 1); mpz_setbit(p, hb - 2); next_prime_par(p, p);
+        mpz_urandomb(q, st, hb); mpz_setbit(q, hb - 1); mpz_setbit(q, hb - 2); next_prime_par(q, q);
         if (p.bits() != (size_t)hb || q.bits() != (size_t)hb) continue;
         rc = key_from_pq(ctx, p, q, out);
     }

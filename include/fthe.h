@@ -82,6 +82,10 @@ int  fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out)
  *                        draws unconstrained random primes); opt-in. */
 #define FTHE_KEYGEN_KNOWN_ORDER 1
 int  fthe_key_generate_ex(fthe_ctx *ctx, int n_bits, uint64_t seed, int flags, fthe_key **out);
+/* fthe_next_prime        host only (no device): the smallest prime > start (words
+ *                        little-endian u32) into out, as mpz_nextprime; the keygen's prime
+ *                        search, sieved and tested on up to 16 host threads. */
+int  fthe_next_prime(const uint32_t *start, int words, uint32_t *out, int out_words);
 int  fthe_key_from_primes(fthe_ctx *ctx, const uint32_t *p, const uint32_t *q,
                           int pq_words, fthe_key **out);
 int  fthe_key_from_n(fthe_ctx *ctx, const uint32_t *n, int n_words, fthe_key **out);
