@@ -586,11 +586,12 @@ class GHPairs:
         self.encrypted = True
         return self
 
-    def homo_decrypt(self, pl):
-        """GHPair::homo_decrypt (common.h:136-146): g = (float)(long)dec / 1e6."""
+    def homo_decrypt(self, pl, short=False):
+        """GHPair::homo_decrypt (common.h:136-146): g = (float)(long)dec / 1e6.
+        short: plaintexts known < p (codec values and their sums): p half of the CRT only."""
         if not self.encrypted:
             return self
-        low = pl.decrypt_u64(np.concatenate([self.g_enc, self.h_enc]))
+        low = pl.decrypt_u64(np.concatenate([self.g_enc, self.h_enc]), short=short)
         self.g = decode_fixed(low[:len(self)])
         self.h = decode_fixed(low[len(self):])
         self.encrypted = False
@@ -675,9 +676,9 @@ class HEServer:
         """server.h:113-135."""
         return raw.homo_encrypt(self.paillier, seed=seed, fixed_base_exact=fixed_base_exact)
 
-    def decrypt_gh_pairs(self, encrypted):
-        """server.h:80-111."""
-        return encrypted.homo_decrypt(self.paillier)
+    def decrypt_gh_pairs(self, encrypted, short=False):
+        """server.h:80-111.  short: see GHPairs.homo_decrypt (opt-in, ~2x)."""
+        return encrypted.homo_decrypt(self.paillier, short=short)
 
     def decrypt_gh(self, gh):
         """server.h:69-78 (single pair, as a batch of one)."""

@@ -29,6 +29,7 @@ int main(int argc, char **argv) {
         party.add(hist.host_data()[i].g_enc, hist.host_data()[i].g_enc, gh.host_data()[i].g_enc);
         party.add(hist.host_data()[i].h_enc, hist.host_data()[i].h_enc, gh.host_data()[i].h_enc);
     }
+    if (mode == "short") server.dec_short = true;                // p half of the CRT only
     server.decrypt(hist);                                        // decrypt_gh_pairs
     int bad = 0;
     for (int i = 0; i < 5; i++) {

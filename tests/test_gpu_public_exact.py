@@ -182,6 +182,9 @@ def test_public_exact_histogram_flow(dev):
     total = (hists[0] + hists[1]).homo_decrypt(srv.paillier)
     want_g = (np.round(g[0] * 1e6).astype(np.int64) + np.round(g[1] * 1e6).astype(np.int64)) / 1e6
     assert np.allclose(total.g, want_g, atol=2e-6)
+    # the short decrypt (p half only: plaintexts < p) decodes the same sums
+    short = srv.decrypt_gh_pairs(hists[0] + hists[1], short=True)
+    assert np.array_equal(short.g, total.g) and np.array_equal(short.h, total.h)
     # without published bases the flag falls back to the default public path
     plain = HEParty()
     srv.send_key(plain)
