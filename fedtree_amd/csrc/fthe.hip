@@ -16,7 +16,9 @@
 #include <atomic>
 #include <cmath>
 #include <functional>
+#include <map>
 #include <memory>
+#include <string>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -192,7 +194,7 @@ struct fthe_key {
         if (d_pqwords) (void)hipFree(d_pqwords);
         for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) (void)hipFree(p);
         for (uint32_t *p : {xb.d_tab[0], xb.d_tab[1], xb.d_prog}) if (p) (void)hipFree(p);
-        for (uint32_t *p : {pb.d_tab, pb.d_prog}) if (p) (void)hipFree(p);
+        if (pb.d_prog) (void)hipFree(pb.d_prog);           // pb.tab: shared, freed by its last key
     }
     // constant handles
     int add_const(const std::vector<uint32_t> &limbs) {
@@ -257,10 +259,17 @@ struct fthe_key {
     // ---- public exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT, public form) ----
     // Bases hs_i = t_i^n mod n^2 published by the key holder, <t_1 .. t_nb> = Z_n^*;
     // r^n = prod hs_i^y_i with y_i uniform below 2^(16 nwin) >= n 2^64.
+    // The tables depend on (device, n, bases) only and are shared between the keys that hold
+    // them: in FedTree's simulation every party has its own copy of the public key.
+    struct SharedTab {
+        uint32_t *d = nullptr;
+        ~SharedTab() { if (d) (void)hipFree(d); }
+    };
     struct PublicBase {
         bool ready = false, rows = false;
         int nb = 0, nwin = 0, ew = 0;     // bases, 16-bit windows per exponent, words per entry
         Mpz hs[3];
+        std::shared_ptr<SharedTab> tab;
         uint32_t *d_tab = nullptr, *d_prog = nullptr;
         double mm = 0;
     } pb;
@@ -1838,15 +1847,42 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
     if (!k->pub_ok || (k->sn2.lanes == 4 && !k->rowio)) return FTHE_ERR_UNSUPPORTED;
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipDeviceSynchronize());                       // no call may still read the old tables
-    for (uint32_t **p : {&B.d_tab, &B.d_prog})
-        if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (B.d_prog) { (void)hipFree(B.d_prog); B.d_prog = nullptr; }
+    B.tab.reset();
+    B.d_tab = nullptr;
     B.ready = false;
     B.nb = nb;
     B.nwin = (int)((k->n_bits + 64 + 15) / 16);
     B.rows = k->sn2.lanes == 4;
     for (int i = 0; i < nb; i++) mpz_set(B.hs[i], hs[i]);
+    // process-wide cache: (device, n, hs_1 .. hs_nb) -> tables
+    static std::mutex cache_mu;
+    static std::map<std::string, std::weak_ptr<fthe_key::SharedTab>> cache;
+    std::string id = std::to_string(c->device) + ":";
+    {
+        const int cw = 2 * k->n_words;
+        std::vector<uint32_t> w((size_t)(nb + 1) * cw, 0);
+        mpz_to_words(k->n, w.data(), cw);
+        for (int i = 0; i < nb; i++) mpz_to_words(B.hs[i], w.data() + (size_t)(i + 1) * cw, cw);
+        id.append((const char *)w.data(), w.size() * 4);
+    }
     int rc;
-    if ((rc = pub_tables(k, c, B.hs, nb, B.nwin, true, &B.d_tab, &B.ew))) return rc;
+    {
+        std::lock_guard<std::mutex> lk(cache_mu);
+        auto it = cache.find(id);
+        if (it != cache.end()) B.tab = it->second.lock();
+        if (B.tab) {
+            B.ew = B.rows ? 2 * k->n_words : 4 * ((k->mn2.m.S + 3) / 4);
+        } else {
+            auto t = std::make_shared<fthe_key::SharedTab>();
+            if ((rc = pub_tables(k, c, B.hs, nb, B.nwin, true, &t->d, &B.ew))) return rc;
+            B.tab = t;
+            cache[id] = t;
+            for (auto i = cache.begin(); i != cache.end();)      // drop entries whose tables are gone
+                i = i->second.expired() ? cache.erase(i) : std::next(i);
+        }
+    }
+    B.d_tab = B.tab->d;
     Prog e;                                              // X = prod_j entry(j, digit j), then (1 + m n) X
     e.loadgd16(0);
     for (int j = 1; j < nb * B.nwin; j++) e.mulgd16(j);

@@ -216,3 +216,39 @@ def test_public_exact_refusals(dev):
         pub.encrypt_u64(np.arange(2, dtype=np.uint64), r=np.zeros((2, 5), np.uint32), fixed_base_exact=True)
     c = pub.encrypt_u64(np.arange(4, dtype=np.uint64), seed=1, fixed_base_exact=True)
     assert np.array_equal(server.decrypt_u64(c), np.arange(4, dtype=np.uint64))
+
+
+def test_public_exact_tables_shared_between_copies(dev):
+    """Every party holds its own copy of the public key (party.h:181-185); copies with the same
+    (device, n, bases) share one set of tables (13 GB at P-2048) instead of building their own."""
+    import gc
+
+    import torch
+    from fedtree_amd.paillier import Paillier
+    p, q = golden_key(load_golden("ref_gmp_L4096.json"))
+    server = Paillier.from_primes(p, q, dev)
+    hs = server.public_bases(seed=21)
+    free0 = torch.cuda.mem_get_info(0)[0]
+    a = server.public(bases=hs)
+    dev.sync()
+    free1 = torch.cuda.mem_get_info(0)[0]
+    assert free0 - free1 > 12 << 30                           # the first copy builds the tables
+    b = server.public(bases=hs)
+    c2 = server.public(bases=hs)
+    dev.sync()
+    free2 = torch.cuda.mem_get_info(0)[0]
+    assert free1 - free2 < 1 << 30                            # later copies share them
+    m = np.arange(1000, dtype=np.uint64)
+    y = [(3, 5, 7)] * 4
+    ca = a.encrypt_u64(m[:4], r=y, fixed_base_exact=True)
+    del a
+    gc.collect()
+    assert np.array_equal(b.encrypt_u64(m[:4], r=y, fixed_base_exact=True), ca)
+    assert np.array_equal(server.decrypt_u64(c2.encrypt_u64(m, seed=4, fixed_base_exact=True)), m)
+    other = server.public(bases=server.public_bases(seed=22))  # other bases: own tables
+    dev.sync()
+    assert torch.cuda.mem_get_info(0)[0] < free2 - (12 << 30)
+    del b, c2, other
+    gc.collect()
+    dev.sync()
+    assert torch.cuda.mem_get_info(0)[0] > free0 - (2 << 30)  # freed with the last copy
