@@ -212,7 +212,7 @@ def main():
                             "per lane per exponentiation), 2.2% of HBM bandwidth in a VALU-bound kernel")
 
     secondary = {}
-    if rank == 0 and not a.no_secondary:
+    if rank == 0 and world == 1 and not a.no_secondary:      # N=1 runs only: scaling runs stay lean
         # CRT decrypt of 1M ciphertexts (config 3's decrypt half), device-resident
         nd = min(2 * P, 1 << 20)
         low = torch.empty(nd, dtype=torch.int64, device=f"cuda:{local}")
