@@ -663,12 +663,13 @@ class HEServer:
     def homo_init(self, keylength, seed=0):
         """server.h:58-67 (NTL build: keygen(keylength))."""
         self.paillier.keygen(keylength, seed)
+        self._bases = None                      # published bases belong to the previous key
 
     def send_key(self, party, bases=False):
         """server.h:53-55: party.paillier = paillier (public part only).
         bases: also publish checked fixed-base bases (Paillier.public_bases) for the
         parties' FTHE_ENC_FIXED_BASE_EXACT histogram encryption."""
-        if bases and not hasattr(self, "_bases"):
+        if bases and getattr(self, "_bases", None) is None:
             self._bases = self.paillier.public_bases()
         party.paillier = self.paillier.public(self._bases if bases else None)
 
