@@ -28,15 +28,20 @@ class ShardedPaillier:
     """A Paillier key replicated on several devices; batch calls are split
     across them and run concurrently (ctypes releases the GIL in the engine)."""
 
-    def __init__(self, key, devices):
+    def __init__(self, key, devices, bases=None):
+        """bases: published fixed-base bases (Paillier.public_bases) for public-key copies'
+        encrypt_u64(fixed_base_exact=True); each device builds its own tables."""
         from .paillier import Device, Paillier
         self.devices = [Device(d) if not isinstance(d, Device) else d for d in devices]
         self.keys = []
         for dev in self.devices:
             if key.has_private:
-                self.keys.append(Paillier.from_primes(key.p, key.q, dev))
+                k = Paillier.from_primes(key.p, key.q, dev)
             else:
-                self.keys.append(Paillier.from_public(key.modulus, dev))
+                k = Paillier.from_public(key.modulus, dev)
+            if bases is not None:
+                k.set_public_bases(bases)
+            self.keys.append(k)
         self.n_words = key.n_words
 
     def _run(self, n, fn):
@@ -61,18 +66,26 @@ class ShardedPaillier:
                 raise e
         return out
 
-    def encrypt_u64(self, m, seed=0):
+    def encrypt_u64(self, m, seed=0, **modes):
+        """modes: public / fixed_base / fixed_base_exact, as Paillier.encrypt_u64."""
         m = np.ascontiguousarray(m, dtype=np.uint64)
         # distinct per-shard streams; seed 0 keeps the /dev/urandom default
-        parts = self._run(len(m), lambda k, lo, hi: k.encrypt_u64(m[lo:hi], seed=(seed * 1315423911 + lo) if seed else 0))
+        parts = self._run(len(m), lambda k, lo, hi: k.encrypt_u64(
+            m[lo:hi], seed=(seed * 1315423911 + lo) if seed else 0, **modes))
         return np.concatenate(parts) if parts else np.zeros((0, 2 * self.n_words), np.uint32)
 
-    def decrypt_u64(self, c):
+    def decrypt_u64(self, c, short=False):
         c = np.ascontiguousarray(c, dtype=np.uint32)
-        return np.concatenate(self._run(len(c), lambda k, lo, hi: k.decrypt_u64(c[lo:hi])))
+        return np.concatenate(self._run(len(c), lambda k, lo, hi: k.decrypt_u64(c[lo:hi], short=short)))
 
     def add_batch(self, a, b):
         return np.concatenate(self._run(len(a), lambda k, lo, hi: k.add_batch(a[lo:hi], b[lo:hi])))
+
+    def sub_batch(self, a, b):
+        return np.concatenate(self._run(len(a), lambda k, lo, hi: k.sub_batch(a[lo:hi], b[lo:hi])))
+
+    def scalar_mul(self, x, k64):
+        return np.concatenate(self._run(len(x), lambda k, lo, hi: k.scalar_mul(x[lo:hi], k64)))
 
     def reduce_kway(self, x):
         return np.concatenate(self._run(x.shape[1], lambda k, lo, hi: k.reduce_kway(x[:, lo:hi])))

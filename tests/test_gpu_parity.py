@@ -309,6 +309,14 @@ def test_sharded_two_contexts(dev, coracle):
     assert np.array_equal(pl.decrypt_u64(c), m)
     s = sp.add_batch(c, c[::-1].copy())
     assert np.array_equal(s, pl.add_batch(c, c[::-1].copy()))
+    assert np.array_equal(sp.sub_batch(c[:500], c[500:1000]), pl.sub_batch(c[:500], c[500:1000]))
+    assert np.array_equal(sp.scalar_mul(c[:300], 12345), pl.scalar_mul(c[:300], 12345))
+    assert np.array_equal(sp.decrypt_u64(c, short=True), m)
+    # parties: public-key copies with published bases on every context
+    pub = ShardedPaillier(pl.public(), [Device(0), Device(0)], bases=pl.public_bases(seed=2))
+    cp = pub.encrypt_u64(m, seed=6, fixed_base_exact=True)
+    assert np.array_equal(pl.decrypt_u64(cp), m)
+    assert np.array_equal(pub.encrypt_u64(m, seed=6, fixed_base_exact=True), cp)
 
 
 # ---------------------------------------------------------------- segmented product / histogram
