@@ -496,9 +496,12 @@ class Paillier:
             ctypes.c_void_p(out.data_ptr())), "histogram_dev")
         return out
 
-    def encrypt_words(self, m, r=None, seed=0, public=False):
+    def encrypt_words(self, m, r=None, seed=0, public=False, fixed_base_exact=False):
         """General plaintexts (Paillier::encrypt(const ZZ&), paillier.cpp:122-139): m is a list of
-        ints (any size up to n_words words) or a (count, words) uint32 array; r as encrypt_u64."""
+        ints (any size up to n_words words) or a (count, words) uint32 array; r as encrypt_u64
+        (fixed_base_exact: r = None, the device draws the exponents)."""
+        if fixed_base_exact and r is not None:
+            raise ValueError("encrypt_words: injected exponents go through encrypt_u64")
         if not isinstance(m, np.ndarray):
             m = np.stack([_words(int(x), self.n_words) for x in m]) if len(m) else np.zeros((0, self.n_words), np.uint32)
         m = np.ascontiguousarray(m, dtype=np.uint32)
@@ -510,7 +513,7 @@ class Paillier:
             rw = np.ascontiguousarray(rw, dtype=np.uint32).reshape(cnt, -1)
         _lib.check(self.lib.fthe_encrypt_words(self._key, self.dev.ctx, _ptr(m), mw, cnt, _ptr(rw),
                                                rw.shape[1] if rw is not None else 0, int(seed), _ptr(out),
-                                               self._flags(public, False)), "encrypt_words")
+                                               self._flags(public, False, fixed_base_exact)), "encrypt_words")
         return out
 
     # ---- reference single-value signatures (batch of one) ------------------

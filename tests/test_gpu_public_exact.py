@@ -192,6 +192,21 @@ def test_public_exact_histogram_flow(dev):
     assert np.allclose(enc.homo_decrypt(srv.paillier).g, np.round(g[0] * 1e6) / 1e6, atol=2e-6)
 
 
+def test_public_exact_general_plaintexts(dev):
+    """Paillier::encrypt(const ZZ&) plaintexts (any size < n) through the published-bases mode."""
+    from fedtree_amd.paillier import Paillier
+    p, q = golden_key(load_golden("ref_gmp_L4096.json"))
+    n = p * q
+    server = Paillier.from_primes(p, q, dev)
+    party = server.public(bases=server.public_bases(seed=5))
+    rng = np.random.default_rng(41)
+    ms = [0, 1, 2**64, 2**200 + 7, n - 1] + [int.from_bytes(rng.bytes(255), "little") for _ in range(11)]
+    c = party.encrypt_words(ms, seed=3, fixed_base_exact=True)
+    _, full = server.decrypt_u64(c, full=True)
+    assert [pyoracle.from_words(x) for x in full] == [x % n for x in ms]
+    assert len({bytes(x) for x in c}) == len(ms)
+
+
 def test_public_exact_refusals(dev):
     from fedtree_amd.paillier import Paillier
     p, q = golden_key(load_golden("ref_gmp_L2048.json"))
