@@ -3,7 +3,7 @@
 // decrypt_gh per node, :758-764; the distributed decode loops, distributed_server.cpp:1427):
 // T host threads share ONE key object, each on its own engine context (thread_ctx),
 // issuing small batch and single-element calls concurrently.  Every result is checked.
-//   concurrency_test [bits] [threads] [iters] [default|exact]
+//   concurrency_test [bits] [threads] [iters] [default|exact|public_exact]
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -20,9 +20,12 @@ int main(int argc, char **argv) {
     int iters = argc > 3 ? std::atoi(argv[3]) : 24;
     Paillier_HIP server;
     server.keygen(bits);
-    if (argc > 4 && std::string(argv[4]) == "exact") server.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;
+    const std::string mode = argc > 4 ? argv[4] : "default";
+    if (mode == "exact") server.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;
+    if (mode == "public_exact") server.publish_bases();  // the party encrypts from the published bases
     Paillier_HIP party;
     party = server;                                   // public part, shared by the party threads
+    if (mode == "public_exact") party.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;
     std::atomic<int> bad{0}, done{0};
     std::vector<std::thread> th;
     for (int t = 0; t < T; t++)

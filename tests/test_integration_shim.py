@@ -35,7 +35,7 @@ def test_shim_runs_server_party_flow(tmp_path, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["default", "exact"])
+@pytest.mark.parametrize("mode", ["default", "exact", "public_exact"])
 def test_shim_concurrent_threads_share_one_key(tmp_path, mode):
     """16 host threads, one shared key, a context per thread (the OpenMP call pattern)."""
     exe = _build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp")
