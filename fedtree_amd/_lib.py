@@ -63,8 +63,8 @@ _PROTOS = {
     "fthe_key_fixed_base_exact_info": (_I, [_P, _I, _I, _P, _P]),
     "fthe_key_fixed_base_exact_bases": (_I, [_P]),
     "fthe_next_prime": (_I, [_P, _I, _P, _I]),
-    "fthe_key_public_bases": (_I, [_P, _U64, _P, _P]),
-    "fthe_key_set_public_bases": (_I, [_P, _P, _P, _I]),
+    "fthe_key_public_bases": (_I, [_P, _U64, _P, _P, _P]),
+    "fthe_key_set_public_bases": (_I, [_P, _P, _P, _I, _P]),
     "fthe_key_public_bases_info": (_I, [_P, _P, _P]),
     "fthe_encrypt_u64_dev": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_encrypt_u64": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),

@@ -267,7 +267,9 @@ struct fthe_key {
     };
     struct PublicBase {
         bool ready = false, rows = false;
-        int nb = 0, nwin = 0, ew = 0;     // bases, 16-bit windows per exponent, words per entry
+        int nb = 0, ew = 0;               // bases, words per table entry
+        int nwin[3] = {0, 0, 0};          // 16-bit windows of each base's exponent
+        int wtot = 0;                     // windows of all bases
         Mpz hs[3];
         std::shared_ptr<SharedTab> tab;
         uint32_t *d_tab = nullptr, *d_prog = nullptr;
@@ -1379,10 +1381,11 @@ int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32
     return end_call(c, Lc);
 }
 
-// Public-form (mod n^2) fixed-base tables for bases hs[0 .. nb), nwin16 16-bit windows each,
+// Public-form (mod n^2) fixed-base tables for bases hs[0 .. nb), nwin16[b] 16-bit windows for base b,
 // base after base: one-lane n^2 kernels store radix-2^B limb entries, the four-lane kernel
 // canonical 2 n_words-word rows (k->sn2.lanes == 4).  wide = false keeps 8-bit windows.
-int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, int nwin16, bool wide, uint32_t **d_tab, int *ew) {
+int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *nwin16, bool wide, uint32_t **d_tab,
+               int *ew) {
     const MontMod &M = k->mn2.m;
     const bool rows = k->sn2.lanes == 4;
     const int cw = 2 * k->n_words;
@@ -1391,12 +1394,12 @@ int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, int nwin16, bool
     for (int b = 0; b < nb; b++) {
         std::vector<uint32_t> tb;
         if (rows)
-            tb = fb_table(hs[b], k->n2, 2 * nwin16, cw, [&M, cw](const mpz_t x, uint32_t *dst) {
+            tb = fb_table(hs[b], k->n2, 2 * nwin16[b], cw, [&M, cw](const mpz_t x, uint32_t *dst) {
                 Mpz t; mpz_mul(t, x, M.R); mpz_mod(t, t, M.N);
                 mpz_to_words(t, dst, cw);
             });
         else
-            tb = fb_table(hs[b], k->n2, 2 * nwin16, *ew, fb_store_limbs(M));
+            tb = fb_table(hs[b], k->n2, 2 * nwin16[b], *ew, fb_store_limbs(M));
         if (nb == 1) tab.swap(tb);
         else tab.insert(tab.end(), tb.begin(), tb.end());
     }
@@ -1404,7 +1407,9 @@ int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, int nwin16, bool
     uint32_t *d8 = nullptr;
     if ((rc = fb_upload(tab, &d8))) return rc;
     if (!wide) { *d_tab = d8; return FTHE_OK; }
-    rc = fb_widen(k, c, k->mn2, k->sn2, d8, nb * nwin16, *ew, rows, d_tab);
+    int total = 0;
+    for (int b = 0; b < nb; b++) total += nwin16[b];
+    rc = fb_widen(k, c, k->mn2, k->sn2, d8, total, *ew, rows, d_tab);
     (void)hipFree(d8);
     return rc;
 }
@@ -1445,7 +1450,7 @@ int fb_build(fthe_key *k, fthe_ctx *c, const mpz_t h) {
         const int nwin16 = (k->n_bits + 64 + 15) / 16;          // alpha: n_bits + 64 bits
         F.nwin_pub = wide ? nwin16 : 2 * nwin16;
         F.pub_rows = k->sn2.lanes == 4;
-        if ((rc = pub_tables(k, c, &F.hs, 1, nwin16, wide, &F.d_tab_pub, &F.ew_pub))) return rc;
+        if ((rc = pub_tables(k, c, &F.hs, 1, &nwin16, wide, &F.d_tab_pub, &F.ew_pub))) return rc;
         Prog e;
         expo(e, F.nwin_pub);
         e.storex(SL_SAVED);
@@ -1842,7 +1847,7 @@ std::vector<Mpz> pb_primes(const fthe_key *k) {
     return ls;
 }
 
-int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
+int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *ebits) {
     fthe_key::PublicBase &B = k->pb;
     if (!k->pub_ok || (k->sn2.lanes == 4 && !k->rowio)) return FTHE_ERR_UNSUPPORTED;
     HIPOK(hipSetDevice(c->device));
@@ -1852,7 +1857,11 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
     B.d_tab = nullptr;
     B.ready = false;
     B.nb = nb;
-    B.nwin = (int)((k->n_bits + 64 + 15) / 16);
+    B.wtot = 0;
+    for (int i = 0; i < nb; i++) {
+        B.nwin[i] = ebits ? ebits[i] / 16 : (k->n_bits + 64 + 15) / 16;
+        B.wtot += B.nwin[i];
+    }
     B.rows = k->sn2.lanes == 4;
     for (int i = 0; i < nb; i++) mpz_set(B.hs[i], hs[i]);
     // process-wide cache: (device, n, hs_1 .. hs_nb) -> tables
@@ -1865,6 +1874,7 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
         mpz_to_words(k->n, w.data(), cw);
         for (int i = 0; i < nb; i++) mpz_to_words(B.hs[i], w.data() + (size_t)(i + 1) * cw, cw);
         id.append((const char *)w.data(), w.size() * 4);
+        id.append((const char *)B.nwin, sizeof(B.nwin));
     }
     int rc;
     {
@@ -1885,7 +1895,7 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
     B.d_tab = B.tab->d;
     Prog e;                                              // X = prod_j entry(j, digit j), then (1 + m n) X
     e.loadgd16(0);
-    for (int j = 1; j < nb * B.nwin; j++) e.mulgd16(j);
+    for (int j = 1; j < B.wtot; j++) e.mulgd16(j);
     e.storex(SL_SAVED);
     e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);
     if (B.rows) e.storew(2); else e.storex(SL_OUTP);
@@ -1898,7 +1908,41 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb) {
 
 }  // namespace
 
-extern "C" int fthe_key_public_bases(fthe_key *k, uint64_t seed, uint32_t *hs, int *nb) {
+// Known-order keys, g = gcd(p-1, q-1) < 2^64: t_1 a primitive root mod p and mod q (order
+// lambda = lcm(p-1, q-1), verified at every factor) and t_2 with t_2 mod p, q in different
+// classes of Z_n^* / <t_1> = Z_g (rank 2 with t_1 at every l | g).  Then r = t_1^y_1 t_2^y_2
+// is uniform once y_1 is uniform mod lambda and y_2 mod g: y_2 needs 128 bits, not n + 64.
+static bool pb_pick_short(fthe_key *k, gmp_randstate_t st, Mpz t[2]) {
+    Mpz gg, pm1, qm1, e, x, span, gc;
+    mpz_sub_ui(pm1, k->p, 1); mpz_sub_ui(qm1, k->q, 1);
+    mpz_gcd(gg, pm1, qm1);
+    if (mpz_sizeinbase(gg, 2) > 64) return false;
+    std::vector<Mpz> lg;                                  // primes dividing g (all recorded factors)
+    for (const Mpz &l : k->pm1_factors)
+        if (mpz_divisible_p(gg, l)) lg.push_back(l);
+    mpz_sub_ui(span, k->n, 3);
+    auto primitive = [&](const mpz_t t, const mpz_t P, const mpz_t Pm1, const std::vector<Mpz> &fs) {
+        for (const Mpz &l : fs) {
+            mpz_divexact(e, Pm1, l);
+            mpz_powm(x, t, e, P);
+            if (mpz_cmp_ui(x, 1) == 0) return false;
+        }
+        return true;
+    };
+    for (;;) {
+        mpz_urandomm(t[0], st, span); mpz_add_ui(t[0], t[0], 2);
+        mpz_gcd(gc, t[0], k->n);
+        if (mpz_cmp_ui(gc, 1) == 0 && primitive(t[0], k->p, pm1, k->pm1_factors) &&
+            primitive(t[0], k->q, qm1, k->qm1_factors)) break;
+    }
+    for (;;) {
+        mpz_urandomm(t[1], st, span); mpz_add_ui(t[1], t[1], 2);
+        mpz_gcd(gc, t[1], k->n);
+        if (mpz_cmp_ui(gc, 1) == 0 && pb_generates(t, 2, k->p, k->q, lg)) return true;
+    }
+}
+
+extern "C" int fthe_key_public_bases(fthe_key *k, uint64_t seed, uint32_t *hs, int *nb, int *exp_bits) {
     if (!k) return FTHE_ERR_ARG;
     if (!k->priv) return FTHE_ERR_NOPRIV;
     const int nbases = k->order_known ? 2 : 3;
@@ -1911,28 +1955,35 @@ extern "C" int fthe_key_public_bases(fthe_key *k, uint64_t seed, uint32_t *hs, i
     mpz_mul_2exp(sd, sd, 64);
     mpz_add_ui(sd, sd, seed ? 0x5055424241534553ull : urandom64());
     gmp_randseed(st, sd);
-    const std::vector<Mpz> ls = pb_primes(k);
     Mpz t[3], span, g;
-    mpz_sub_ui(span, k->n, 3);
-    for (;;) {
-        bool unit = true;
-        for (int i = 0; i < nbases; i++) {
-            mpz_urandomm(t[i], st, span); mpz_add_ui(t[i], t[i], 2);
-            mpz_gcd(g, t[i], k->n);
-            unit = unit && mpz_cmp_ui(g, 1) == 0;
+    const int full = 16 * ((k->n_bits + 64 + 15) / 16);
+    int eb[3] = {full, full, full};
+    if (k->order_known && pb_pick_short(k, st, t)) {
+        eb[1] = 128;
+    } else {
+        const std::vector<Mpz> ls = pb_primes(k);
+        mpz_sub_ui(span, k->n, 3);
+        for (;;) {
+            bool unit = true;
+            for (int i = 0; i < nbases; i++) {
+                mpz_urandomm(t[i], st, span); mpz_add_ui(t[i], t[i], 2);
+                mpz_gcd(g, t[i], k->n);
+                unit = unit && mpz_cmp_ui(g, 1) == 0;
+            }
+            if (unit && pb_generates(t, nbases, k->p, k->q, ls)) break;
         }
-        if (unit && pb_generates(t, nbases, k->p, k->q, ls)) break;
     }
     gmp_randclear(st);
     const int cw = 2 * k->n_words;
     for (int i = 0; i < nbases; i++) {
         mpz_powm(g, t[i], k->n, k->n2);
         mpz_to_words(g, hs + (size_t)i * cw, cw);
+        if (exp_bits) exp_bits[i] = eb[i];
     }
     return FTHE_OK;
 }
 
-extern "C" int fthe_key_set_public_bases(fthe_key *k, fthe_ctx *c, const uint32_t *hs, int nb) {
+extern "C" int fthe_key_set_public_bases(fthe_key *k, fthe_ctx *c, const uint32_t *hs, int nb, const int *exp_bits) {
     if (!k || !c || !hs || k->device != c->device || nb < 1 || nb > 3) return FTHE_ERR_ARG;
     const int cw = 2 * k->n_words;
     Mpz h[3], g;
@@ -1940,9 +1991,11 @@ extern "C" int fthe_key_set_public_bases(fthe_key *k, fthe_ctx *c, const uint32_
         mpz_from_words(h[i], hs + (size_t)i * cw, cw);
         mpz_gcd(g, h[i], k->n);
         if (mpz_sgn(h[i]) <= 0 || mpz_cmp(h[i], k->n2) >= 0 || mpz_cmp_ui(g, 1) != 0) return FTHE_ERR_ARG;
+        if (exp_bits && (exp_bits[i] < 16 || exp_bits[i] % 16 || exp_bits[i] > 16 * ((k->n_bits + 64 + 15) / 16)))
+            return FTHE_ERR_ARG;
     }
     std::lock_guard<std::mutex> lk(k->fb_mu);
-    return pb_build(k, c, h, nb);
+    return pb_build(k, c, h, nb, exp_bits);
 }
 
 extern "C" int fthe_key_public_bases_info(fthe_key *k, int *nb, int *exp_words) {
@@ -1950,20 +2003,26 @@ extern "C" int fthe_key_public_bases_info(fthe_key *k, int *nb, int *exp_words) 
     std::lock_guard<std::mutex> lk(k->fb_mu);
     if (!k->pb.ready) return FTHE_ERR_ARG;
     if (nb) *nb = k->pb.nb;
-    if (exp_words) *exp_words = (k->pb.nwin + 1) / 2;
+    if (exp_words)
+        for (int i = 0; i < k->pb.nb; i++) exp_words[i] = (k->pb.nwin[i] + 1) / 2;
     return FTHE_OK;
 }
 
 static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y, int y_words,
                            uint64_t rng_seed, uint32_t *out, HostPipe *pipe) {
     const fthe_key::PublicBase &B = k->pb;
-    const int nb = B.nb, ewd = (B.nwin + 1) / 2;          // words per injected exponent
-    if (y && y_words != nb * ewd) return FTHE_ERR_ARG;
+    const int nb = B.nb;
+    int ewd[3], ewo[3], wo[3], ytot = 0, wsum = 0;        // words per injected exponent, their offsets
+    for (int b = 0; b < nb; b++) {
+        ewd[b] = (B.nwin[b] + 1) / 2; ewo[b] = ytot; ytot += ewd[b];
+        wo[b] = wsum; wsum += B.nwin[b];                  // first window of base b
+    }
+    if (y && y_words != ytot) return FTHE_ERR_ARG;
     Launch Lc;
     int rc;
     if ((rc = begin_call(c, k, count, Lc, nslots_for(k), k->sn2))) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
-    const size_t exp_bytes = (size_t)B.nwin * L * 2, dig_bytes = nb * exp_bytes;
+    const size_t dig_bytes = (size_t)B.wtot * L * 2;     // u16 digits [window][L], base after base
     if ((rc = c->scratch.ensure(dig_bytes))) return rc;
     uint8_t *dig = (uint8_t *)c->scratch.p;
     RngKey rk{};
@@ -1978,15 +2037,15 @@ static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
         Lc.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         for (int b = 0; b < nb; b++) {
-            uint8_t *dst = dig + b * exp_bytes;
+            uint8_t *dst = dig + (size_t)wo[b] * L * 2;
             if (y) {
-                hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, y + off * y_words + (size_t)b * ewd,
-                                   y_words, ewd, cnt, B.nwin, L, 2, dst);
+                hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, y + off * y_words + ewo[b],
+                                   y_words, ewd[b], cnt, B.nwin[b], L, 2, dst);
             } else {
                 RngKey kb = rk;
                 kb.nonce += (uint64_t)(b + 1) << 56;                       // one stream per base
-                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, kb, (uint64_t)off, cnt, B.nwin, L,
-                                   2, 0, dst);
+                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, kb, (uint64_t)off, cnt, B.nwin[b],
+                                   L, 2, 0, dst);
             }
         }
         m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);

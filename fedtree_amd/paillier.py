@@ -132,6 +132,14 @@ def _stream_ordered(fn):
     return wrap
 
 
+class PublicBases(list):
+    """Published fixed-base bases hs_i (ints) and the bits of each base's exponent."""
+
+    def __init__(self, hs, exp_bits):
+        super().__init__(hs)
+        self.exp_bits = list(exp_bits)
+
+
 class Paillier:
     """Paillier key + batch engine (mirror of Paillier / Paillier_GPU).
 
@@ -259,18 +267,25 @@ class Paillier:
 
     def public_bases(self, seed=0):
         """Key holder: bases hs_i = t_i^n mod n^2 with <t_i> = Z_n^* (checked), to publish with n
-        (fthe_key_public_bases).  Returns a list of 3 ints (2 for known-order keys)."""
+        (fthe_key_public_bases).  Returns a PublicBases list of 3 ints (2 for known-order keys)
+        carrying the exponent bits of each base (.exp_bits)."""
         nb = ctypes.c_int()
-        _lib.check(self.lib.fthe_key_public_bases(self._key, int(seed), None, ctypes.byref(nb)), "key_public_bases")
-        hs = np.zeros((nb.value, self._cw()), dtype=np.uint32)
-        _lib.check(self.lib.fthe_key_public_bases(self._key, int(seed), _ptr(hs), ctypes.byref(nb)),
+        _lib.check(self.lib.fthe_key_public_bases(self._key, int(seed), None, ctypes.byref(nb), None),
                    "key_public_bases")
-        return [int.from_bytes(row.tobytes(), "little") for row in hs]
+        hs = np.zeros((nb.value, self._cw()), dtype=np.uint32)
+        eb = np.zeros(nb.value, dtype=np.int32)
+        _lib.check(self.lib.fthe_key_public_bases(self._key, int(seed), _ptr(hs), ctypes.byref(nb), _ptr(eb)),
+                   "key_public_bases")
+        return PublicBases([int.from_bytes(row.tobytes(), "little") for row in hs], [int(x) for x in eb])
 
-    def set_public_bases(self, hs):
-        """Build the public exact fixed-base tables for published bases (any key)."""
+    def set_public_bases(self, hs, exp_bits=None):
+        """Build the public exact fixed-base tables for published bases (any key); exp_bits
+        from a PublicBases list, or given, or None (full-length exponents)."""
+        if exp_bits is None:
+            exp_bits = getattr(hs, "exp_bits", None)
         arr = np.stack([_words(int(h), self._cw()) for h in hs])
-        _lib.check(self.lib.fthe_key_set_public_bases(self._key, self.dev.ctx, _ptr(arr), len(hs)),
+        eb = None if exp_bits is None else np.ascontiguousarray(exp_bits, dtype=np.int32)
+        _lib.check(self.lib.fthe_key_set_public_bases(self._key, self.dev.ctx, _ptr(arr), len(hs), _ptr(eb)),
                    "key_set_public_bases")
 
     @property
@@ -278,11 +293,11 @@ class Paillier:
         return bool(self._key) and self.lib.fthe_key_public_bases_info(self._key, None, None) == 0
 
     def public_bases_info(self):
-        """(bases, words per injected exponent) of the built public tables."""
-        nb, ew = ctypes.c_int(), ctypes.c_int()
-        _lib.check(self.lib.fthe_key_public_bases_info(self._key, ctypes.byref(nb), ctypes.byref(ew)),
+        """(bases, [words per injected exponent of each base]) of the built public tables."""
+        nb, ew = ctypes.c_int(), np.zeros(3, dtype=np.int32)
+        _lib.check(self.lib.fthe_key_public_bases_info(self._key, ctypes.byref(nb), _ptr(ew)),
                    "key_public_bases_info")
-        return nb.value, ew.value
+        return nb.value, [int(x) for x in ew[:nb.value]]
 
     def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
         """c = g^m r^n mod n^2 for every m (paillier.cpp:134-137).
@@ -302,13 +317,11 @@ class Paillier:
         if r is not None:
             if not isinstance(r, np.ndarray) and fixed_base_exact:
                 if public or not self.has_private:  # tuples of `bases` exponents (public_bases_info)
-                    nb, hw = self.public_bases_info()
-                    tot = nb * hw
+                    hws = self.public_bases_info()[1]
                 else:                               # tuples of 2 * bases exponents (fixed_base_exact_info)
-                    hw = self.n_words // 2
-                    tot = 6 * hw
-                r = np.stack([np.concatenate([_words(int(x), hw) for x in t]) for t in r]) if cnt \
-                    else np.zeros((0, tot), np.uint32)
+                    hws = [self.n_words // 2] * 6
+                r = np.stack([np.concatenate([_words(int(x), hw) for x, hw in zip(t, hws)]) for t in r]) if cnt \
+                    else np.zeros((0, sum(hws)), np.uint32)
             if not isinstance(r, np.ndarray):
                 nw = self.n_words + (2 if fixed_base else 0)
                 if fixed_base and cnt:

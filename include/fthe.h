@@ -183,18 +183,24 @@ int fthe_key_fixed_base_exact_bases(fthe_key *key);
  *                            p-1 or q-1 (rank 2 over GF(l) where l divides both;
  *                            a larger l escapes with probability < 2^-65), at every
  *                            l for FTHE_KEYGEN_KNOWN_ORDER keys; writes hs_i (nb *
- *                            2*n_words words; hs NULL: *nb only).  nb = 3, or 2
- *                            for known-order keys.  seed 0: /dev/urandom.  Host only.
+ *                            2*n_words words; hs NULL: *nb only) and the bits of
+ *                            each base's exponent (exp_bits[nb], nullable; published
+ *                            with the bases).  nb = 3 with 16 nwin bits each, or for
+ *                            known-order keys with gcd(p-1, q-1) < 2^64: 2, the first
+ *                            of order lcm(p-1, q-1) (16 nwin bits), the second
+ *                            generating the quotient Z_gcd (128 bits: 140 instead of
+ *                            264 products at P-2048).  seed 0: /dev/urandom.  Host only.
  * fthe_key_set_public_bases  any key with the public form: builds the tables for the
- *                            published hs (nb * 2*n_words words, 1 <= nb <= 3); then
- *                            FTHE_ENC_FIXED_BASE_EXACT on a public key (or with
- *                            FTHE_ENC_PUBLIC) uses them.  Not concurrent with calls
- *                            that use the key.
- * fthe_key_public_bases_info nb and the words per injected exponent (exp_words) of
- *                            the built tables; injected exponents (parity): r = y,
- *                            r_words = nb * exp_words, y_i < 2^(16 nwin). */
-int fthe_key_public_bases(fthe_key *key, uint64_t seed, uint32_t *hs, int *nb);
-int fthe_key_set_public_bases(fthe_key *key, fthe_ctx *ctx, const uint32_t *hs, int nb);
+ *                            published hs (nb * 2*n_words words, 1 <= nb <= 3) and
+ *                            exp_bits (multiples of 16, <= 16 nwin; NULL: 16 nwin
+ *                            each); then FTHE_ENC_FIXED_BASE_EXACT on a public key (or
+ *                            with FTHE_ENC_PUBLIC) uses them.  Not concurrent with
+ *                            calls that use the key.
+ * fthe_key_public_bases_info nb and the words per injected exponent of each base
+ *                            (exp_words[nb]); injected exponents (parity): r = y,
+ *                            r_words = sum exp_words, y_i < 2^exp_bits_i. */
+int fthe_key_public_bases(fthe_key *key, uint64_t seed, uint32_t *hs, int *nb, int *exp_bits);
+int fthe_key_set_public_bases(fthe_key *key, fthe_ctx *ctx, const uint32_t *hs, int nb, const int *exp_bits);
 int fthe_key_public_bases_info(fthe_key *key, int *nb, int *exp_words);
 
 /* ---- decrypt: m = L(c^lambda mod n^2) * mu mod n (paillier.cpp:153-156) ---

@@ -109,9 +109,10 @@ public:
     // r^n from the tables (~5.6x the per-ciphertext rate at P-2048).  Not in the reference.
     void publish_bases() {
         int nb = 0;
-        fthe_shim::check(fthe_key_public_bases(key_, 0, nullptr, &nb), "public_bases");
+        fthe_shim::check(fthe_key_public_bases(key_, 0, nullptr, &nb, nullptr), "public_bases");
         bases_.assign((size_t)nb * 2 * fthe_key_n_words(key_), 0);
-        fthe_shim::check(fthe_key_public_bases(key_, 0, bases_.data(), &nb), "public_bases");
+        base_bits_.assign(nb, 0);
+        fthe_shim::check(fthe_key_public_bases(key_, 0, bases_.data(), &nb, base_bits_.data()), "public_bases");
         nbases_ = nb;
     }
 
@@ -122,6 +123,7 @@ public:
         if (key_) fthe_key_destroy(key_);
         key_ = nullptr;
         bases_.clear();
+        base_bits_.clear();
         nbases_ = 0;
         fthe_shim::check(fthe_key_generate_ex(fthe_shim::thread_ctx(), keyLength, 0, keygen_flags, &key_), "keygen");
         export_cpu();
@@ -227,6 +229,7 @@ public:
 private:
     fthe_key *key_ = nullptr;
     std::vector<uint32_t> bases_;          // published fixed-base bases (nbases_ x 2 n_words words)
+    std::vector<int> base_bits_;           // and the bits of each base's exponent
     int nbases_ = 0;
     static size_t words(const mpz_t x) { return (mpz_sizeinbase(x, 2) + 31) / 32; }
     void copy_public(const Paillier_HIP &o) {
@@ -235,10 +238,11 @@ private:
         paillier_cpu = o.paillier_cpu;                                    // public part only
         parameters_cpu_to_gpu();
         bases_ = o.bases_;                                                // published with n (publish_bases)
+        base_bits_ = o.base_bits_;
         nbases_ = o.nbases_;
         if (nbases_)
-            fthe_shim::check(fthe_key_set_public_bases(key_, fthe_shim::thread_ctx(), bases_.data(), nbases_),
-                             "set_public_bases");
+            fthe_shim::check(fthe_key_set_public_bases(key_, fthe_shim::thread_ctx(), bases_.data(), nbases_,
+                                                       base_bits_.data()), "set_public_bases");
     }
     void export_cpu() {
         int nw = fthe_key_n_words(key_), hw = (nw + 1) / 2;

@@ -47,6 +47,7 @@ def _primes_below(n):
 
 
 SMALL = _primes_below(1 << 12)
+SMALL16 = _primes_below(1 << 16)
 
 
 def _dlog(z, a, l, P):
@@ -102,7 +103,7 @@ def test_public_exact_injected_exponents(dev, name):
     assert not party.has_private and party.has_public_bases
     nb, ew = party.public_bases_info()
     nwin = (n.bit_length() + 64 + 15) // 16
-    assert nb == 3 and ew == (nwin + 1) // 2
+    assert nb == 3 and ew == [(nwin + 1) // 2] * 3 and hs.exp_bits == [16 * nwin] * 3
     ebits = 16 * nwin
     rng = np.random.default_rng(len(name) + 300)
     cnt = 24
@@ -146,22 +147,80 @@ def test_public_exact_random_roundtrip(dev, coracle, name):
     assert np.array_equal(server.decrypt_u64(s), m[:1000] + m[1000:2000])
 
 
-def test_public_exact_known_order_two_bases(dev):
-    """FTHE_KEYGEN_KNOWN_ORDER: every prime factor of p-1, q-1 is checked, two bases."""
+def _full_factors(x):
+    """Distinct primes of x = (primes < 2^16 part) * (at most one large prime cofactor), the shape of
+    p - 1 for known-order keys (2 s P' with s a product of primes < 2^16); the cofactor is checked prime."""
+    fs = []
+    for l in SMALL16:
+        if x % l == 0:
+            fs.append(l)
+            while x % l == 0:
+                x //= l
+    if x > 1:
+        fs.append(x)
+    return fs
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_public_exact_known_order_short_exponent(dev, bits):
+    """FTHE_KEYGEN_KNOWN_ORDER keys: t_1 of order lcm(p-1, q-1) (a primitive root mod p and mod q,
+    checked here at every prime factor) with a full exponent, t_2 generating the quotient Z_g,
+    g = gcd(p-1, q-1), with a 128-bit exponent: 2 bases, 16 nwin + 128 exponent bits."""
     from fedtree_amd.paillier import Paillier
-    server = Paillier(dev)
-    server.keygen(1024, seed=77, known_order=True)
-    hs = server.public_bases(seed=3)
-    assert len(hs) == 2
+    rng = np.random.default_rng(bits)
+    server = Paillier(dev).keygen(bits, seed=77, known_order=True)
     p, q = server.p, server.q
+    n = p * q
+    hs = server.public_bases(seed=3)
+    nwin = (n.bit_length() + 64 + 15) // 16
+    assert len(hs) == 2 and hs.exp_bits == [16 * nwin, 128]
+    g = math.gcd(p - 1, q - 1)
+    for P in (p, q):
+        fs = _full_factors(P - 1)
+        assert _is_prime_list(fs, rng)
+        for l in fs:                                          # hs_1 mod P generates Z_P^* (t -> t^n bijective)
+            assert pow(hs[0] % P, (P - 1) // l, P) != 1, l
+    for l in _full_factors(g):                                 # t_2 generates Z_n^* / <t_1> = Z_g
+        a = [pow(h % p, (p - 1) // l, p) for h in hs]
+        b = [pow(h % q, (q - 1) // l, q) for h in hs]
+        assert pow(b[0], _dlog(a[0], a[1], l, p), q) != b[1], l
     _check_public_bases(hs, p, q)
     party = server.public(bases=hs)
+    nb, ew = party.public_bases_info()
+    assert nb == 2 and ew == [(nwin + 1) // 2, 4]
     m = np.arange(20000, dtype=np.uint64) * np.uint64(1000003)
     c = party.encrypt_u64(m, seed=2, fixed_base_exact=True)
     assert np.array_equal(server.decrypt_u64(c), m)
-    ys = [(5, 7), (0, 1), (2**1000 + 3, 2**900)]
-    c = party.encrypt_u64(m[:3], r=ys, fixed_base_exact=True)
-    assert pyoracle.words_to_ints(c) == [_want(p * q, x, y, hs) for x, y in zip(m[:3], ys)]
+    ys = [(5, 7), (0, 1), (2**(16 * nwin) - 1, 2**128 - 1), (2**1000 + 3, 2**100)]
+    c = party.encrypt_u64(m[:4], r=ys, fixed_base_exact=True)
+    assert pyoracle.words_to_ints(c) == [_want(n, x, y, hs) for x, y in zip(m[:4], ys)]
+    # full-length exponents on the same bases (exp_bits omitted) still encrypt correctly
+    full = server.public()
+    full.set_public_bases(list(hs))
+    assert full.public_bases_info() == (2, [(nwin + 1) // 2] * 2)
+    assert np.array_equal(server.decrypt_u64(full.encrypt_u64(m[:500], seed=9, fixed_base_exact=True)), m[:500])
+
+
+def _is_prime_list(fs, rng):
+    def mr(x):
+        if x < 4:
+            return x in (2, 3)
+        d, s = x - 1, 0
+        while d % 2 == 0:
+            d, s = d // 2, s + 1
+        for _ in range(24):
+            a = int(rng.integers(2, 2**62)) % (x - 3) + 2
+            y = pow(a, d, x)
+            if y in (1, x - 1):
+                continue
+            for _ in range(s - 1):
+                y = y * y % x
+                if y == x - 1:
+                    break
+            else:
+                return False
+        return True
+    return all(mr(f) for f in fs)
 
 
 def test_public_exact_histogram_flow(dev):
@@ -224,7 +283,11 @@ def test_public_exact_refusals(dev):
     for bad in ([n], [0], [n * n], [2, 3, 5, 7]):             # not a unit / out of range / nb > 3
         with pytest.raises(RuntimeError):
             pub.set_public_bases(bad)
-    assert pub.lib.fthe_key_set_public_bases(pub._key, pub.dev.ctx, None, 0) == _lib.FTHE_ERR_ARG
+    assert pub.lib.fthe_key_set_public_bases(pub._key, pub.dev.ctx, None, 0, None) == _lib.FTHE_ERR_ARG
+    with pytest.raises(RuntimeError):                        # exponent bits not a multiple of 16 / too long
+        pub.set_public_bases([2, 3], exp_bits=[100, 128])
+    with pytest.raises(RuntimeError):
+        pub.set_public_bases([2, 3], exp_bits=[16 * 200, 128])
     hs = server.public_bases(seed=1)
     pub.set_public_bases(hs)
     with pytest.raises(RuntimeError):                        # wrong injected exponent width
