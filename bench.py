@@ -324,7 +324,20 @@ def main():
             "crt_encrypt_per_s": round(nfb / ko_s), "decrypt_roundtrip_ok": bool(torch.equal(lowfb, m[:nfb])),
             "note": "FTHE_KEYGEN_KNOWN_ORDER key (p-1, q-1 factored): one verified generator per prime, 64 gathered "
                     "products per prime, exactly the reference's ciphertext distribution"}
-        del cfb, lowfb, pko
+        # parties of a known-order key: 2 published bases, the second with a 128-bit exponent
+        kparty = pko.public(bases=pko.public_bases())
+        kparty.encrypt_u64_dev(m[:nfb], cfb, seed=15, fixed_base_exact=True)
+        dev.sync()
+        kparty.encrypt_u64_dev(m[:nfb], cfb, seed=16, fixed_base_exact=True)
+        dev.sync()
+        kp_rate = nfb / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3)
+        pko.decrypt_u64_dev(cfb, lowfb)
+        dev.sync()
+        secondary["public_fixed_base_exact"]["known_order_key"] = {
+            "public_encrypt_per_s": round(kp_rate), "decrypt_roundtrip_ok": bool(torch.equal(lowfb, m[:nfb])),
+            "note": "t_1 of order lcm(p-1, q-1) (full exponent) and t_2 generating Z_n^*/<t_1> = Z_gcd(p-1,q-1) "
+                    "(128-bit exponent): 140 gathered products"}
+        del cfb, lowfb, pko, kparty
         # ciphertext adds (x*y mod n^2, 4096-bit n^2 on the four-lane kernel), device-resident
         na = min(2 * P, 1 << 20)
         o = torch.empty((na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
