@@ -124,13 +124,14 @@ int fthe_encrypt_words(fthe_key *key, fthe_ctx *ctx, const uint32_t *m, int m_wo
  * h per key; c = (1 + m n) * hs^alpha mod n^2 with hs = h^n mod n^2, i.e. a
  * Paillier encryption of m under r = h^alpha (Damgard-Jurik-Nielsen fixed-base
  * randomizer).  Decryption, add, mul are unchanged.  alpha is drawn per
- * ciphertext from the device ChaCha20 stream (r == NULL: 8*nwin random bits,
- * 64 more than the order of hs, independently mod p^2 and q^2 under CRT), or
- * injected through the r / r_words arguments of fthe_encrypt_u64[_dev]
- * (little-endian words, alpha < 2^alpha_bits; the same alpha for both CRT
- * halves).  8-bit windows: nwin gathered products from precomputed tables
- * (hs^(d 256^j), 256 entries per window, ~34 MB per key at P-2048) instead of
- * ~1.2 log2(n) products.
+ * ciphertext from the device ChaCha20 stream (r == NULL: alpha_bits random
+ * bits, 64 more than the bits of the modulus, independently mod p^2 and q^2
+ * under CRT), or injected through the r / r_words arguments of
+ * fthe_encrypt_u64[_dev] (little-endian words, alpha < 2^alpha_bits; the same
+ * alpha for both CRT halves).  16-bit windows (FTHE_FB_WINDOW=8: 8-bit): one
+ * gathered product per window from precomputed tables (hs^(d 65536^j), 65536
+ * entries per window, ~4.4 GB public + 2 x 1.2 GB CRT at P-2048, widened on the
+ * device from host-built 8-bit tables) instead of ~1.2 log2(n) products.
  * fthe_key_fixed_base        (re)build the tables for base h (h_words words,
  *                            1 <= h < n); h == NULL draws h from /dev/urandom.
  *                            Built on first use otherwise.  Not concurrent with
