@@ -130,7 +130,7 @@ int fthe_encrypt_words(fthe_key *key, fthe_ctx *ctx, const uint32_t *m, int m_wo
  * fthe_encrypt_u64[_dev] (little-endian words, alpha < 2^alpha_bits; the same
  * alpha for both CRT halves).  16-bit windows (FTHE_FB_WINDOW=8: 8-bit): one
  * gathered product per window from precomputed tables (hs^(d 65536^j), 65536
- * entries per window, ~4.4 GB public + 2 x 1.2 GB CRT at P-2048, widened on the
+ * entries per window, ~4.4 GB public + 2 x 1.4 GB CRT at P-2048, widened on the
  * device from host-built 8-bit tables) instead of ~1.2 log2(n) products.
  * fthe_key_fixed_base        (re)build the tables for base h (h_words words,
  *                            1 <= h < n); h == NULL draws h from /dev/urandom.
