@@ -146,10 +146,8 @@ public:
             for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
         });
         std::vector<uint32_t> c(2 * n * (size_t)cw);
-        int flags = enc_flags;            // exact fixed-base: p, q (key holder) or published bases (party)
-        if (!fthe_key_has_private(key_) && !nbases_) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
         fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
-                                          flags), "encrypt");
+                                          eff_flags()), "encrypt");
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) {
                 fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
@@ -222,6 +220,88 @@ public:
         fthe_shim::from_words(result, o.data(), cw);
     }
 
+    // ---- batch helpers for FedTree's HE call sites (not Paillier_GPU members) ----
+    // Each replaces a loop of per-pair GHPair operators (CPU GMP, ~11.5 us per add) with one engine call.
+    // Unencrypted operands are encrypted first, as the operators promote them (common.h:156-160).
+
+    // Histogram of one node (hist_tree_builder.cpp:565-595): hist[cut_col_ptr[f] + b] accumulates gh[i]
+    // for each instance i whose feature f has bin b = dense_bin_id[i * n_col + f] (b == max_num_bin: a
+    // missing value, skipped), in instance order: one segmented product over g and h
+    // (fthe_reduce_segments).  hist holds cut_col_ptr[n_col] entries; bins without instances are left
+    // untouched (unencrypted zero, like the reference's).  A populated bin is the product of its members;
+    // the reference's first += also folds in a fresh Enc(0) (Q10): same plaintext, other randomness.
+    void histogram(SyncArray<GHPair> &gh, const unsigned char *dense_bin_id, const int *cut_col_ptr, int n_col,
+                   int max_num_bin, SyncArray<GHPair> &hist) {
+        const size_t n = gh.size(), nb = (size_t)cut_col_ptr[n_col];
+        if (hist.size() < nb) throw std::runtime_error("histogram: hist smaller than cut_col_ptr[n_col]");
+        std::vector<int64_t> ptr(2 * nb + 1, 0);                 // CSR: g segments, then h segments
+        for (size_t i = 0; i < n; i++)
+            for (int f = 0; f < n_col; f++) {
+                const int b = dense_bin_id[i * n_col + f];
+                if (b != max_num_bin) ptr[cut_col_ptr[f] + b + 1]++;
+            }
+        for (size_t s = 0; s < nb; s++) ptr[s + 1] += ptr[s];
+        const int64_t tot = ptr[nb];
+        std::vector<int64_t> idx(2 * (size_t)tot), cur(ptr.begin(), ptr.begin() + nb);
+        for (size_t i = 0; i < n; i++)
+            for (int f = 0; f < n_col; f++) {
+                const int b = dense_bin_id[i * n_col + f];
+                if (b != max_num_bin) idx[cur[cut_col_ptr[f] + b]++] = (int64_t)i;
+            }
+        for (size_t s = 0; s < nb; s++) ptr[nb + s + 1] = tot + ptr[s + 1];    // h rows are n .. 2n-1
+        for (int64_t t = 0; t < tot; t++) idx[tot + t] = idx[t] + (int64_t)n;
+        const int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> x = rows(gh), out(2 * nb * (size_t)cw);
+        fthe_shim::check(fthe_reduce_segments(key_, fthe_shim::thread_ctx(), x.data(), 2 * n, ptr.data(), idx.data(),
+                                              2 * nb, out.data()), "histogram");
+        auto *hd = hist.host_data();
+        fthe_shim::parallel_for(nb, [&](size_t b, size_t e) {
+            for (size_t s = b; s < e; s++)
+                if (ptr[s + 1] > ptr[s]) set_enc(hd[s], &out[s * cw], &out[(nb + s) * cw], cw);
+        });
+    }
+
+    // k-party merge (hist_tree_builder.cpp:1015-1058): out[b] = prod_j parties[j][b] as one k-way product
+    // (fthe_reduce_kway).  zero_first: Enc(0) * prod_j ..., the reference's exact sequence (its zero
+    // accumulator's first += encrypts 0) at the price of one fresh encryption per entry;
+    // without it the plaintexts are the same and only the randomness differs.
+    void merge(const std::vector<SyncArray<GHPair> *> &parties, SyncArray<GHPair> &out, bool zero_first = false) {
+        const size_t z = zero_first ? 1 : 0, k = parties.size() + z, nb = out.size();
+        if (k > 64 || parties.empty()) throw std::runtime_error("merge: 1 to 63 parties per call");
+        for (auto *pt : parties)
+            if (pt->size() != nb) throw std::runtime_error("merge: histogram sizes differ");
+        const int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> x(k * 2 * nb * (size_t)cw), o(2 * nb * (size_t)cw);
+        if (zero_first) {
+            std::vector<uint64_t> zero(2 * nb, 0);
+            fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), zero.data(), 2 * nb, nullptr, 0, 0,
+                                              x.data(), eff_flags()), "merge");
+        }
+        for (size_t j = z; j < k; j++) {
+            std::vector<uint32_t> r = rows(*parties[j - z]);
+            std::copy(r.begin(), r.end(), x.begin() + j * 2 * nb * (size_t)cw);
+        }
+        fthe_shim::check(fthe_reduce_kway(key_, fthe_shim::thread_ctx(), x.data(), (int)k, 2 * nb, o.data()), "merge");
+        auto *d = out.host_data();
+        fthe_shim::parallel_for(nb, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; i++) set_enc(d[i], &o[i * cw], &o[(nb + i) * cw], cw);
+        });
+    }
+
+    // Sibling histogram (hist_tree_builder.cpp:678) and missing_gh (:724): out = a - b, exactly the ciphertext
+    // GHPair::operator- produces (a * b^(2^64-1), common.h:253-337), as one fused batch (fthe_sub).
+    void subtract(SyncArray<GHPair> &a, SyncArray<GHPair> &b, SyncArray<GHPair> &out) {
+        const size_t n = a.size();
+        if (b.size() != n || out.size() != n) throw std::runtime_error("subtract: sizes differ");
+        const int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> xa = rows(a), xb = rows(b), o(2 * n * (size_t)cw);
+        fthe_shim::check(fthe_sub(key_, fthe_shim::thread_ctx(), xa.data(), xb.data(), 2 * n, o.data()), "subtract");
+        auto *d = out.host_data();
+        fthe_shim::parallel_for(n, [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; i++) set_enc(d[i], &o[i * cw], &o[(n + i) * cw], cw);
+        });
+    }
+
     uint32_t key_length;
     Paillier_GMP paillier_cpu;          // host copy the GHPair operators use (common.h:72)
     fthe_key *key() const { return key_; }
@@ -232,6 +312,52 @@ private:
     std::vector<int> base_bits_;           // and the bits of each base's exponent
     int nbases_ = 0;
     static size_t words(const mpz_t x) { return (mpz_sizeinbase(x, 2) + 31) / 32; }
+    int eff_flags() const {             // exact fixed-base: p, q (key holder) or published bases (party)
+        int flags = enc_flags;
+        if (!fthe_key_has_private(key_) && !nbases_) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
+        return flags;
+    }
+    void set_enc(GHPair &p, const uint32_t *g, const uint32_t *h, int cw) const {
+        fthe_shim::from_words(p.g_enc, g, cw);
+        fthe_shim::from_words(p.h_enc, h, cw);
+        p.g = 0;
+        p.h = 0;
+        p.encrypted = true;
+        p.paillier = paillier_cpu;      // the public key rides along, as after GHPair::operator+
+    }
+    // g rows then h rows of a batch (2 n_words words each); unencrypted entries are encrypted here
+    std::vector<uint32_t> rows(SyncArray<GHPair> &a) {
+        auto *d = a.host_data();
+        const size_t n = a.size();
+        const int cw = 2 * fthe_key_n_words(key_);
+        std::vector<uint32_t> x(2 * n * (size_t)cw, 0);
+        std::vector<size_t> plain;
+        for (size_t i = 0; i < n; i++)
+            if (!d[i].encrypted) plain.push_back(i);
+        if (!plain.empty()) {
+            const size_t np = plain.size();
+            std::vector<uint64_t> m(2 * np);
+            for (size_t j = 0; j < np; j++) {
+                m[j] = fthe_shim::encode(d[plain[j]].g);
+                m[np + j] = fthe_shim::encode(d[plain[j]].h);
+            }
+            std::vector<uint32_t> c(2 * np * (size_t)cw);
+            fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * np, nullptr, 0, 0, c.data(),
+                                              eff_flags()), "encrypt");
+            for (size_t j = 0; j < np; j++) {
+                std::copy(&c[j * cw], &c[(j + 1) * cw], &x[plain[j] * cw]);
+                std::copy(&c[(np + j) * cw], &c[(np + j + 1) * cw], &x[(n + plain[j]) * cw]);
+            }
+        }
+        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; i++) {
+                if (!d[i].encrypted) continue;
+                fthe_shim::to_words(d[i].g_enc, &x[i * cw], cw);
+                fthe_shim::to_words(d[i].h_enc, &x[(n + i) * cw], cw);
+            }
+        });
+        return x;
+    }
     void copy_public(const Paillier_HIP &o) {
         if (key_) fthe_key_destroy(key_);
         key_ = nullptr;

@@ -50,6 +50,44 @@ int main(int argc, char **argv) {
         }
         printf("big batch of %zu checked\n", N);
     }
+    if (mode == "helpers") {                                     // histogram / merge / sibling subtract
+        const int n = 40, n_col = 2, cut[3] = {0, 4, 7}, missing = 255;
+        std::vector<unsigned char> bins(n * n_col);
+        SyncArray<GHPair> ggh(n);
+        double want_g[7] = {0}, want_h[7] = {0};
+        for (int i = 0; i < n; i++) {
+            const float gi = 0.01f * (float)(i % 13) - 0.05f, hi = 0.02f * (float)(i % 7) + 0.1f;
+            ggh.host_data()[i] = GHPair(gi, hi);
+            bins[i * n_col] = (unsigned char)(i % 4);
+            bins[i * n_col + 1] = (unsigned char)(i % 5 == 4 ? missing : i % 3);
+            for (int f = 0; f < n_col; f++) {
+                const int b = bins[i * n_col + f];
+                if (b == missing) continue;
+                want_g[cut[f] + b] += (double)(long)(gi * 1e6) / 1e6;
+                want_h[cut[f] + b] += (double)(long)(hi * 1e6) / 1e6;
+            }
+        }
+        server.encrypt(ggh);
+        for (int i = 0; i < n; i++) ggh.host_data()[i].encrypted = true;
+        SyncArray<GHPair> h1(7), merged(7), sib(7);
+        party.histogram(ggh, bins.data(), cut, n_col, missing, h1);   // party side, public key
+        SyncArray<GHPair> h2(7), h3(7);
+        for (int s = 0; s < 7; s++) { h2.host_data()[s] = h1.host_data()[s]; h3.host_data()[s] = h1.host_data()[s]; }
+        h3.host_data()[6] = GHPair(0.5f, 0.25f);                        // an unencrypted operand is promoted
+        party.merge({&h1, &h2, &h3}, merged, true);
+        party.subtract(merged, h1, sib);
+        server.decrypt(h1);
+        server.decrypt(merged);
+        server.decrypt(sib);
+        for (int s = 0; s < 7; s++) {
+            const double g3 = s == 6 ? 2 * want_g[s] + 0.5 : 3 * want_g[s], h3v = s == 6 ? 2 * want_h[s] + 0.25 : 3 * want_h[s];
+            if (std::fabs(h1.host_data()[s].g - want_g[s]) > 1e-5 || std::fabs(h1.host_data()[s].h - want_h[s]) > 1e-5) bad++;
+            if (std::fabs(merged.host_data()[s].g - g3) > 1e-5 || std::fabs(merged.host_data()[s].h - h3v) > 1e-5) bad++;
+            if (std::fabs(sib.host_data()[s].g - (g3 - want_g[s])) > 1e-5) bad++;
+            printf("bin %d: hist g %.6f (want %.6f)  merged g %.6f (want %.6f)  sibling g %.6f\n", s,
+                   h1.host_data()[s].g, want_g[s], merged.host_data()[s].g, g3, sib.host_data()[s].g);
+        }
+    }
     GHPair one = gh.host_data()[0];
     server.decrypt(one);                                         // decrypt_gh
     if (std::fabs(one.g - g[0]) > 2e-6) bad++;

@@ -27,7 +27,7 @@ def test_shim_compiles_and_links(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["default", "exact", "exact_known_order", "public_exact", "short", "big"])
+@pytest.mark.parametrize("mode", ["default", "exact", "exact_known_order", "public_exact", "short", "helpers", "big"])
 def test_shim_runs_server_party_flow(tmp_path, mode):
     exe = _build(str(tmp_path / "shim_test"))
     r = subprocess.run([exe, "1024", mode], capture_output=True, text=True, timeout=300)
