@@ -288,6 +288,25 @@ public:
         });
     }
 
+    // Per-feature prefix sums of a histogram (inclusive_scan_by_key, hist_tree_builder.cpp:695-708), in
+    // place: hist[t] = sum of hist[cut_col_ptr[f] .. t] within feature f, one segmented scan (g and h
+    // planes as segments of their own, fthe_scan_segments).
+    void prefix(SyncArray<GHPair> &hist, const int *cut_col_ptr, int n_col) {
+        const size_t nb = (size_t)cut_col_ptr[n_col];
+        if (hist.size() < nb) throw std::runtime_error("prefix: hist smaller than cut_col_ptr[n_col]");
+        const int cw = 2 * fthe_key_n_words(key_);
+        std::vector<int64_t> seg(2 * (size_t)n_col + 1);
+        for (int f = 0; f <= n_col; f++) seg[f] = cut_col_ptr[f];
+        for (int f = 1; f <= n_col; f++) seg[n_col + f] = (int64_t)nb + cut_col_ptr[f];
+        std::vector<uint32_t> x = rows_n(hist, nb), o(2 * nb * (size_t)cw);
+        fthe_shim::check(fthe_scan_segments(key_, fthe_shim::thread_ctx(), x.data(), seg.data(), 2 * (size_t)n_col,
+                                            o.data()), "prefix");
+        auto *d = hist.host_data();
+        fthe_shim::parallel_for(nb, [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; i++) set_enc(d[i], &o[i * cw], &o[(nb + i) * cw], cw);
+        });
+    }
+
     // Sibling histogram (hist_tree_builder.cpp:678) and missing_gh (:724): out = a - b, exactly the ciphertext
     // GHPair::operator- produces (a * b^(2^64-1), common.h:253-337), as one fused batch (fthe_sub).
     void subtract(SyncArray<GHPair> &a, SyncArray<GHPair> &b, SyncArray<GHPair> &out) {
@@ -326,9 +345,9 @@ private:
         p.paillier = paillier_cpu;      // the public key rides along, as after GHPair::operator+
     }
     // g rows then h rows of a batch (2 n_words words each); unencrypted entries are encrypted here
-    std::vector<uint32_t> rows(SyncArray<GHPair> &a) {
+    std::vector<uint32_t> rows(SyncArray<GHPair> &a) { return rows_n(a, a.size()); }
+    std::vector<uint32_t> rows_n(SyncArray<GHPair> &a, size_t n) {       // the first n entries
         auto *d = a.host_data();
-        const size_t n = a.size();
         const int cw = 2 * fthe_key_n_words(key_);
         std::vector<uint32_t> x(2 * n * (size_t)cw, 0);
         std::vector<size_t> plain;

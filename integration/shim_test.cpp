@@ -76,6 +76,16 @@ int main(int argc, char **argv) {
         h3.host_data()[6] = GHPair(0.5f, 0.25f);                        // an unencrypted operand is promoted
         party.merge({&h1, &h2, &h3}, merged, true);
         party.subtract(merged, h1, sib);
+        SyncArray<GHPair> pre(7);
+        for (int s = 0; s < 7; s++) pre.host_data()[s] = h1.host_data()[s];
+        party.prefix(pre, cut, n_col);                                  // per-feature inclusive scan
+        server.decrypt(pre);
+        double acc = 0;
+        for (int s = 0; s < 7; s++) {
+            acc = (s == cut[0] || s == cut[1]) ? want_g[s] : acc + want_g[s];
+            if (std::fabs(pre.host_data()[s].g - acc) > 2e-5) bad++;
+            printf("bin %d: prefix g %.6f (want %.6f)\n", s, pre.host_data()[s].g, acc);
+        }
         server.decrypt(h1);
         server.decrypt(merged);
         server.decrypt(sib);
