@@ -5,7 +5,7 @@
   decrypt on a strided sample);
 * the homomorphic sum of all 20M ciphertexts (one segmented product, the root-sum reduction of
   tree.cpp:20-34 at its largest) decrypts to the plaintext sum mod 2^64 -- a checksum of the whole batch;
-* the same over the g plane alone, per 1M-element segment (20 segment checksums);
+* the same over the g plane alone, per 2^20-element segment (10 segment checksums, the last ragged);
 * seeded determinism on a slice across the 393,216-lane chunk boundary.
 The oracle's per-element bit-exactness is covered at smaller sizes (test_gpu_parity.py); these checks
 are what the full size adds.  Integer work: every comparison is exact.
@@ -50,7 +50,7 @@ def test_fullsize_encrypt_decrypt_and_checksums(dev):
     pl.decrypt_u64_dev(tot, s)
     want = int(m_host.sum(dtype=np.uint64))                                     # wraps mod 2^64
     assert int(s.cpu().numpy().view(np.uint64)[0]) == want
-    # 20 segment checksums over the g plane (1M elements each, the last one ragged)
+    # 10 segment checksums over the g plane (2^20 elements each, the last one ragged)
     bounds = list(range(0, PAIRS, 1 << 20)) + [PAIRS]
     seg = torch.tensor(bounds, dtype=torch.int64, device="cuda:0")
     sums = torch.empty((len(bounds) - 1, 2 * pl.n_words), dtype=torch.int32, device="cuda:0")
