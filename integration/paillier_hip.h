@@ -21,6 +21,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <exception>
 #include <stdexcept>
 #include <string>
@@ -33,8 +35,18 @@
 #include "FedTree/Encryption/paillier_gmp.h"
 
 namespace fthe_shim {
+// Engine status codes become exceptions.  The reference aborts on engine errors (CUDA_CHECK ->
+// CHECK_EQ, exit(1); common.h:47-52, paillier_gpu.cu:13-16): uncaught, an exception does the same
+// (std::terminate), and a caller that wants to recover can catch it.  Define FTHE_SHIM_ABORT to
+// print and abort() instead, as LOG(FATAL) would.
 inline void check(int st, const char *what) {
-    if (st != FTHE_OK) throw std::runtime_error(std::string(what) + ": " + fthe_strerror(st));
+    if (st == FTHE_OK) return;
+#ifdef FTHE_SHIM_ABORT
+    std::fprintf(stderr, "fthe: %s: %s\n", what, fthe_strerror(st));
+    std::abort();
+#else
+    throw std::runtime_error(std::string(what) + ": " + fthe_strerror(st));
+#endif
 }
 // One engine context per host thread (the boundary is entered from OpenMP
 // regions, FLtrainer.cpp:275-306); device from FTHE_DEVICE (default 0).
