@@ -10,8 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INTEG = os.path.join(ROOT, "integration")
 
 
-def _build(out, src="shim_test.cpp"):
-    cmd = ["g++", "-O2", "-std=c++17", "-pthread", "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
+def _build(out, src="shim_test.cpp", extra=()):
+    cmd = ["g++", "-O2", "-std=c++17", "-pthread", *extra, "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
            "-I" + os.path.join(ROOT, "include"), "-idirafter", "/opt/conda/include",
            os.path.join(INTEG, src), "-o", out, "-L" + os.path.join(ROOT, "fedtree_amd"), "-lfthe",
            "-Wl,-rpath," + os.path.join(ROOT, "fedtree_amd"), "-l:libgmp.so.10"]
@@ -24,6 +24,7 @@ def test_shim_compiles_and_links(tmp_path):
     exe = _build(str(tmp_path / "shim_test"))
     assert os.path.exists(exe)
     assert os.path.exists(_build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp"))
+    assert os.path.exists(_build(str(tmp_path / "shim_abort"), extra=("-DFTHE_SHIM_ABORT",)))
 
 
 @pytest.mark.gpu
