@@ -1,5 +1,6 @@
 """Small driver for kernel traces / counters of the mod-n^2 (four-lane) kernel:
-one device-resident add, one 8-way reduce and one histogram scatter at Paillier-2048.
+one device-resident add, one 8-way reduce, one Montgomery-resident add, one party encrypt
+from published bases and one histogram scatter at Paillier-2048 (--ops selects).
 
   python tools/prof_ops.py [--n 262144]
 """
@@ -40,6 +41,17 @@ def main():
         pl.reduce_kway_dev(x, 8, o)
         dev.sync()
         print("kway8", n, "ms", dev.last_kernel_ms())
+    if "mont" in ops:                                 # Montgomery-resident add (one product per add)
+        mr = torch.empty_like(c)
+        pl.to_mont_dev(c, mr)
+        pl.add_mont_dev(mr, mr, o)
+        dev.sync()
+        print("add_mont", n, "ms", dev.last_kernel_ms())
+    if "pbx" in ops:                                  # party encrypt from published bases (gathered products)
+        party = pl.public(bases=pl.public_bases(seed=3))
+        party.encrypt_u64_dev(m, o, seed=2, fixed_base_exact=True)
+        dev.sync()
+        print("public_exact", n, "ms", dev.last_kernel_ms())
     if "hist" in ops:
         rng = np.random.default_rng(1)
         ni = n // 2
