@@ -250,6 +250,26 @@ def main():
         fbr["note"] = ("opt-in FTHE_ENC_FIXED_BASE: c = (1+mn) hs^alpha, hs = h^n mod n^2, alpha from the device "
                        "CSPRNG; 16-bit-window tables; r = h^alpha ranges over a subgroup, not the reference's distribution")
         secondary["fixed_base"] = fbr
+        # latency of one GHPair (2 ciphertexts), host in and out: decrypt_gh (server.h:69-78) per node, from
+        # OpenMP threads (FLtrainer.cpp:758-764).  One wave runs each modexp serially, so a lone pair costs the
+        # full exponentiation time; concurrent callers on their own contexts overlap.
+        mh = np.array([123456, 654321], dtype=np.uint64)
+        ch = pl.encrypt_u64(mh, seed=3)
+        pl.decrypt_u64(ch)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            pl.decrypt_u64(ch)
+        dec1_ms = (time.perf_counter() - t0) / 5 * 1e3
+        t0 = time.perf_counter()
+        for _ in range(5):
+            pl.encrypt_u64(mh, seed=4)
+        enc1_ms = (time.perf_counter() - t0) / 5 * 1e3
+        secondary["single_pair_latency_ms"] = {"decrypt": round(dec1_ms, 2), "encrypt": round(enc1_ms, 2),
+                                               "decrypt_short": None}
+        t0 = time.perf_counter()
+        for _ in range(5):
+            pl.decrypt_u64(ch, short=True)
+        secondary["single_pair_latency_ms"]["decrypt_short"] = round((time.perf_counter() - t0) / 5 * 1e3, 2)
         # key generation (homo_init; re-run every round in the vertical simulation, FLtrainer.cpp:556):
         # host prime search on up to 16 threads + device key set-up
         t0 = time.perf_counter()
