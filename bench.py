@@ -251,8 +251,9 @@ def main():
                        "CSPRNG; 16-bit-window tables; r = h^alpha ranges over a subgroup, not the reference's distribution")
         secondary["fixed_base"] = fbr
         # latency of one GHPair (2 ciphertexts), host in and out: decrypt_gh (server.h:69-78) per node, from
-        # OpenMP threads (FLtrainer.cpp:758-764).  One wave runs each modexp serially, so a lone pair costs the
-        # full exponentiation time; concurrent callers on their own contexts overlap.
+        # OpenMP threads (FLtrainer.cpp:758-764).  One lane runs each modexp serially; batches this small run the
+        # mod-q half on the context's side stream beside the mod-p half, so a lone pair costs one exponentiation
+        # (the short decrypt has only the p half).  Concurrent callers on their own contexts overlap.
         mh = np.array([123456, 654321], dtype=np.uint64)
         ch = pl.encrypt_u64(mh, seed=3)
         pl.decrypt_u64(ch)

@@ -73,6 +73,16 @@ size_t chunk_lanes() {
     return v;
 }
 
+// Decrypts of at most this many lanes run their p and q halves on two streams (half the chip's
+// 2-waves/SIMD capacity at s74); FTHE_DEC_SPLIT overrides, 0 turns it off (A/B).
+size_t dec_split_lanes() {
+    static size_t v = [] {
+        const char *e = getenv("FTHE_DEC_SPLIT");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)65536;
+    }();
+    return v;
+}
+
 // Launch size of the row-I/O ops (four-lane kernel, no slots but the R^k constant):
 // 4 chunks; FTHE_ROWIO_CHUNK overrides (A/B)
 size_t rowio_chunk_lanes() {
@@ -129,6 +139,8 @@ struct fthe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t copy = nullptr;               // host<->device staging copies, overlapped with compute
+    hipStream_t side = nullptr;               // second compute stream: the q half of small decrypts
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     PinBuf stage_out[2], stage_in[2];
     hipEvent_t ev_done[2] = {}, ev_copied[2] = {}, ev_in[2] = {};
     hipModule_t mod[MAX_VARIANTS] = {};
@@ -223,7 +235,7 @@ struct fthe_key {
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
-    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
@@ -327,6 +339,9 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
     c->device = device;
     HIPOK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPOK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    HIPOK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIPOK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIPOK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     for (int i = 0; i < 2; i++) {
         HIPOK(hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
         HIPOK(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
@@ -351,6 +366,7 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) (void)hipModuleUnload(c->mod[i]);
     if (c->cub_tmp) (void)hipFree(c->cub_tmp);
     for (auto &e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -358,6 +374,9 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     for (int i = 0; i < 2; i++) {
         if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
         if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
@@ -572,7 +591,16 @@ static int key_finish(fthe_key *k) {
                 e.storex(SL_SAVED);
                 e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);    // m (n mod P^2)
                 e.addsmall(1); e.mul(SL_SAVED);                  // (1 + m n) r^n mod P^2
-                if (side) e.storex(SL_OUTQ); else crt_tail(e);
+                if (side) {
+                    e.storex(SL_OUTQ);
+                } else {
+                    // the split form (q half on the side stream) stops at c_p and runs the tail after the join
+                    Prog nt = e; nt.storex(SL_OUTP); nt.end();
+                    k->pr_enc_p_nt = k->add_prog(nt);
+                    Prog t; t.loadx(SL_OUTP); crt_tail(t); t.end();
+                    k->pr_enc_tail = k->add_prog(t);
+                    crt_tail(e);
+                }
                 e.end();
                 (side ? k->pr_enc_q : k->pr_enc_p) = k->add_prog(e);
             }
@@ -898,7 +926,8 @@ namespace {
 
 // Launch the montprog kernel, bracketed by profiling events when enabled.
 int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, const DevMod &mod, double lane_mm,
-                    size_t live, const void *const *rows = nullptr, int nrows = 0) {
+                    size_t live, const void *const *rows = nullptr, int nrows = 0, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     struct {
         void *s; const void *p; const void *cx; uint32_t ls, ss; uint32_t live, pad; const void *rows[16];
     } args = {slots, prog, mod.d_ctx, (uint32_t)L * 4, (uint32_t)((size_t)S * L * 4), (uint32_t)live, 0, {}};
@@ -926,12 +955,12 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
         c->prof_mm[c->prof_used] = lane_mm;
         c->prof_vi[c->prof_used] = vi;
         ev = &c->prof_ev[c->prof_used++];
-        HIPOK(hipEventRecord(ev->first, c->stream));
+        HIPOK(hipEventRecord(ev->first, st));
     }
-    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, 256, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
+    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg) != hipSuccess)
         return FTHE_ERR_HIP;
     if (ev) {
-        HIPOK(hipEventRecord(ev->second, c->stream));
+        HIPOK(hipEventRecord(ev->second, st));
         c->prof_lane_mm += lane_mm * (double)live;
         c->prof_alg_macs += lane_mm * (double)live * mod.w_alg();
         c->prof_launch_lanes += (double)live;
@@ -954,24 +983,25 @@ void unpack_rows(hipStream_t st, uint32_t *x, const uint32_t *N, int S, int L, s
 struct Launch {
     fthe_ctx *c; const fthe_key *k; int L; int S; int B; double mm = 0; size_t live = 0;
     void *base = nullptr;          // slot region (c->slots, or c->slots1 for small-modulus programs)
+    hipStream_t st = nullptr;      // compute stream (null: the context's main stream)
     uint32_t *slot(int s) const { return (uint32_t *)base + (size_t)s * S * L; }
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
     int prog(const fthe_key::PH &ph, const DevMod &mod, const void *const *rows = nullptr, int nrows = 0) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows);
+        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows, st);
         if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;
     }
     int prog_raw(const uint32_t *p, double pmm, const DevMod &mod, const void *const *rows, int nrows) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, base, S, L, p, mod, pmm, live, rows, nrows);
+        int rc = launch_montprog(c, base, S, L, p, mod, pmm, live, rows, nrows, st);
         if (rc) return rc;
         mm += pmm * (double)live;
         return FTHE_OK;
     }
     void fill(int s, int h) {
-        hipLaunchKernelGGL(k_fill_const, grid(), dim3(256), 0, c->stream, k->cst(h), slot(s), S, L);
+        hipLaunchKernelGGL(k_fill_const, grid(), dim3(256), 0, st ? st : c->stream, k->cst(h), slot(s), S, L);
     }
 };
 
@@ -1185,8 +1215,14 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     }
     if (!crt && !k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     if (flags & FTHE_ENC_FIXED_BASE) return encrypt_fb_impl(k, c, m, count, r, r_words, rng_seed, out, crt, pipe);
+    static const bool no_direct = getenv("FTHE_NO_DIRECT_Y") != nullptr;
+    const bool direct_y = crt && !r && !no_direct;
+    // small batches: the q half on the side stream in a second slot region, as decrypt_impl
+    const int vi = variant_index(k->spq.S);
+    const bool split = direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    const int nsl = nslots_for(k);
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k), crt ? k->spq : k->sn2);
+    int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     // Device-drawn randomness under CRT draws y_p, y_q uniform in [1,p), [1,q) and
@@ -1195,8 +1231,6 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     // y^P mod P^2 for uniform y has exactly the distribution of r^n mod P^2 for the
     // reference's uniform r, independently for P = p, q (CRT).  FTHE_NO_DIRECT_Y=1
     // keeps the explicit r (A/B).  Injected r always takes both stages (bit-exact).
-    static const bool no_direct = getenv("FTHE_NO_DIRECT_Y") != nullptr;
-    const bool direct_y = crt && !r && !no_direct;
     // scratch: AoS r words for the device RNG
     if (!r && (rc = c->scratch.ensure((size_t)L * nw * 4 * (direct_y ? 2 : 1)))) return rc;
     RngKey rk{};
@@ -1206,6 +1240,14 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         rk.nonce = splitmix64(s);
     }
     Launch L1 = Lc;                    // stage A: mod p, q on the small-limb kernel, own slot region
+    Launch Lq = Lc;                    // split: q half, region 2 of the slots, side stream
+    if (split) {
+        Lq.base = (uint8_t *)Lc.base + (size_t)nsl * S * L * 4;
+        Lq.st = c->side;
+        HIPOK(hipEventRecord(c->ev_fork, c->stream));
+        HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_nRq);
+    }
     if (direct_y) {
         Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
         Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_nRq);
@@ -1225,7 +1267,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     }
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
-        Lc.live = cnt; L1.live = cnt;
+        Lc.live = cnt; L1.live = cnt; Lq.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         const uint32_t *rw = r + (r ? off * r_words : 0);
         int rwn = r_words;
@@ -1239,6 +1281,25 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
             pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lc.slot(SL_T3), S, L, Lc.B);
             pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lc.slot(SL_T4), S, L, Lc.B);
+            if (split) {
+                m.pack(c->stream, Lc.grid(), off, cnt, Lq.slot(SL_IN1), S, L, Lc.B);
+                pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lq.slot(SL_T4), S, L, Lc.B);
+                HIPOK(hipEventRecord(c->ev_fork, c->stream));
+                HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+                if ((rc = Lq.prog(k->pr_enc_q, k->mq2))) return rc;
+                HIPOK(hipEventRecord(c->ev_join, c->side));
+                if ((rc = Lc.prog(k->pr_enc_p_nt, k->mp2))) return rc;
+                HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lq.slot(SL_OUTQ),
+                                   k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+                if ((rc = Lc.prog(k->pr_enc_tail, k->mp2))) return rc;
+                hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S,
+                                   L, Lc.B);
+                mul_add_out(c->stream, Lc.grid(), Lq.slot(SL_OUTQ), S, k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt,
+                            out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+                if (pipe && (rc = pipe->after(off, cnt))) return rc;
+                continue;
+            }
             if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
             hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
                                k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
@@ -1286,6 +1347,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         Lc.mm += L1.mm; L1.mm = 0;
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
+    Lc.mm += Lq.mm;
     return end_call(c, Lc);
 }
 
@@ -2140,21 +2202,43 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
                         uint32_t *m_full, HostPipe *pipe, bool short_pt = false) {
     if (!k || !c || (!ct && count)) return FTHE_ERR_ARG;
     if (!k->priv) return FTHE_ERR_NOPRIV;
+    // Batches that leave most of the chip idle (a GHPair from decrypt_gh, one tree node's sums) run the
+    // c^(q-1) mod q^2 exponentiation on the side stream, in a second slot region, beside c^(p-1) mod p^2:
+    // one exponentiation of latency instead of two.  Large batches fill the chip with one half at a time.
+    const int vi = variant_index(k->spq.S);
+    const bool split = !short_pt && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    const int nsl = nslots_for(k);
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, nslots_for(k), k->spq);
+    int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, k->spq);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    Launch Lq = Lc;                        // q half: region 2 of the slots, side stream
+    if (split) {
+        Lq.base = (uint8_t *)Lc.base + (size_t)nsl * S * L * 4;
+        Lq.st = c->side;
+        HIPOK(hipEventRecord(c->ev_fork, c->stream));
+        HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_R3q); Lq.fill(SL_T5, k->c_one);
+    }
     Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p);
     Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_R3q);
     Lc.fill(SL_T5, k->c_one);
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
-        Lc.live = cnt;
+        Lc.live = cnt; Lq.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         const uint32_t *src = ct + off * cw;
         pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         pack_rows(c->stream, src, cw, cnt, Lc.B * S,
                            Lc.slot(SL_IN1), S, L, Lc.B);
+        if (split) {
+            pack_rows(c->stream, src, cw, cnt, 0, Lq.slot(SL_IN0), S, L, Lc.B);
+            pack_rows(c->stream, src, cw, cnt, Lc.B * S, Lq.slot(SL_IN1), S, L, Lc.B);
+            HIPOK(hipEventRecord(c->ev_fork, c->stream));
+            HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+            if ((rc = Lq.prog(k->pr_dec_q, k->mq2))) return rc;
+            HIPOK(hipEventRecord(c->ev_join, c->side));
+        }
         if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
         if (short_pt) {
             // plaintext < p: m = m_p = L_p(c^(p-1) mod p^2) h_p mod p, the q half and the CRT skipped
@@ -2171,10 +2255,14 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
             if (pipe && (rc = pipe->after(off, cnt))) return rc;
             continue;
         }
-        if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) return rc;
+        if (split) {
+            HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        } else if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) {
+            return rc;
+        }
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,
                            k->cst(k->c_pinv), k->kp, Lc.slot(SL_T1), L, Lc.B);
-        hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2), S,
+        hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, (split ? Lq : Lc).slot(SL_OUTQ), k->cst(k->c_q2), S,
                            k->cst(k->c_qinv2), k->kq, Lc.slot(SL_T2), L, Lc.B);
         // slots C0/C1/C2 are reused for the mod-p / mod-q constants of the tail
         Lc.fill(SL_C0, k->c_hRp); Lc.fill(SL_C1, k->c_hRq); Lc.fill(SL_C2, k->c_qinvRp);
@@ -2193,6 +2281,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         }
         if (pipe && (rc = pipe->after(off, cnt))) return rc;
     }
+    Lc.mm += Lq.mm;
     return end_call(c, Lc);
 }
 

@@ -1,0 +1,67 @@
+"""Small-batch latency path: decrypts (paillier.cpp:141-157) and device-randomness
+CRT encrypts (paillier.cpp:122-139) of at most 65,536 lanes run the mod-q half on
+the context's side stream, in a second slot region, beside the mod-p half.
+
+The split must not change a single bit: the same seeded batch encrypted as a
+large (one-stream) call and as small (two-stream) calls gives identical
+ciphertexts, every one decrypts to its plaintext through both decrypt forms,
+and the full plaintexts agree with the C oracle's decryption.
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import golden_key, load_golden
+
+pytestmark = pytest.mark.gpu
+
+SPLIT_MAX = 65536     # dec_split_lanes() default (one lane per ciphertext at P-1024 and P-2048)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from fedtree_amd.paillier import Device
+    return Device(0)
+
+
+@pytest.mark.parametrize("name", ["ref_gmp_L2048.json", "ref_gmp_L1024.json"])
+def test_split_matches_single_stream(dev, name):
+    from fedtree_amd.paillier import Paillier
+    g = load_golden(name)
+    p, q = golden_key(g)
+    pl = Paillier.from_primes(p, q, dev)
+    rng = np.random.default_rng(11)
+    big = SPLIT_MAX + 1000                       # above the threshold: one stream
+    m = rng.integers(0, 2**64, big, dtype=np.uint64)
+    m[:4] = [0, 1, 2**64 - 1, 2**63]
+    c_big = pl.encrypt_u64(m, seed=77)
+    for cnt in (1, 2, 3, 1000):                  # below: q half on the side stream
+        c_small = pl.encrypt_u64(m[:cnt], seed=77)
+        assert np.array_equal(c_small, c_big[:cnt]), cnt
+        lo, full = pl.decrypt_u64(c_big[:cnt], full=True)
+        assert np.array_equal(lo, m[:cnt]), cnt
+        assert [pyoracle.from_words(w) for w in full] == [int(x) for x in m[:cnt]]
+    assert np.array_equal(pl.decrypt_u64(c_big), m)
+    # decrypt side: a small batch of sums (plaintexts need the full CRT) equals the large-call result
+    s = pl.add_batch(c_big[:2048], c_big[2048:4096])
+    want = (m[:2048] + m[2048:4096])               # mod 2^64
+    _, f_small = pl.decrypt_u64(s, full=True)
+    assert np.array_equal(pl.decrypt_u64(s), want)
+    key = pyoracle.keygen_from_primes(p, q)
+    ints = pyoracle.words_to_ints(s[:8])
+    assert [pyoracle.from_words(w) for w in f_small[:8]] == [pyoracle.decrypt(key, x) for x in ints]
+
+
+def test_split_injected_r_golden(dev):
+    """Injected r keeps the two-stage single-stream encrypt; the split decrypt returns the
+    reference's plaintexts on its golden ciphertexts (all P-2048 cases in one small call
+    and one at a time)."""
+    from fedtree_amd.paillier import Paillier
+    g = load_golden("ref_gmp_L2048.json")
+    p, q = golden_key(g)
+    pl = Paillier.from_primes(p, q, dev)
+    cts = pyoracle.ints_to_words([int(c["c"], 16) for c in g["cases"]], 2 * g["n_words"])
+    want = np.array([c["m"] for c in g["cases"]], dtype=np.uint64)
+    assert np.array_equal(pl.decrypt_u64(cts), want)
+    for i in range(3):
+        assert pl.decrypt_u64(cts[i:i + 1])[0] == want[i]
