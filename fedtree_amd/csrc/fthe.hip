@@ -38,8 +38,10 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 3;
-const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}};
+constexpr int MAX_VARIANTS = 4;
+// s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency)
+const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4}};
+constexpr Shape kLatShape{80, 27, 4};
 
 int variant_index(int S) {
     for (int i = 0; i < MAX_VARIANTS; i++) if (kVariants[i].S == S) return i;
@@ -79,6 +81,16 @@ size_t dec_split_lanes() {
     static size_t v = [] {
         const char *e = getenv("FTHE_DEC_SPLIT");
         return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)65536;
+    }();
+    return v;
+}
+
+// Decrypts of at most this many ciphertexts take the four-lane s80 kernel (Paillier-2048 keys);
+// FTHE_DEC_QUAD overrides, 0 turns it off (A/B).
+size_t dec_quad_max() {
+    static size_t v = [] {
+        const char *e = getenv("FTHE_DEC_QUAD");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)16384;
     }();
     return v;
 }
@@ -185,6 +197,10 @@ struct fthe_key {
     Mpz n, n2, g, p, q, lambda, mu;
     DevMod mn2, mp2, mq2, mp, mq, mp1, mq1;   // mp1/mq1: mod p, q on the small-limb kernel
     Shape sp1{0, 0, 0};
+    // small-batch decrypt on the four-lane s80 kernel (each product spread over a quad of lanes)
+    Shape slat{0, 0, 0};
+    DevMod mp2l, mq2l;
+    int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1;
     int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
     int kp = 0, kq = 0;             // limbs of p, q
     // device constants: one allocation, each its modulus' limb count
@@ -199,7 +215,7 @@ struct fthe_key {
     uint32_t *d_pqwords = nullptr;  // p then q as pq_w u32 words each (device-drawn y_p, y_q)
     int pq_w = 0;
     ~fthe_key() {
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1}) if (d->d_ctx) (void)hipFree(d->d_ctx);
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l}) if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
         if (d_nwords) (void)hipFree(d_nwords);
@@ -235,7 +251,7 @@ struct fthe_key {
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
-    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_pl, pr_dec_ql, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
@@ -648,6 +664,30 @@ static int key_finish(fthe_key *k) {
             d.mul(SL_T5);                                        // * 1 -> out of Montgomery
             d.storex(side ? SL_OUTQ : SL_OUTP); d.end();
             (side ? k->pr_dec_q : k->pr_dec_p) = k->add_prog(d);
+        }
+        // the same exponentiations on the four-lane s80 kernel, for batches that leave the chip idle
+        if (S == 74 && !getenv("FTHE_NO_QUAD_DEC") && p2.bits() + 8 <= (size_t)kLatShape.S * kLatShape.B &&
+            q2.bits() + 8 <= (size_t)kLatShape.S * kLatShape.B) {
+            const Shape ls = kLatShape;
+            if ((rc = upload_mod(k->mp2l, p2, ls))) return rc;
+            if ((rc = upload_mod(k->mq2l, q2, ls))) return rc;
+            auto Q_ = [&](const mpz_t x) { return to_limbs(x, ls.S, ls.B); };
+            k->cl_R2p = k->add_const(Q_(k->mp2l.m.R2)); k->cl_R3p = k->add_const(Q_(k->mp2l.m.R3));
+            k->cl_R2q = k->add_const(Q_(k->mq2l.m.R2)); k->cl_R3q = k->add_const(Q_(k->mq2l.m.R3));
+            k->cl_one = k->add_const(Q_(one));
+            k->cl_p2 = k->add_const(Q_(p2)); k->cl_q2 = k->add_const(Q_(q2));
+            for (int side = 0; side < 2; side++) {
+                Prog d;
+                d.loadx(SL_IN1); d.mul(side ? SL_C3 : SL_C1);
+                d.storex(SL_T0);
+                d.loadx(SL_IN0); d.mul(side ? SL_C2 : SL_C0);
+                d.addslot(SL_T0);
+                d.pow(side ? qm1 : pm1, SL_TAB, SL_SQ, k->w_dec);
+                d.mul(SL_T5);
+                d.storex(side ? SL_OUTQ : SL_OUTP); d.end();
+                (side ? k->pr_dec_ql : k->pr_dec_pl) = k->add_prog(d);
+            }
+            k->slat = ls;
         }
         for (int side = 0; side < 2; side++) {
             Prog d; d.loadx(side ? SL_T2 : SL_T1); d.mul(side ? SL_C1 : SL_C0);
@@ -2205,13 +2245,31 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
     // Batches that leave most of the chip idle (a GHPair from decrypt_gh, one tree node's sums) run the
     // c^(q-1) mod q^2 exponentiation on the side stream, in a second slot region, beside c^(p-1) mod p^2:
     // one exponentiation of latency instead of two.  Large batches fill the chip with one half at a time.
+    // Smaller batches still (<= 16,384 ciphertexts) take both exponentiations on the four-lane s80 kernel,
+    // each Montgomery product spread over a quad of lanes (~3x less latency per exponentiation), and
+    // hand c^(P-1) mod P^2 back to the s74 layout for the unchanged L-function / CRT tail.
     const int vi = variant_index(k->spq.S);
-    const bool split = !short_pt && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    const bool quad = k->slat.S && count > 0 && count <= dec_quad_max();
+    const bool split = !quad && !short_pt && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, k->spq);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
+    Launch Lp4 = Lc, Lq4 = Lc;             // quad: s80 regions for the p and q halves (slots1)
+    const int wl = (kLatShape.S * kLatShape.B + 31) / 32;   // u32 words of an s80 row
+    uint32_t *rowp = nullptr, *rowq = nullptr;
+    if (quad) {
+        if (count > (size_t)L) return FTHE_ERR_ARG;        // one chunk by construction
+        const size_t reg = (size_t)nsl * kLatShape.S * L * 4;
+        if ((rc = c->slots1.ensure(2 * reg))) return rc;
+        if ((rc = c->scratch.ensure((size_t)2 * L * wl * 4))) return rc;
+        rowp = (uint32_t *)c->scratch.p; rowq = rowp + (size_t)L * wl;
+        Lp4.S = kLatShape.S; Lp4.B = kLatShape.B; Lp4.base = c->slots1.p;
+        Lq4 = Lp4; Lq4.base = (uint8_t *)c->slots1.p + reg; Lq4.st = c->side;
+        Lp4.fill(SL_C0, k->cl_R2p); Lp4.fill(SL_C1, k->cl_R3p); Lp4.fill(SL_T5, k->cl_one);
+        if (!short_pt) { Lq4.fill(SL_C2, k->cl_R2q); Lq4.fill(SL_C3, k->cl_R3q); Lq4.fill(SL_T5, k->cl_one); }
+    }
     Launch Lq = Lc;                        // q half: region 2 of the slots, side stream
     if (split) {
         Lq.base = (uint8_t *)Lc.base + (size_t)nsl * S * L * 4;
@@ -2228,6 +2286,30 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         Lc.live = cnt; Lq.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
         const uint32_t *src = ct + off * cw;
+        if (quad) {
+            const int S4 = kLatShape.S, B4 = kLatShape.B;
+            Lp4.live = cnt; Lq4.live = cnt;
+            pack_rows(c->stream, src, cw, cnt, 0, Lp4.slot(SL_IN0), S4, L, B4);
+            pack_rows(c->stream, src, cw, cnt, B4 * S4, Lp4.slot(SL_IN1), S4, L, B4);
+            if (!short_pt) {
+                pack_rows(c->stream, src, cw, cnt, 0, Lq4.slot(SL_IN0), S4, L, B4);
+                pack_rows(c->stream, src, cw, cnt, B4 * S4, Lq4.slot(SL_IN1), S4, L, B4);
+                HIPOK(hipEventRecord(c->ev_fork, c->stream));
+                HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+                if ((rc = Lq4.prog(k->pr_dec_ql, k->mq2l))) return rc;
+                HIPOK(hipEventRecord(c->ev_join, c->side));
+            }
+            if ((rc = Lp4.prog(k->pr_dec_pl, k->mp2l))) return rc;
+            // canonical c^(P-1) mod P^2 rows -> the s74 slots the tail reads
+            unpack_rows(c->stream, Lp4.slot(SL_OUTP), k->cst(k->cl_p2), S4, L, cnt, rowp, wl, B4);
+            pack_rows(c->stream, rowp, wl, cnt, 0, Lc.slot(SL_OUTP), S, L, Lc.B);
+            if (!short_pt) {
+                HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                unpack_rows(c->stream, Lq4.slot(SL_OUTQ), k->cst(k->cl_q2), S4, L, cnt, rowq, wl, B4);
+                pack_rows(c->stream, rowq, wl, cnt, 0, Lc.slot(SL_OUTQ), S, L, Lc.B);
+            }
+            Lc.mm += Lp4.mm + Lq4.mm; Lp4.mm = Lq4.mm = 0;
+        } else {
         pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
         pack_rows(c->stream, src, cw, cnt, Lc.B * S,
                            Lc.slot(SL_IN1), S, L, Lc.B);
@@ -2240,6 +2322,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
             HIPOK(hipEventRecord(c->ev_join, c->side));
         }
         if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
+        }
         if (short_pt) {
             // plaintext < p: m = m_p = L_p(c^(p-1) mod p^2) h_p mod p, the q half and the CRT skipped
             hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,
@@ -2257,7 +2340,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         }
         if (split) {
             HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-        } else if ((rc = Lc.prog(k->pr_dec_q, k->mq2))) {
+        } else if (!quad && (rc = Lc.prog(k->pr_dec_q, k->mq2))) {
             return rc;
         }
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,

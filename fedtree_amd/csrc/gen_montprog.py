@@ -533,6 +533,10 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     index; kernarg limb_stride = L*4 for L ciphertexts."""
     assert S % 4 == 0 and U % 2 == 0
     Q = S // 4
+    # row I/O (LOADW/MULW/STOREW and the gathers) is laid out for 152 limbs of 27 bits
+    # (4096-bit rows of n^2); other shapes (the 80-limb mod-p^2 latency kernel) dispatch
+    # the slot ops only and end the program on any other opcode
+    rowio = Q == 38 and B == 27
     MASK = (1 << B) - 1
     NTRIPS, TAIL = S // U, S % U
     # VGPRs: v0 tid (set-up) then the lane's A-write base, v1 lane offset in a
@@ -621,10 +625,11 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_add_u32 s6, s6, 8')
     e('  s_addc_u32 s7, s7, 0')
     e('  s_waitcnt lgkmcnt(0)')
-    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'),
-                      (5, '.Laddslot'), (6, '.Laddsmall'), (7, '.Lloadw'), (8, '.Lmulw'),
-                      (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg'), (14, '.Lloadwd'), (15, '.Lmulwd'),
-                      (16, '.Lloadwd16'), (17, '.Lmulwd16')):
+    ops = ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (5, '.Laddslot'), (6, '.Laddsmall'))
+    if rowio:
+        ops += ((7, '.Lloadw'), (8, '.Lmulw'), (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg'),
+                (14, '.Lloadwd'), (15, '.Lmulwd'), (16, '.Lloadwd16'), (17, '.Lmulwd16'))
+    for code, lab in ops:
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -742,7 +747,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     # written in place of the layout-conversion kernels.  Row table entry t
     # (kernarg 32) points at row 0 of this launch; ciphertext g's lane k owns
     # words [32k, 32k+32) and the radix-2^B limbs [kQ, kQ+Q) = bits [1026k, 1026k+1026).
-    assert Q == 38 and B == 27, "row I/O is laid out for 152 limbs of 27 bits (4096-bit rows)"
+    # (row I/O is emitted only for this shape; other quad shapes run slot programs alone)
     W0 = TB               # 33 row words (T window is free outside a product)
     A0 = TB + 34          # 38 limbs of a MULW operand
     D0 = TB               # STOREW: X - N
@@ -792,6 +797,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
                 e(f'  v_alignbit_b32 {dst(j)}, v{W0 + a + 1}, v{W0 + a}, {sh}')
                 e(f'  v_and_b32_e32 {dst(j)}, {hex(MASK)}, {dst(j)}')
 
+    mark = len(o)
     e('.Lloadw:')
     row_ptr()
     live_mask()
@@ -951,6 +957,9 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_waitcnt vmcnt(0)')
     restore_exec()
     e('  s_branch .Lprog')
+
+    if not rowio:
+        del o[mark:]
 
     def iteration(u):
         ai = f"v{V_AI[u % 2]}"
