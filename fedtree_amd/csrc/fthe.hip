@@ -153,6 +153,8 @@ struct fthe_ctx {
     hipStream_t copy = nullptr;               // host<->device staging copies, overlapped with compute
     hipStream_t side = nullptr;               // second compute stream: the q half of small decrypts
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int n_cu = 256;                           // compute units (small-batch spreading)
+    int static_lds[MAX_VARIANTS] = {};        // per-variant static LDS bytes per workgroup
     PinBuf stage_out[2], stage_in[2];
     hipEvent_t ev_done[2] = {}, ev_copied[2] = {}, ev_in[2] = {};
     hipModule_t mod[MAX_VARIANTS] = {};
@@ -370,9 +372,11 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         char name[64];
         snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
+        HIPOK(hipFuncGetAttribute(&c->static_lds[i], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, c->fn[i]));
     }
     HIPOK(hipEventCreate(&c->ev0));
     HIPOK(hipEventCreate(&c->ev1));
+    HIPOK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     *out = c.release();
     return FTHE_OK;
 }
@@ -965,8 +969,11 @@ extern "C" int fthe_key_export(const fthe_key *k, uint32_t *n, uint32_t *lambda,
 namespace {
 
 // Launch the montprog kernel, bracketed by profiling events when enabled.
+constexpr int kSpreadLds = 84 * 1024;   // > 80 KB: one workgroup per CU (gfx950: 160 KB LDS per CU)
+
 int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, const DevMod &mod, double lane_mm,
-                    size_t live, const void *const *rows = nullptr, int nrows = 0, hipStream_t st = nullptr) {
+                    size_t live, const void *const *rows = nullptr, int nrows = 0, hipStream_t st = nullptr,
+                    bool spread = false) {
     if (!st) st = c->stream;
     struct {
         void *s; const void *p; const void *cx; uint32_t ls, ss; uint32_t live, pad; const void *rows[16];
@@ -997,7 +1004,13 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
         ev = &c->prof_ev[c->prof_used++];
         HIPOK(hipEventRecord(ev->first, st));
     }
-    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg) != hipSuccess)
+    // Two concurrent small launches (the p and q halves on two streams) would otherwise pack two
+    // workgroups onto one CU -- two waves per SIMD, each at half speed.  Dynamic LDS beyond half
+    // the CU's 160 KB keeps one workgroup per CU while both launches fit on the chip together.
+    unsigned shm = 0;
+    if (spread && 2 * blocks <= (unsigned)c->n_cu && c->static_lds[vi] < kSpreadLds)
+        shm = (unsigned)(kSpreadLds - c->static_lds[vi]);
+    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, 256, 1, 1, shm, st, nullptr, cfg) != hipSuccess)
         return FTHE_ERR_HIP;
     if (ev) {
         HIPOK(hipEventRecord(ev->second, st));
@@ -1024,18 +1037,19 @@ struct Launch {
     fthe_ctx *c; const fthe_key *k; int L; int S; int B; double mm = 0; size_t live = 0;
     void *base = nullptr;          // slot region (c->slots, or c->slots1 for small-modulus programs)
     hipStream_t st = nullptr;      // compute stream (null: the context's main stream)
+    bool spread = false;           // one workgroup per CU (small concurrent launches)
     uint32_t *slot(int s) const { return (uint32_t *)base + (size_t)s * S * L; }
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
     int prog(const fthe_key::PH &ph, const DevMod &mod, const void *const *rows = nullptr, int nrows = 0) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows, st);
+        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows, st, spread);
         if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;
     }
     int prog_raw(const uint32_t *p, double pmm, const DevMod &mod, const void *const *rows, int nrows) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, base, S, L, p, mod, pmm, live, rows, nrows, st);
+        int rc = launch_montprog(c, base, S, L, p, mod, pmm, live, rows, nrows, st, spread);
         if (rc) return rc;
         mm += pmm * (double)live;
         return FTHE_OK;
@@ -1284,6 +1298,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     if (split) {
         Lq.base = (uint8_t *)Lc.base + (size_t)nsl * S * L * 4;
         Lq.st = c->side;
+        Lc.spread = Lq.spread = true;
         HIPOK(hipEventRecord(c->ev_fork, c->stream));
         HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
         Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_nRq);
@@ -2265,7 +2280,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         if ((rc = c->slots1.ensure(2 * reg))) return rc;
         if ((rc = c->scratch.ensure((size_t)2 * L * wl * 4))) return rc;
         rowp = (uint32_t *)c->scratch.p; rowq = rowp + (size_t)L * wl;
-        Lp4.S = kLatShape.S; Lp4.B = kLatShape.B; Lp4.base = c->slots1.p;
+        Lp4.S = kLatShape.S; Lp4.B = kLatShape.B; Lp4.base = c->slots1.p; Lp4.spread = !short_pt;
         Lq4 = Lp4; Lq4.base = (uint8_t *)c->slots1.p + reg; Lq4.st = c->side;
         Lp4.fill(SL_C0, k->cl_R2p); Lp4.fill(SL_C1, k->cl_R3p); Lp4.fill(SL_T5, k->cl_one);
         if (!short_pt) { Lq4.fill(SL_C2, k->cl_R2q); Lq4.fill(SL_C3, k->cl_R3q); Lq4.fill(SL_T5, k->cl_one); }
@@ -2274,6 +2289,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
     if (split) {
         Lq.base = (uint8_t *)Lc.base + (size_t)nsl * S * L * 4;
         Lq.st = c->side;
+        Lc.spread = Lq.spread = true;
         HIPOK(hipEventRecord(c->ev_fork, c->stream));
         HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
         Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_R3q); Lq.fill(SL_T5, k->c_one);
