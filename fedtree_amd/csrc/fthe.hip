@@ -202,7 +202,7 @@ struct fthe_key {
     // small-batch decrypt on the four-lane s80 kernel (each product spread over a quad of lanes)
     Shape slat{0, 0, 0};
     DevMod mp2l, mq2l;
-    int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1;
+    int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1, cl_nRp = -1, cl_nRq = -1;
     int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
     int kp = 0, kq = 0;             // limbs of p, q
     // device constants: one allocation, each its modulus' limb count
@@ -253,7 +253,7 @@ struct fthe_key {
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
-    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_pl, pr_dec_ql, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
+    PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_pl, pr_dec_ql, pr_enc_pl, pr_enc_ql, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
@@ -690,6 +690,19 @@ static int key_finish(fthe_key *k) {
                 d.mul(SL_T5);
                 d.storex(side ? SL_OUTQ : SL_OUTP); d.end();
                 (side ? k->pr_dec_ql : k->pr_dec_pl) = k->add_prog(d);
+            }
+            // direct-y encrypt stage B, (1 + m n) y^P mod P^2, stopping at c_P (the CRT tail runs on s74)
+            k->cl_nRp = k->add_const(k->mp2l.m.mont(np)); k->cl_nRq = k->add_const(k->mq2l.m.mont(nq));
+            const int wB = best_window(std::max(k->p.bits(), k->q.bits()));
+            for (int side = 0; side < 2; side++) {
+                Prog e;
+                e.loadx(side ? SL_T4 : SL_T3); e.mul(side ? SL_C2 : SL_C0);
+                e.pow(side ? k->q : k->p, SL_TAB, SL_SQ, wB);
+                e.storex(SL_SAVED);
+                e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);
+                e.addsmall(1); e.mul(SL_SAVED);
+                e.storex(side ? SL_OUTQ : SL_OUTP); e.end();
+                (side ? k->pr_enc_ql : k->pr_enc_pl) = k->add_prog(e);
             }
             k->slat = ls;
         }
@@ -1273,7 +1286,9 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     const bool direct_y = crt && !r && !no_direct;
     // small batches: the q half on the side stream in a second slot region, as decrypt_impl
     const int vi = variant_index(k->spq.S);
-    const bool split = direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    // and smaller ones both halves on the four-lane s80 kernel (as decrypt_impl)
+    const bool quad = direct_y && k->slat.S && count > 0 && count <= dec_quad_max();
+    const bool split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2);
@@ -1286,7 +1301,10 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     // reference's uniform r, independently for P = p, q (CRT).  FTHE_NO_DIRECT_Y=1
     // keeps the explicit r (A/B).  Injected r always takes both stages (bit-exact).
     // scratch: AoS r words for the device RNG
-    if (!r && (rc = c->scratch.ensure((size_t)L * nw * 4 * (direct_y ? 2 : 1)))) return rc;
+    const int wl = (kLatShape.S * kLatShape.B + 31) / 32;   // u32 words of an s80 row
+    if (!r && (rc = c->scratch.ensure(std::max((size_t)L * nw * 4 * (direct_y ? 2 : 1),
+                                               quad ? (size_t)L * (2 * k->pq_w + 2 * wl) * 4 : (size_t)0))))
+        return rc;
     RngKey rk{};
     if (!r) {
         uint64_t s = rng_seed ? rng_seed : urandom64();
@@ -1302,6 +1320,16 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         HIPOK(hipEventRecord(c->ev_fork, c->stream));
         HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
         Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_nRq);
+    }
+    Launch Lp4 = Lc, Lq4 = Lc;         // quad: s80 regions for the p and q halves (slots1)
+    if (quad) {
+        if (count > (size_t)L) return FTHE_ERR_ARG;        // one chunk by construction
+        const size_t reg = (size_t)nsl * kLatShape.S * L * 4;
+        if ((rc = c->slots1.ensure(2 * reg))) return rc;
+        Lp4.S = kLatShape.S; Lp4.B = kLatShape.B; Lp4.base = c->slots1.p; Lp4.spread = true;
+        Lq4 = Lp4; Lq4.base = (uint8_t *)c->slots1.p + reg; Lq4.st = c->side;
+        Lp4.fill(SL_C0, k->cl_R2p); Lp4.fill(SL_C1, k->cl_nRp);
+        Lq4.fill(SL_C2, k->cl_R2q); Lq4.fill(SL_C3, k->cl_nRq);
     }
     if (direct_y) {
         Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
@@ -1336,6 +1364,36 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
             pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lc.slot(SL_T3), S, L, Lc.B);
             pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lc.slot(SL_T4), S, L, Lc.B);
+            if (quad) {
+                const int S4 = kLatShape.S, B4 = kLatShape.B;
+                uint32_t *rowp = yq + (size_t)L * k->pq_w, *rowq = rowp + (size_t)L * wl;
+                Lp4.live = cnt; Lq4.live = cnt;
+                m.pack(c->stream, Lc.grid(), off, cnt, Lp4.slot(SL_IN1), S4, L, B4);
+                m.pack(c->stream, Lc.grid(), off, cnt, Lq4.slot(SL_IN1), S4, L, B4);
+                pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lp4.slot(SL_T3), S4, L, B4);
+                pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lq4.slot(SL_T4), S4, L, B4);
+                HIPOK(hipEventRecord(c->ev_fork, c->stream));
+                HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+                if ((rc = Lq4.prog(k->pr_enc_ql, k->mq2l))) return rc;
+                HIPOK(hipEventRecord(c->ev_join, c->side));
+                if ((rc = Lp4.prog(k->pr_enc_pl, k->mp2l))) return rc;
+                // canonical c_p, c_q rows -> the s74 slots of the CRT tail
+                unpack_rows(c->stream, Lp4.slot(SL_OUTP), k->cst(k->cl_p2), S4, L, cnt, rowp, wl, B4);
+                pack_rows(c->stream, rowp, wl, cnt, 0, Lc.slot(SL_OUTP), S, L, Lc.B);
+                HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                unpack_rows(c->stream, Lq4.slot(SL_OUTQ), k->cst(k->cl_q2), S4, L, cnt, rowq, wl, B4);
+                pack_rows(c->stream, rowq, wl, cnt, 0, Lc.slot(SL_OUTQ), S, L, Lc.B);
+                Lc.mm += Lp4.mm + Lq4.mm; Lp4.mm = Lq4.mm = 0;
+                hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ),
+                                   k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
+                if ((rc = Lc.prog(k->pr_enc_tail, k->mp2))) return rc;
+                hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S,
+                                   L, Lc.B);
+                mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S, k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt,
+                            out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+                if (pipe && (rc = pipe->after(off, cnt))) return rc;
+                continue;
+            }
             if (split) {
                 m.pack(c->stream, Lc.grid(), off, cnt, Lq.slot(SL_IN1), S, L, Lc.B);
                 pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lq.slot(SL_T4), S, L, Lc.B);
