@@ -56,9 +56,12 @@ const char *fthe_strerror(int status);
 
 /* ---- device context (one HIP stream + workspace) ------------------------ */
 /* Every call is ordered on the context stream.  Small decrypts and device-
- * randomness encrypts (<= 65,536 lanes) fork their mod-q half onto a private
- * side stream and join it back before any output is written, so callers see
- * one stream: fthe_ctx_sync / an event on fthe_ctx_stream cover all of it. */
+ * randomness encrypts (<= 65,536 lanes; <= 16,384 ciphertexts of a
+ * Paillier-2048 key also switch to the four-lane s80 kernel) fork their mod-q
+ * half onto a private side stream and join it back before any output is
+ * written, so callers see one stream: fthe_ctx_sync / an event on
+ * fthe_ctx_stream cover all of it.  Results are bit-identical whichever path
+ * a batch size takes. */
 int   fthe_ctx_create(int device, fthe_ctx **out);
 void  fthe_ctx_destroy(fthe_ctx *ctx);
 int   fthe_ctx_sync(fthe_ctx *ctx);
