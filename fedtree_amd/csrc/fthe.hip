@@ -2384,18 +2384,17 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
             }
             Lc.mm += Lp4.mm + Lq4.mm; Lp4.mm = Lq4.mm = 0;
         } else {
-        pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
-        pack_rows(c->stream, src, cw, cnt, Lc.B * S,
-                           Lc.slot(SL_IN1), S, L, Lc.B);
-        if (split) {
-            pack_rows(c->stream, src, cw, cnt, 0, Lq.slot(SL_IN0), S, L, Lc.B);
-            pack_rows(c->stream, src, cw, cnt, Lc.B * S, Lq.slot(SL_IN1), S, L, Lc.B);
-            HIPOK(hipEventRecord(c->ev_fork, c->stream));
-            HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-            if ((rc = Lq.prog(k->pr_dec_q, k->mq2))) return rc;
-            HIPOK(hipEventRecord(c->ev_join, c->side));
-        }
-        if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
+            pack_rows(c->stream, src, cw, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+            pack_rows(c->stream, src, cw, cnt, Lc.B * S, Lc.slot(SL_IN1), S, L, Lc.B);
+            if (split) {
+                pack_rows(c->stream, src, cw, cnt, 0, Lq.slot(SL_IN0), S, L, Lc.B);
+                pack_rows(c->stream, src, cw, cnt, Lc.B * S, Lq.slot(SL_IN1), S, L, Lc.B);
+                HIPOK(hipEventRecord(c->ev_fork, c->stream));
+                HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+                if ((rc = Lq.prog(k->pr_dec_q, k->mq2))) return rc;
+                HIPOK(hipEventRecord(c->ev_join, c->side));
+            }
+            if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
         }
         if (short_pt) {
             // plaintext < p: m = m_p = L_p(c^(p-1) mod p^2) h_p mod p, the q half and the CRT skipped
