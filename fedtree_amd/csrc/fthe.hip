@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <functional>
 #include <map>
 #include <memory>
@@ -190,8 +191,26 @@ struct DevMod {
     }
 };
 
+// Group-commit queue of fthe_decrypt_shared (one per key, created on first use).
+struct DecReq {
+    const uint32_t *ct; size_t count; uint64_t *m_low; uint32_t *m_full; bool short_pt;
+    int rc = FTHE_OK; bool done = false;
+};
+struct Coalescer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<DecReq *> pending;
+    bool leader = false;
+    fthe_ctx *ctx = nullptr;                 // the key's own context, used by one leader at a time
+    std::vector<uint32_t> ct, full;
+    std::vector<uint64_t> lo;
+    ~Coalescer() { if (ctx) fthe_ctx_destroy(ctx); }
+};
+
 // A named constant (S limbs) on the device.
 struct fthe_key {
+    std::mutex co_mu;
+    std::unique_ptr<Coalescer> co;           // released first in ~fthe_key (its context drains there)
     int device = 0;
     Shape spq{0, 0, 0}, sn2{0, 0, 0};   // kernel shapes: mod p^2/q^2/p/q and mod n^2
     int n_bits = 0, n_words = 0;
@@ -217,6 +236,7 @@ struct fthe_key {
     uint32_t *d_pqwords = nullptr;  // p then q as pq_w u32 words each (device-drawn y_p, y_q)
     int pq_w = 0;
     ~fthe_key() {
+        co.reset();
         for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l}) if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
@@ -3049,6 +3069,73 @@ static int decrypt_host(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
 
 extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full) {
     return decrypt_host(k, c, ct, count, m_low, m_full, false);
+}
+
+// One leader runs everything pending (its own request included) as at most two batched calls
+// (full / short), then hands leadership to a caller still waiting.
+static void coalesced_batch(fthe_key *k, Coalescer *co, const std::vector<DecReq *> &batch) {
+    const size_t cw = 2 * (size_t)k->n_words, nw = k->n_words;
+    int rc0 = FTHE_OK;
+    if (!co->ctx) rc0 = fthe_ctx_create(k->device, &co->ctx);
+    for (int kind = 0; kind < 2; kind++) {
+        size_t tot = 0;
+        bool want_full = false;
+        for (DecReq *r : batch)
+            if (r->short_pt == (kind == 1)) { tot += r->count; want_full |= r->m_full != nullptr; }
+        if (!tot) continue;
+        int rc = rc0;
+        if (!rc) {
+            co->ct.resize(tot * cw); co->lo.resize(tot);
+            if (want_full) co->full.resize(tot * nw);
+            size_t at = 0;
+            for (DecReq *r : batch)
+                if (r->short_pt == (kind == 1)) { memcpy(&co->ct[at * cw], r->ct, r->count * cw * 4); at += r->count; }
+            rc = decrypt_host(k, co->ctx, co->ct.data(), tot, co->lo.data(), want_full ? co->full.data() : nullptr,
+                              kind == 1);
+        }
+        size_t at = 0;
+        for (DecReq *r : batch) {
+            if (r->short_pt != (kind == 1)) continue;
+            r->rc = rc;
+            if (!rc) {
+                if (r->m_low) memcpy(r->m_low, &co->lo[at], r->count * 8);
+                if (r->m_full) memcpy(r->m_full, &co->full[at * nw], r->count * nw * 4);
+            }
+            at += r->count;
+        }
+    }
+}
+
+extern "C" int fthe_decrypt_shared(fthe_key *k, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full,
+                                   int short_pt) {
+    if (!k || (!ct && count)) return FTHE_ERR_ARG;
+    if (!k->priv) return FTHE_ERR_NOPRIV;
+    if (!count) return FTHE_OK;
+    Coalescer *co;
+    {
+        std::lock_guard<std::mutex> g(k->co_mu);
+        if (!k->co) k->co.reset(new Coalescer);
+        co = k->co.get();
+    }
+    DecReq r{ct, count, m_low, m_full, short_pt != 0};
+    std::unique_lock<std::mutex> lk(co->mu);
+    co->pending.push_back(&r);
+    for (;;) {
+        if (r.done) return r.rc;
+        if (!co->leader) {
+            co->leader = true;
+            std::vector<DecReq *> batch;
+            batch.swap(co->pending);                 // includes r
+            lk.unlock();
+            coalesced_batch(k, co, batch);
+            lk.lock();
+            for (DecReq *q : batch) q->done = true;
+            co->leader = false;
+            co->cv.notify_all();
+            return r.rc;
+        }
+        co->cv.wait(lk);
+    }
 }
 
 extern "C" int fthe_decrypt_short(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t count, uint64_t *m_low,

@@ -346,6 +346,18 @@ class Paillier:
         _lib.check(fn(self._key, self.dev.ctx, _ptr(c), cnt, _ptr(low), _ptr(fullw)), "decrypt")
         return (low, fullw) if full else low
 
+    def decrypt_u64_shared(self, c, full=False, short=False):
+        """decrypt_u64 through the key's coalescing queue (fthe_decrypt_shared): safe to call from
+        many threads on one Paillier object; concurrent calls are merged into one batch
+        (decrypt_gh per node from OpenMP threads, FLtrainer.cpp:758-764)."""
+        c = np.ascontiguousarray(c, dtype=np.uint32).reshape(-1, self._cw())
+        cnt = len(c)
+        low = np.zeros(cnt, dtype=np.uint64)
+        fullw = np.zeros((cnt, self.n_words), dtype=np.uint32) if full else None
+        _lib.check(self.lib.fthe_decrypt_shared(self._key, _ptr(c), cnt, _ptr(low), _ptr(fullw), int(short)),
+                   "decrypt_shared")
+        return (low, fullw) if full else low
+
     def add_batch(self, a, b):
         """x*y mod n^2 (paillier.cpp:103), alias-safe."""
         a = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self._cw())

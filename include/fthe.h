@@ -233,6 +233,17 @@ int fthe_decrypt_short_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size
 int fthe_decrypt_short(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t count,
                        uint64_t *m_low, uint32_t *m_full);
 
+/* Coalescing host-resident decrypt for many concurrent callers of one key:
+ * Server::decrypt_gh per tree node from OpenMP threads (server.h:69-78,
+ * FLtrainer.cpp:758-764).  Thread-safe, no context argument: requests that
+ * arrive while a batch runs are merged into the next one, run by one of the
+ * waiting callers on a context the key owns, so N concurrent single-pair
+ * calls cost about two batch latencies instead of N (small launches from
+ * separate contexts share the process's few hardware queues and serialise).
+ * short_pt != 0: fthe_decrypt_short semantics.  Same results as fthe_decrypt. */
+int fthe_decrypt_shared(fthe_key *key, const uint32_t *c, size_t count,
+                        uint64_t *m_low, uint32_t *m_full, int short_pt);
+
 /* ---- homomorphic add: x*y mod n^2 (paillier.cpp:103) ------------------------
  * Replaces Paillier::add / Paillier_GMP::add (paillier_gmp.cpp:16) and
  * Paillier_GPU::add (paillier_gpu.cu:58).  Alias-safe: out may equal a or b

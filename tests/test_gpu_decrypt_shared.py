@@ -1,0 +1,81 @@
+"""fthe_decrypt_shared: the coalescing decrypt for concurrent callers of one key
+(Server::decrypt_gh per node from OpenMP threads, server.h:69-78, FLtrainer.cpp:758-764).
+
+Many threads on ONE Paillier object, mixed full / short / full-plaintext requests of
+different sizes: every caller gets exactly its own plaintexts (the batches are merged
+and scattered back), the same as fthe_decrypt; argument errors as the other decrypts.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import golden_key, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pl():
+    from fedtree_amd.paillier import Device, Paillier
+    g = load_golden("ref_gmp_L2048.json")
+    p, q = golden_key(g)
+    return Paillier.from_primes(p, q, Device(0))
+
+
+def test_shared_matches_decrypt(pl):
+    rng = np.random.default_rng(5)
+    m = rng.integers(0, 2**64, 300, dtype=np.uint64)
+    c = pl.encrypt_u64(m, seed=9)
+    lo, full = pl.decrypt_u64_shared(c, full=True)
+    assert np.array_equal(lo, m)
+    assert np.array_equal(full, pl.decrypt_u64(c, full=True)[1])
+    assert np.array_equal(pl.decrypt_u64_shared(c, short=True), m)
+    assert len(pl.decrypt_u64_shared(c[:0])) == 0
+
+
+def test_shared_many_threads(pl):
+    rng = np.random.default_rng(6)
+    T, R = 24, 3
+    sizes = [2 if i % 3 else int(rng.integers(1, 40)) for i in range(T)]
+    ms = [rng.integers(0, 2**64, s, dtype=np.uint64) for s in sizes]
+    cs = [pl.encrypt_u64(m, seed=100 + i) for i, m in enumerate(ms)]
+    # sums decrypt to plaintexts above 2^64: full plaintexts must come back per caller too
+    sums = [pl.add_batch(c, c) for c in cs]
+    bad = []
+    go = threading.Barrier(T)
+
+    def work(i):
+        try:
+            go.wait()
+            for r in range(R):
+                kind = (i + r) % 3
+                if kind == 0:
+                    ok = np.array_equal(pl.decrypt_u64_shared(cs[i]), ms[i])
+                elif kind == 1:
+                    ok = np.array_equal(pl.decrypt_u64_shared(cs[i], short=True), ms[i])
+                else:
+                    _, f = pl.decrypt_u64_shared(sums[i], full=True)
+                    want = [2 * int(x) for x in ms[i]]
+                    got = [int.from_bytes(w.astype("<u4").tobytes(), "little") for w in f]
+                    ok = got == want
+                if not ok:
+                    bad.append((i, r))
+        except Exception as e:
+            bad.append((i, repr(e)))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not bad, bad
+
+
+def test_shared_public_key_rejected(pl):
+    from fedtree_amd import _lib
+    from fedtree_amd.paillier import Paillier
+    pub = Paillier.from_public(pl.modulus, pl.dev)
+    c = pl.encrypt_u64(np.array([1], dtype=np.uint64), seed=1)
+    with pytest.raises(_lib.FtheError):
+        pub.decrypt_u64_shared(c)
