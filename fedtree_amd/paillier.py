@@ -614,12 +614,14 @@ class GHPairs:
         self.encrypted = True
         return self
 
-    def homo_decrypt(self, pl, short=False):
+    def homo_decrypt(self, pl, short=False, shared=False):
         """GHPair::homo_decrypt (common.h:136-146): g = (float)(long)dec / 1e6.
-        short: plaintexts known < p (codec values and their sums): p half of the CRT only."""
+        short: plaintexts known < p (codec values and their sums): p half of the CRT only.
+        shared: through the key's coalescing queue (thread-safe on one key, fthe_decrypt_shared)."""
         if not self.encrypted:
             return self
-        low = pl.decrypt_u64(np.concatenate([self.g_enc, self.h_enc]), short=short)
+        dec = pl.decrypt_u64_shared if shared else pl.decrypt_u64
+        low = dec(np.concatenate([self.g_enc, self.h_enc]), short=short)
         self.g = decode_fixed(low[:len(self)])
         self.h = decode_fixed(low[len(self):])
         self.encrypted = False
@@ -710,8 +712,10 @@ class HEServer:
         return encrypted.homo_decrypt(self.paillier, short=short)
 
     def decrypt_gh(self, gh):
-        """server.h:69-78 (single pair, as a batch of one)."""
-        return gh.homo_decrypt(self.paillier)
+        """server.h:69-78 (single pair).  FedTree calls it per tree node from OpenMP threads
+        (FLtrainer.cpp:758-764): it goes through the key's coalescing queue, so concurrent
+        calls share one launch and threads need no context of their own."""
+        return gh.homo_decrypt(self.paillier, shared=True)
 
 
 class HEParty:

@@ -198,8 +198,9 @@ public:
         fthe_shim::to_words(message.g_enc, &c[0], cw);
         fthe_shim::to_words(message.h_enc, &c[cw], cw);
         uint64_t m[2];
-        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key_, fthe_shim::thread_ctx(), c.data(), 2, m,
-                                                                         nullptr), "decrypt");
+        // Server::decrypt_gh runs this per tree node from OpenMP threads (FLtrainer.cpp:758-764):
+        // the key's coalescing queue merges the concurrent pairs into one launch
+        fthe_shim::check(fthe_decrypt_shared(key_, c.data(), 2, m, nullptr, dec_short ? 1 : 0), "decrypt");
         message.g = fthe_shim::decode(m[0]);
         message.h = fthe_shim::decode(m[1]);
     }
