@@ -271,6 +271,30 @@ def main():
         for _ in range(5):
             pl.decrypt_u64(ch, short=True)
         secondary["single_pair_latency_ms"]["decrypt_short"] = round((time.perf_counter() - t0) / 5 * 1e3, 2)
+        # decrypt_gh from 32 OpenMP-style threads on one key: merged by the key's coalescing queue
+        import threading
+        nthr, rounds = 32, 4
+        cts = [pl.encrypt_u64(np.array([7 * i, 11 * i], dtype=np.uint64), seed=50 + i) for i in range(nthr)]
+        ok = [True] * nthr
+        go = threading.Barrier(nthr + 1)
+
+        def _dgh(i):
+            go.wait()
+            for _ in range(rounds):
+                ok[i] &= bool(np.array_equal(pl.decrypt_u64_shared(cts[i]), [7 * i, 11 * i]))
+
+        ths = [threading.Thread(target=_dgh, args=(i,)) for i in range(nthr)]
+        for t in ths:
+            t.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for t in ths:
+            t.join()
+        ms = (time.perf_counter() - t0) * 1e3 / rounds
+        secondary["concurrent_decrypt_gh"] = {"threads": nthr, "ms_per_round": round(ms, 2),
+                                              "pairs_per_s": round(nthr / ms * 1e3), "ok": all(ok),
+                                              "note": "fthe_decrypt_shared: concurrent single-pair calls on one key "
+                                                      "merged into one launch (group commit)"}
         # key generation (homo_init; re-run every round in the vertical simulation, FLtrainer.cpp:556):
         # host prime search on up to 16 threads + device key set-up
         t0 = time.perf_counter()
