@@ -75,6 +75,7 @@ _PROTOS = {
     "fthe_decrypt_short_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_decrypt_short": (_I, [_P, _P, _P, _SZ, _P, _P]),
     "fthe_decrypt_shared": (_I, [_P, _P, _SZ, _P, _P, _I]),
+    "fthe_encrypt_shared": (_I, [_P, _P, _SZ, _P, _I]),
     "fthe_add_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_to_mont_dev": (_I, [_P, _P, _P, _SZ, _P]),
     "fthe_from_mont_dev": (_I, [_P, _P, _P, _SZ, _P]),

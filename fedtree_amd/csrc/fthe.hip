@@ -196,15 +196,23 @@ struct DecReq {
     const uint32_t *ct; size_t count; uint64_t *m_low; uint32_t *m_full; bool short_pt;
     int rc = FTHE_OK; bool done = false;
 };
+struct EncReq {
+    const uint64_t *m; size_t count; uint32_t *out; int flags;
+    int rc = FTHE_OK; bool done = false;
+};
 struct Coalescer {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<DecReq *> pending;
-    bool leader = false;
-    fthe_ctx *ctx = nullptr;                 // the key's own context, used by one leader at a time
-    std::vector<uint32_t> ct, full;
-    std::vector<uint64_t> lo;
-    ~Coalescer() { if (ctx) fthe_ctx_destroy(ctx); }
+    std::vector<EncReq *> epending;          // fthe_encrypt_shared: its own leader and context
+    bool leader = false, eleader = false;
+    fthe_ctx *ctx = nullptr, *ectx = nullptr;   // the key's own contexts, one leader each at a time
+    std::vector<uint32_t> ct, full, eout;
+    std::vector<uint64_t> lo, em;
+    ~Coalescer() {
+        if (ctx) fthe_ctx_destroy(ctx);
+        if (ectx) fthe_ctx_destroy(ectx);
+    }
 };
 
 // A named constant (S limbs) on the device.
@@ -3106,17 +3114,47 @@ static void coalesced_batch(fthe_key *k, Coalescer *co, const std::vector<DecReq
     }
 }
 
+// Encrypt side of the queue: requests grouped by flags, fresh device randomness per batch.
+static void coalesced_encrypt(fthe_key *k, Coalescer *co, const std::vector<EncReq *> &batch) {
+    const size_t cw = 2 * (size_t)k->n_words;
+    int rc0 = FTHE_OK;
+    if (!co->ectx) rc0 = fthe_ctx_create(k->device, &co->ectx);
+    std::vector<int> kinds;
+    for (EncReq *r : batch)
+        if (std::find(kinds.begin(), kinds.end(), r->flags) == kinds.end()) kinds.push_back(r->flags);
+    for (int fl : kinds) {
+        size_t tot = 0;
+        for (EncReq *r : batch) if (r->flags == fl) tot += r->count;
+        int rc = rc0;
+        if (!rc) {
+            co->em.resize(tot); co->eout.resize(tot * cw);
+            size_t at = 0;
+            for (EncReq *r : batch)
+                if (r->flags == fl) { memcpy(&co->em[at], r->m, r->count * 8); at += r->count; }
+            rc = encrypt_host(k, co->ectx, co->em.data(), 0, tot, nullptr, 0, 0, co->eout.data(), fl);
+        }
+        size_t at = 0;
+        for (EncReq *r : batch) {
+            if (r->flags != fl) continue;
+            r->rc = rc;
+            if (!rc) memcpy(r->out, &co->eout[at * cw], r->count * cw * 4);
+            at += r->count;
+        }
+    }
+}
+
+static Coalescer *key_coalescer(fthe_key *k) {
+    std::lock_guard<std::mutex> g(k->co_mu);
+    if (!k->co) k->co.reset(new Coalescer);
+    return k->co.get();
+}
+
 extern "C" int fthe_decrypt_shared(fthe_key *k, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full,
                                    int short_pt) {
     if (!k || (!ct && count)) return FTHE_ERR_ARG;
     if (!k->priv) return FTHE_ERR_NOPRIV;
     if (!count) return FTHE_OK;
-    Coalescer *co;
-    {
-        std::lock_guard<std::mutex> g(k->co_mu);
-        if (!k->co) k->co.reset(new Coalescer);
-        co = k->co.get();
-    }
+    Coalescer *co = key_coalescer(k);
     DecReq r{ct, count, m_low, m_full, short_pt != 0};
     std::unique_lock<std::mutex> lk(co->mu);
     co->pending.push_back(&r);
@@ -3266,4 +3304,29 @@ extern "C" int fthe_decode_fixed_dev(fthe_ctx *c, const uint64_t *m, size_t coun
     HIPOK(hipSetDevice(c->device));
     hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, c->stream, m, count, x);
     return hipGetLastError() == hipSuccess ? FTHE_OK : FTHE_ERR_HIP;
+}
+
+extern "C" int fthe_encrypt_shared(fthe_key *k, const uint64_t *m, size_t count, uint32_t *out, int flags) {
+    if (!k || ((!m || !out) && count)) return FTHE_ERR_ARG;
+    if (!count) return FTHE_OK;
+    Coalescer *co = key_coalescer(k);
+    EncReq r{m, count, out, flags};
+    std::unique_lock<std::mutex> lk(co->mu);
+    co->epending.push_back(&r);
+    for (;;) {
+        if (r.done) return r.rc;
+        if (!co->eleader) {
+            co->eleader = true;
+            std::vector<EncReq *> batch;
+            batch.swap(co->epending);                // includes r
+            lk.unlock();
+            coalesced_encrypt(k, co, batch);
+            lk.lock();
+            for (EncReq *q : batch) q->done = true;
+            co->eleader = false;
+            co->cv.notify_all();
+            return r.rc;
+        }
+        co->cv.wait(lk);
+    }
 }

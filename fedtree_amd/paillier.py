@@ -346,6 +346,15 @@ class Paillier:
         _lib.check(fn(self._key, self.dev.ctx, _ptr(c), cnt, _ptr(low), _ptr(fullw)), "decrypt")
         return (low, fullw) if full else low
 
+    def encrypt_u64_shared(self, m, public=False):
+        """encrypt_u64 with fresh device randomness through the key's coalescing queue
+        (fthe_encrypt_shared): thread-safe on one Paillier object, concurrent calls share a launch."""
+        m = np.ascontiguousarray(m, dtype=np.uint64).reshape(-1)
+        out = np.zeros((len(m), self._cw()), dtype=np.uint32)
+        flags = _lib.FTHE_ENC_PUBLIC if public else 0
+        _lib.check(self.lib.fthe_encrypt_shared(self._key, _ptr(m), len(m), _ptr(out), flags), "encrypt_shared")
+        return out
+
     def decrypt_u64_shared(self, c, full=False, short=False):
         """decrypt_u64 through the key's coalescing queue (fthe_decrypt_shared): safe to call from
         many threads on one Paillier object; concurrent calls are merged into one batch

@@ -244,6 +244,13 @@ int fthe_decrypt_short(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t c
 int fthe_decrypt_shared(fthe_key *key, const uint32_t *c, size_t count,
                         uint64_t *m_low, uint32_t *m_full, int short_pt);
 
+/* The same queue for encryption (a second leader and context): concurrent
+ * fthe_encrypt_u64 calls with fresh device randomness (r = NULL, seed from
+ * /dev/urandom per batch) on one key -- single GHPair encrypts from threads
+ * (GHPair::homo_encrypt, common.h:125-133; party.h:118-142 per party) --
+ * merged into one launch per flags value.  c: count * 2*n_words words. */
+int fthe_encrypt_shared(fthe_key *key, const uint64_t *m, size_t count, uint32_t *c, int flags);
+
 /* ---- homomorphic add: x*y mod n^2 (paillier.cpp:103) ------------------------
  * Replaces Paillier::add / Paillier_GMP::add (paillier_gmp.cpp:16) and
  * Paillier_GPU::add (paillier_gpu.cu:58).  Alias-safe: out may equal a or b

@@ -57,6 +57,7 @@ def test_null_arguments_rejected():
     assert lib.fthe_encrypt_u64_dev(None, None, None, 0, None, 0, 0, None, 0) == _lib.FTHE_ERR_ARG
     assert lib.fthe_decrypt_dev(None, None, None, 0, None, None) == _lib.FTHE_ERR_ARG
     assert lib.fthe_decrypt_shared(None, None, 0, None, None, 0) == _lib.FTHE_ERR_ARG
+    assert lib.fthe_encrypt_shared(None, None, 0, None, 0) == _lib.FTHE_ERR_ARG
     assert lib.fthe_add_dev(None, None, None, None, 0, None) == _lib.FTHE_ERR_ARG
     assert lib.fthe_reduce_segments_dev(None, None, None, 0, None, None, 0, None) == _lib.FTHE_ERR_ARG
     assert lib.fthe_reduce_segments(None, None, None, 0, None, None, 0, None) == _lib.FTHE_ERR_ARG

@@ -72,6 +72,37 @@ def test_shared_many_threads(pl):
     assert not bad, bad
 
 
+def test_encrypt_shared_many_threads(pl):
+    """fthe_encrypt_shared: 24 threads on one key, CRT and public-key requests merged per flags;
+    every ciphertext decrypts to its own caller's plaintexts."""
+    from fedtree_amd.paillier import Paillier
+    pub = Paillier.from_public(pl.modulus, pl.dev)
+    rng = np.random.default_rng(8)
+    T = 24
+    ms = [rng.integers(0, 2**64, 2 if i % 4 else 17, dtype=np.uint64) for i in range(T)]
+    outs, bad = [None] * T, []
+    go = threading.Barrier(T)
+
+    def work(i):
+        try:
+            go.wait()
+            outs[i] = (pub if i % 5 == 0 else pl).encrypt_u64_shared(ms[i], public=(i % 3 == 0))
+        except Exception as e:
+            bad.append((i, repr(e)))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not bad, bad
+    for i in range(T):
+        assert np.array_equal(pl.decrypt_u64(outs[i]), ms[i]), i
+    # fresh randomness: equal plaintexts give different ciphertexts
+    a = pl.encrypt_u64_shared(np.zeros(4, dtype=np.uint64))
+    assert len({bytes(r.tobytes()) for r in a}) == 4
+
+
 def test_shared_public_key_rejected(pl):
     from fedtree_amd import _lib
     from fedtree_amd.paillier import Paillier
