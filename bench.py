@@ -9,15 +9,18 @@ randomness per ciphertext from the device ChaCha20 stream + c = g^m r^n mod n^2
 mod p^2 drawn as y^p mod p^2 for uniform y, the same distribution),
 output 20M x 512 B ciphertexts left in HBM.
 
-Multi-GPU: one process per GPU (torchrun), each rank encrypts its own 10M
-pairs -- independent units, no collective on the data path (weak scaling);
-the barrier and the max-over-ranks elapsed time use torch.distributed.
+Multi-GPU: one process per GPU, each rank encrypts its own 10M pairs --
+independent units, no collective on the data path (weak scaling); the barrier
+and the max-over-ranks elapsed time use torch.distributed.  Under torchrun the
+ranks come from the environment (WORLD_SIZE must equal --gpus); a plain
+`python bench.py --gpus N` spawns the N rank processes itself.
 
 Printed by rank 0: one JSON line with the driver's contract fields plus
 `roofline` (montprog kernel: algorithmic integer MACs per second vs the
 half-rate v_mad_u64_u32 peak, per-launch HIP events on the engine stream) and
-`cpu_baseline` (the reference's own Paillier_GMP::encrypt, OpenMP over a
-bounded sample on this host's cores).
+`cpu_baseline` (the reference's own Paillier_GMP encrypt / decrypt / add /
+merge on the bench's key and inputs, OpenMP over bounded samples on this
+host's cores, cores and CPU model stated).
 """
 import argparse
 import json
@@ -48,77 +51,265 @@ PMC_FILE = "r01j_pmc.json"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without torchrun the bench spawns them itself")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pairs", type=int, default=10_000_000, help="gradient pairs per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=32768, help="ciphertexts in the CPU baseline sample (about 10-20 s of 16 host threads)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: every core this process may use, see host_cpu())")
+    ap.add_argument("--cpu-scale", type=float, default=1.0, help="CPU-baseline sample size multiplier")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank harness (launcher, barriers, max-over-ranks, "
+                         "per-rank report): gloo, no GPU, a fixed sleep as the step; never a measurement")
     return ap.parse_args()
 
 
-def cpu_baseline(sample, threads):
-    """The reference's Paillier_GMP::encrypt (full PowerMod(g,m,n^2)*PowerMod(r,n,n^2),
-    paillier_gmp.cpp:37-73), OpenMP over elements as server.h:129-133.  Falls back to
-    our C/GMP port of paillier.cpp if the reference build is absent."""
+def launch_ranks(a):
+    """`--gpus N` (N > 1) outside torchrun: start N rank processes of this script, one per GPU,
+    with the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT on 127.0.0.1),
+    and exit with the first failing status.  The parent never touches the GPU (torch is not even
+    imported) and does not re-exec itself: the ranks are children."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for pr in list(live):
+            st = pr.poll()
+            if st is None:
+                continue
+            live.remove(pr)
+            if st != 0 and rc == 0:
+                rc = st
+                for other in live:                      # a rank failed: end the others (exact PIDs)
+                    other.send_signal(signal.SIGTERM)
+    return rc if rc >= 0 else 128 - rc
+
+
+def host_cpu():
+    """The host cores this process may use and what they are: affinity mask, cgroup CPU quota,
+    the box's OMP_NUM_THREADS share (the GPU pool sets it to the CPU share of one GPU), nproc and
+    the /proc/cpuinfo model.  The baseline runs on min(affinity, quota, OMP_NUM_THREADS) threads."""
+    info = {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "omp_num_threads_env": None, "model": None}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        info["omp_num_threads_env"] = int(omp)
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    use = info["affinity_cpus"]
+    if info["cgroup_quota_cpus"]:
+        use = min(use, max(1, int(info["cgroup_quota_cpus"])))
+    if info["omp_num_threads_env"]:
+        use = min(use, info["omp_num_threads_env"])
+    info["threads_used"] = max(1, use)
+    return info
+
+
+def cpu_baseline(a, pl, p1k, m, c, dev):
+    """The reference's own CPU path timed on this host, on the bench's keys and inputs:
+    FedTree's Paillier_GMP (paillier_gmp.cpp, compiled from the reference sources into
+    oracle/_ref) -- encrypt = PowerMod(r, n, n^2) PowerMod(g, m, n^2) (:37-73), decrypt =
+    PowerMod(c, lambda, n^2) (:75-85), add = x y mod n^2 (:16-21) -- OpenMP over elements as
+    Server::encrypt_gh_pairs / decrypt_gh_pairs (server.h:105-109,129-133) and the party merge
+    (hist_tree_builder.cpp:1026-1037) do.  Bounded samples, ~10 s in all on 16 threads.
+    Without oracle/_ref: the C/GMP restatement of paillier.cpp (oracle/paillier_oracle.c)."""
     import ctypes
+    import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    from fedtree_amd.synth import logistic_gradients
-    from fedtree_amd.paillier import encode_fixed
-    g, h = logistic_gradients(sample // 2, SEED)
-    m = np.ascontiguousarray(np.concatenate([encode_fixed(g), encode_fixed(h)]))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    hc = host_cpu()
+    thr = a.cpu_threads or hc["threads_used"]
+    sc = a.cpu_scale
+    nw = pl.n_words
+    m_h = m.cpu().numpy().view(np.uint64)
     try:
         ref = pyoracle.RefGMP()
-        hk = ref.lib.ref_keygen(2 * KEY_BITS)          # GMP keyGen(L) -> L/2-bit n (SURVEY Q2)
-        nw = ref.lib.ref_n_words(hk)
-        out = np.zeros((len(m), 2 * nw), dtype=np.uint32)
-        t0 = time.perf_counter()
-        ref.lib.ref_encrypt_batch(hk, nw, m.ctypes.data, len(m), out.ctypes.data, threads)
-        dt = time.perf_counter() - t0
-        ref.lib.ref_free(hk)
-        kind, what = "reference", "FedTree Paillier_GMP::encrypt compiled from the reference sources"
     except OSError:
-        o = pyoracle.COracle()
-        rng = np.random.default_rng(SEED)
-        hw = KEY_BITS // 64
-        pw = o.next_prime(rng.integers(0, 2**32, hw, dtype=np.uint64).astype(np.uint32))
-        qw = o.next_prime(rng.integers(0, 2**32, hw, dtype=np.uint64).astype(np.uint32))
-        key = o.key(pw, qw)
-        r = rng.integers(0, 2**32, (len(m), 2 * hw), dtype=np.uint64).astype(np.uint32)
-        r[:, -1] &= 0x3FFFFFFF
+        ref = None
+    ops = {}
+
+    def timed(fn):
         t0 = time.perf_counter()
-        key.encrypt_batch(m, r, threads)
-        dt = time.perf_counter() - t0
+        fn()
+        return time.perf_counter() - t0
+
+    if ref is not None:
+        kind, what = "reference", "FedTree Paillier_GMP compiled from the reference sources (oracle/_ref)"
+        h = ref.key_from_primes(pl.p, pl.q)
+        ne = max(thr, int(512 * thr * sc))
+        mm = np.ascontiguousarray(m_h[:ne])
+        ct = np.zeros((ne, 2 * nw), np.uint32)
+        dt = timed(lambda: ref.lib.ref_encrypt_batch(h, nw, mm.ctypes.data, ne, ct.ctypes.data, thr))
+        ops["p2048_encrypt"] = {"per_s": ne / dt, "n": ne, "s": dt}
+        n1 = max(8, int(128 * sc))
+        ct1 = np.zeros((n1, 2 * nw), np.uint32)
+        dt1 = timed(lambda: ref.lib.ref_encrypt_batch(h, nw, mm.ctypes.data, n1, ct1.ctypes.data, 1))
+        ops["p2048_encrypt_1_thread"] = {"per_s": n1 / dt1, "n": n1, "s": dt1}
+        # the CPU ciphertexts are valid under the bench's key: the engine decrypts them to m
+        chk = pl.decrypt_u64(ct[:256])
+        same_key_ok = bool(np.array_equal(chk, mm[:256]))
+        nd = ne
+        cin = np.ascontiguousarray(c[:nd].cpu().numpy().view(np.uint32))
+        lo = np.zeros(nd, np.uint64)
+        dt = timed(lambda: ref.lib.ref_decrypt_batch(h, nw, cin.ctypes.data, nd, lo.ctypes.data, thr))
+        ops["p2048_decrypt"] = {"per_s": nd / dt, "n": nd, "s": dt, "ok": bool(np.array_equal(lo, m_h[:nd]))}
+        na = max(thr, int(65536 * thr * sc))
+        na = min(na, 1 << 20, c.shape[0] // 2)
+        xa = np.ascontiguousarray(c[:na].cpu().numpy().view(np.uint32))
+        xb = np.ascontiguousarray(c[na:2 * na].cpu().numpy().view(np.uint32))
+        so = np.zeros_like(xa)
+        dt = timed(lambda: ref.lib.ref_add_batch(h, nw, xa.ctypes.data, xb.ctypes.data, na, so.ctypes.data, thr))
+        ops["p2048_add"] = {"per_s": na / dt, "n": na, "s": dt}
+        nb, parties = max(thr, int(8192 * thr * sc)), 8
+        nb = min(nb, 1 << 17, c.shape[0] // parties)
+        xk = np.ascontiguousarray(c[:parties * nb].cpu().numpy().view(np.uint32))
+        mo = np.zeros((nb, 2 * nw), np.uint32)
+        dt = timed(lambda: ref.lib.ref_merge_batch(h, nw, xk.ctypes.data, parties, nb, mo.ctypes.data, thr))
+        ops["p2048_merge_8party"] = {"adds_per_s": nb * (parties - 1) / dt, "bins": nb, "s": dt,
+                                     "note": "7 Paillier_GMP::add per bin, parties serial, bins in parallel"}
+        del xa, xb, so, xk, mo, cin
+        ref.lib.ref_free(h)
+        if p1k is not None:
+            h1 = ref.key_from_primes(p1k.p, p1k.q)
+            n1k = max(thr, int(4096 * thr * sc))
+            m1 = np.ascontiguousarray(m_h[:n1k])
+            c1 = np.zeros((n1k, 2 * p1k.n_words), np.uint32)
+            dt = timed(lambda: ref.lib.ref_encrypt_batch(h1, p1k.n_words, m1.ctypes.data, n1k, c1.ctypes.data, thr))
+            ops["p1024_encrypt"] = {"per_s": n1k / dt, "n": n1k, "s": dt}
+            ref.lib.ref_free(h1)
+    else:
         kind, what = "port", "C/GMP restatement of paillier.cpp:122-139 (oracle/paillier_oracle.c)"
-    return {"value": len(m) / dt, "unit": "encrypts/s", "cores": threads, "kind": kind,
-            "sample": f"{len(m)} Paillier-2048 encrypts of synthetic gradients ({what}, full PowerMod, "
-                      f"no CRT, OpenMP {threads} threads), {dt:.1f} s"}
+        same_key_ok = None
+        hw = (max(pl.p.bit_length(), pl.q.bit_length()) + 31) // 32
+        key = pyoracle.COracle().key(pyoracle.to_words(pl.p, hw), pyoracle.to_words(pl.q, hw))
+        ne = max(thr, int(512 * thr * sc))
+        rng = np.random.default_rng(SEED)
+        r = rng.integers(0, 2**32, (ne, nw), dtype=np.uint64).astype(np.uint32)
+        r[:, -1] &= 0x3FFFFFFF
+        dt = timed(lambda: key.encrypt_batch(m_h[:ne], r, thr))
+        ops["p2048_encrypt"] = {"per_s": ne / dt, "n": ne, "s": dt}
+    for v in ops.values():
+        for k_ in ("per_s", "adds_per_s", "s"):
+            if k_ in v:
+                v[k_] = round(v[k_], 3 if k_ == "s" else 1)
+    enc = ops["p2048_encrypt"]
+    one = ops.get("p2048_encrypt_1_thread")
+    return {"value": enc["per_s"], "unit": "encrypts/s", "cores": thr, "kind": kind,
+            "sample": f"{enc['n']} Paillier-2048 encrypts of the bench's own gradients under the bench's own key "
+                      f"({what}: full PowerMod, no CRT; OpenMP {thr} threads), {enc['s']:.1f} s",
+            "per_thread_per_s": round(enc["per_s"] / thr, 1),
+            "single_thread_per_s": one["per_s"] if one else None,
+            "host": hc, "same_key_decrypts_on_gpu": same_key_ok, "ops": ops}
 
 
 def main():
     a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    world = int(env_world or "1")
+    if world != a.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}: launch one rank per GPU")
+    if a.dry_run:
+        return dry_run(a, world)
+    return run(a, world)
+
+
+def dry_run(a, world):
+    """The multi-rank harness with a CPU sleep as the step (tests/test_bench_launcher.py)."""
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("FTHE_BENCH_FAIL_RANK") == str(rank):
+        sys.exit(3)                                   # launcher test: a rank that dies early
+    if world > 1:
+        dist.init_process_group("gloo")
+    times = timed_steps(lambda i: time.sleep(0.02), a, world, sync=lambda: None)
+    per = gather_ranks({"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
+                        "elapsed_s": times}, world)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "elapsed_max_s": max(p["elapsed_s"] for p in per),
+                          "per_rank": per}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def timed_steps(step, a, world, sync):
+    """W untimed steps, then K timed ones bracketed by barrier + device sync on both sides.
+    Returns this rank's elapsed seconds."""
+    import torch.distributed as dist
+    for i in range(a.warmup):
+        step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+        if int(os.environ.get("RANK", "0")) == 0:
+            sync()                      # progress for long runs (one host sync per ~13 s step: no measurable cost)
+            print(f"[bench] step {i + 1}/{a.steps} done at {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+                  flush=True)
+    sync()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    return t1 - t0
+
+
+def gather_ranks(obj, world):
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def run(a, world):
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # FTHE_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- exercises the multi-rank
-    # path (barriers, max-over-ranks timing, rank-0 reporting) on a one-GPU box, where
+    # FTHE_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- exercises the multi-rank path
+    # (launcher, barriers, max-over-ranks timing, rank-0 reporting) on a one-GPU box, where
     # RCCL refuses two ranks on one device.  Never used for reported numbers.
     rehearse = os.environ.get("FTHE_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
-    backend = "gloo" if rehearse else "nccl"
     if world > 1:
         torch.cuda.set_device(local)
         if rehearse:
-            dist.init_process_group(backend)
+            dist.init_process_group("gloo")
         else:
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            # RCCL carries only the barriers and the max-over-ranks gathers: no data-path collective
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from fedtree_amd.paillier import Device, Paillier
     from fedtree_amd.synth import logistic_gradients
     from fedtree_amd import _lib
@@ -126,6 +317,13 @@ def main():
 
     dev = Device(local)
     lib = dev.lib
+    if lib.fthe_ctx_device(dev.ctx) != local:
+        raise SystemExit(f"rank {rank}: engine context on device {lib.fthe_ctx_device(dev.ctx)}, expected {local}")
+    props = torch.cuda.get_device_properties(local)
+    ident = {"rank": rank, "local_rank": local, "device": local,
+             "pci": f"{getattr(props, 'pci_domain_id', 0):04x}:{getattr(props, 'pci_bus_id', 0):02x}:"
+                    f"{getattr(props, 'pci_device_id', 0):02x}",
+             "uuid": str(getattr(props, "uuid", ""))}
     t_kg = time.perf_counter()
     pl = Paillier(dev).keygen(KEY_BITS, seed=SEED)            # the server's key (same on every rank)
     keygen_s = time.perf_counter() - t_kg
@@ -141,40 +339,37 @@ def main():
                                              ctypes.c_void_p(m.data_ptr())), "encode")
         pl.encrypt_u64_dev(m, c, seed=SEED * 1000 + rank * 100 + i + 1)
 
+    def sync():
+        dev.sync()
+        torch.cuda.synchronize()
+
     for i in range(a.warmup):
         step(i)
-    dev.sync()
+    sync()
     lib.fthe_prof_enable(dev.ctx, 1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dev.sync()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i)
-    dev.sync()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
+    wa = argparse.Namespace(**vars(a))
+    wa.warmup = 0                                    # warm-up done above, before profiling is enabled
+    elapsed_rank = timed_steps(lambda i: step(a.warmup + i), wa, world, sync)
     kms, launches, lane_mm, lanes, ems, elaunch, amacs = (ctypes.c_double() for _ in range(7))
     _lib.check(lib.fthe_prof_read(dev.ctx, ctypes.byref(kms), ctypes.byref(launches), ctypes.byref(lane_mm),
                                   ctypes.byref(lanes), ctypes.byref(ems), ctypes.byref(elaunch),
                                   ctypes.byref(amacs)))
     lib.fthe_prof_enable(dev.ctx, 0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    enc_total = world * 2 * P * a.steps
+    enc_rank = 2 * P * a.steps
+    ident.update({"elapsed_s": round(elapsed_rank, 4), "encrypts_per_s": round(enc_rank / elapsed_rank, 1)})
+    per_rank = gather_ranks(ident, world)
+    if world > 1 and not rehearse:
+        # one rank per GPU: every rank on its own device
+        if len({p["pci"] + p["uuid"] for p in per_rank}) != world:
+            raise SystemExit(f"bench.py: ranks share a device: {per_rank}")
+    elapsed = max(p["elapsed_s"] for p in per_rank)
+    enc_total = world * enc_rank
     value = enc_total / elapsed
 
     # -- roofline of the dominant kernel family (montprog s37 + s74, per-launch HIP
     # events on the engine stream, this rank).  Algorithmic work = the Montgomery
     # products the programs perform x W(s) = 2 s^2 + s MACs on s = 32-bit words of
     # the modulus (SURVEY.md 8(d) unit), accumulated per launch by the engine.
-    enc_rank = 2 * P * a.steps
     alg_macs = amacs.value
     k_s = kms.value * 1e-3
     achieved = alg_macs / k_s / 1e12
@@ -188,7 +383,7 @@ def main():
             "alg_macs_per_encrypt": round(alg_macs / enc_rank),
             "survey_alg_macs_per_crt_encrypt_direct": ALG_MACS_PER_CRT_ENC,
             "montmuls_per_encrypt": round(lane_mm.value / enc_rank, 1),
-            "kernel_share_of_step": round(k_s / elapsed, 4)}
+            "kernel_share_of_step": round(k_s / elapsed_rank, 4)}
     for S in (37, 74, 152):
         vms, vn = ctypes.c_double(), ctypes.c_double()
         lib.fthe_prof_variant(dev.ctx, S, ctypes.byref(vms), ctypes.byref(vn))
@@ -211,7 +406,9 @@ def main():
     roof["traffic_note"] = ("HBM bytes are the per-lane window-table operand reads (~190 multiplications x 296 B "
                             "per lane per exponentiation), 2.2% of HBM bandwidth in a VALU-bound kernel")
 
+
     secondary = {}
+    p1k_cpu = None
     if rank == 0 and world == 1 and not a.no_secondary:      # N=1 runs only: scaling runs stay lean
         # CRT decrypt of 1M ciphertexts (config 3's decrypt half), device-resident
         nd = min(2 * P, 1 << 20)
@@ -226,6 +423,28 @@ def main():
         dev.sync()
         secondary["crt_decrypt_short_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
         secondary["decrypt_short_roundtrip_ok"] = bool(torch.equal(low, m[:nd]))
+        # the same CRT encrypt with injected r (stage A r^Q mod P, then stage B): the path the golden,
+        # random-vs-oracle and configs[1] tests pin bit-exactly; r < 2^(n_bits - 2) < n drawn by torch
+        nr = min(2 * P, 1 << 20)
+        gen = torch.Generator(device=f"cuda:{local}").manual_seed(SEED + 5)
+        rinj = torch.randint(-2**31, 2**31 - 1, (nr, pl.n_words), dtype=torch.int32, device=f"cuda:{local}",
+                             generator=gen)
+        rinj[:, -1] &= 0x3FFFFFFF
+        rinj[:, 0] |= 1
+        cinj = torch.empty((nr, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+        pl.encrypt_u64_dev(m[:nr], cinj, r=rinj)
+        dev.sync()
+        pl.encrypt_u64_dev(m[:nr], cinj, r=rinj)
+        dev.sync()
+        inj_rate = nr / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3)
+        pl.decrypt_u64_dev(cinj, low[:nr])
+        dev.sync()
+        secondary["crt_encrypt_injected_r"] = {
+            "encrypts_per_s": round(inj_rate), "ciphertexts": nr, "roundtrip_ok": bool(torch.equal(low[:nr], m[:nr])),
+            "vs_value": round(inj_rate / value, 3),
+            "note": "two-stage CRT with caller r (r^(q mod p-1) mod p on s37, then mod p^2 on s74); the headline "
+                    "draws y_P directly (one stage), pinned bit-exactly by tests/test_gpu_direct_y.py"}
+        del rinj, cinj
         # public-key encrypt (a party without the factorization, party.h:118-142) and the
         # opt-in fixed-base randomizer (r = h^alpha, include/fthe.h FTHE_ENC_FIXED_BASE; not
         # the reference's uniform-r algorithm, so never the headline `value`)
@@ -443,6 +662,7 @@ def main():
         r1k["roundtrip_ok"] = bool(torch.equal(low1k, m[:n1k]))
         r1k["ciphertexts"] = n1k
         secondary["p1024_100k_pairs"] = r1k
+        p1k_cpu = p1k                                  # the CPU baseline's P-1024 key
         del c1k, low1k, p1k
         # configs[3]: 8-party merge of 256 x 4096 bins x {g, h} (hist_tree_builder.cpp:1015-1058)
         bins, parties = 2 * 256 * 4096, 8
@@ -549,7 +769,7 @@ def main():
         del ch, strs, back, fr, g_, dbuf, doffs, dback, hb_, ho_
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a.cpu_sample, a.cpu_threads)
+        cpu = cpu_baseline(a, pl, p1k_cpu, m, c, dev)
 
     if rank == 0:
         line = {
@@ -561,7 +781,11 @@ def main():
                        "pairs_per_gpu": P, "ciphertexts_per_gpu_per_step": 2 * P, "key_bits": KEY_BITS,
                        "parallelism": f"independent shards x{world}"},
             "roofline": roof, "cpu_baseline": cpu, "secondary": secondary,
+            "per_rank": per_rank, "rank_time_max_s": round(elapsed, 4),
+            "rank_time_min_s": round(min(p["elapsed_s"] for p in per_rank), 4),
         }
+        if rehearse:
+            line["rehearsal"] = "FTHE_BENCH_REHEARSE=1: all ranks on cuda:0 over gloo; not a measurement"
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)

@@ -108,6 +108,7 @@ _PROTOS = {
     "fthe_last_kernel_ms": (ctypes.c_double, [_P]),
     "fthe_last_montmuls": (ctypes.c_double, [_P]),
     "fthe_kernel_limbs": (_I, [_I]),
+    "fthe_debug_direct_y": (_I, [_P, _P, _U64, _U64, _SZ, _P, _P]),
     "fthe_prof_enable": (_I, [_P, _I]),
     "fthe_prof_variant": (_I, [_P, _I, _P, _P]),
     "fthe_prof_read": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),

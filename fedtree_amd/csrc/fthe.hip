@@ -21,6 +21,7 @@
 #include <memory>
 #include <string>
 #include <mutex>
+#include <new>
 #include <random>
 #include <thread>
 #include <unordered_map>
@@ -49,12 +50,23 @@ int variant_index(int S) {
     return -1;
 }
 
-uint64_t urandom64() {
-    uint64_t v = 0;
+// n bytes from the kernel CSPRNG (/dev/urandom; std::random_device if it cannot be read)
+void urandom_bytes(void *dst, size_t n) {
+    uint8_t *p = (uint8_t *)dst;
+    size_t got = 0;
     int fd = open("/dev/urandom", O_RDONLY);
-    if (fd >= 0) { if (read(fd, &v, sizeof v) != (ssize_t)sizeof v) v = 0; close(fd); }
-    if (!v) v = std::random_device{}() ^ ((uint64_t)std::random_device{}() << 32);
-    return v;
+    if (fd >= 0) {
+        while (got < n) {
+            ssize_t r = read(fd, p + got, n - got);
+            if (r <= 0) break;
+            got += (size_t)r;
+        }
+        close(fd);
+    }
+    if (got < n) {
+        std::random_device rd;
+        for (; got < n; got++) p[got] = (uint8_t)rd();
+    }
 }
 
 // splitmix64 (seeded key generation / rng keys)
@@ -63,6 +75,39 @@ uint64_t splitmix64(uint64_t &s) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+// ChaCha20 key + nonce of a device randomness stream.  seed 0: 320 bits straight from
+// /dev/urandom; a nonzero seed (tests, benchmarks) expands deterministically with
+// splitmix64.  `tweak` separates the streams of the different randomizer modes.
+RngKey make_rng_key(uint64_t seed, uint64_t tweak) {
+    RngKey rk{};
+    if (!seed) {
+        urandom_bytes(rk.k, sizeof rk.k);
+        urandom_bytes(&rk.nonce, sizeof rk.nonce);
+        return rk;
+    }
+    uint64_t s = seed;
+    for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(s); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
+    rk.nonce = splitmix64(s) ^ tweak;
+    return rk;
+}
+
+// GMP random state for key material: seed 0 -> 256 bits from /dev/urandom, else a
+// deterministic 128-bit expansion of the seed (tests, benchmarks).
+void seed_gmp_state(gmp_randstate_t st, uint64_t seed, uint64_t tweak) {
+    Mpz sd;
+    if (!seed) {
+        uint32_t w[8];
+        urandom_bytes(w, sizeof w);
+        mpz_import(sd, 8, -1, 4, 0, 0, w);
+    } else {
+        uint64_t s = seed;
+        mpz_set_ui(sd, (unsigned long)splitmix64(s));
+        mpz_mul_2exp(sd, sd, 64);
+        mpz_add_ui(sd, sd, (unsigned long)(splitmix64(s) ^ tweak));
+    }
+    gmp_randseed(st, sd);
 }
 
 size_t chunk_lanes() {
@@ -855,10 +900,7 @@ extern "C" int fthe_key_generate_ex(fthe_ctx *ctx, int n_bits, uint64_t seed, in
     if (!(flags & FTHE_KEYGEN_KNOWN_ORDER)) return fthe_key_generate(ctx, n_bits, seed, out);
     if (!ctx || !out || n_bits < 128 || (n_bits & 1)) return FTHE_ERR_ARG;
     gmp_randstate_t st; gmp_randinit_mt(st);
-    uint64_t s = seed ? seed : urandom64();
-    Mpz sd; mpz_set_ui(sd, (unsigned long)splitmix64(s));
-    mpz_mul_2exp(sd, sd, 64); mpz_add_ui(sd, sd, (unsigned long)splitmix64(s) ^ 0x6b6e6f776e6f7264ull);
-    gmp_randseed(st, sd);
+    seed_gmp_state(st, seed, 0x6b6e6f776e6f7264ull);
     const int hb = n_bits / 2;
     int rc = FTHE_ERR_KEY;
     for (int tries = 0; tries < 64 && rc == FTHE_ERR_KEY; tries++) {
@@ -953,10 +995,7 @@ extern "C" int fthe_next_prime(const uint32_t *start, int words, uint32_t *out, 
 extern "C" int fthe_key_generate(fthe_ctx *ctx, int n_bits, uint64_t seed, fthe_key **out) {
     if (!ctx || !out || n_bits < 64 || (n_bits & 1)) return FTHE_ERR_ARG;
     gmp_randstate_t st; gmp_randinit_mt(st);
-    uint64_t s = seed ? seed : urandom64();
-    Mpz sd; mpz_set_ui(sd, (unsigned long)splitmix64(s));
-    mpz_mul_2exp(sd, sd, 64); mpz_add_ui(sd, sd, (unsigned long)splitmix64(s));
-    gmp_randseed(st, sd);
+    seed_gmp_state(st, seed, 0);
     int hb = n_bits / 2;
     int rc = FTHE_ERR_KEY;
     for (int tries = 0; tries < 64 && rc == FTHE_ERR_KEY; tries++) {
@@ -1290,6 +1329,8 @@ struct MsgSrc {
 
 static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *alpha,
                            int a_words, uint64_t rng_seed, uint32_t *out, bool crt, HostPipe *pipe);
+// nonce tweak of the y_q stream of the direct-y CRT encrypt (y_p uses the key's own nonce)
+constexpr uint64_t kYqStream = 0x7172737475767778ull;
 static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y,
                            int y_words, uint64_t rng_seed, uint32_t *out, HostPipe *pipe);
 static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const uint32_t *y, int y_words,
@@ -1315,7 +1356,8 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     // small batches: the q half on the side stream in a second slot region, as decrypt_impl
     const int vi = variant_index(k->spq.S);
     // and smaller ones both halves on the four-lane s80 kernel (as decrypt_impl)
-    const bool quad = direct_y && k->slat.S && count > 0 && count <= dec_quad_max();
+    // (one chunk by construction: FTHE_CHUNK below the quad limit sends the batch down the other paths)
+    const bool quad = direct_y && k->slat.S && count > 0 && count <= dec_quad_max() && count <= chunk_lanes();
     const bool split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
@@ -1334,11 +1376,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                                                quad ? (size_t)L * (2 * k->pq_w + 2 * wl) * 4 : (size_t)0))))
         return rc;
     RngKey rk{};
-    if (!r) {
-        uint64_t s = rng_seed ? rng_seed : urandom64();
-        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(s); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
-        rk.nonce = splitmix64(s);
-    }
+    if (!r) rk = make_rng_key(rng_seed, 0);
     Launch L1 = Lc;                    // stage A: mod p, q on the small-limb kernel, own slot region
     Launch Lq = Lc;                    // split: q half, region 2 of the slots, side stream
     if (split) {
@@ -1384,7 +1422,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         int rwn = r_words;
         if (direct_y) {
             uint32_t *yp = (uint32_t *)c->scratch.p, *yq = yp + (size_t)L * k->pq_w;
-            RngKey rq = rk; rq.nonce ^= 0x7172737475767778ull;       // an independent stream for y_q
+            RngKey rq = rk; rq.nonce ^= kYqStream;                    // an independent stream for y_q
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords, k->pq_w, (int)k->p.bits(),
                                rk, (uint64_t)off, cnt, yp);
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords + k->pq_w, k->pq_w,
@@ -1490,6 +1528,37 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     }
     Lc.mm += Lq.mm;
     return end_call(c, Lc);
+}
+
+// Test hook (include/fthe.h): the exponent bases (y_p, y_q) the direct-y CRT encrypt draws for
+// ciphertexts [index0, index0 + count) of a call with r == NULL and this rng_seed -- the same
+// kernel, keys and per-index counters as encrypt_impl, so a test can rebuild each ciphertext's
+// r = CRT(y_p^(q^-1 mod p-1) mod p, y_q^(p^-1 mod q-1) mod q) and check it against
+// PowerMod(g, m, n^2) PowerMod(r, n, n^2) (paillier.cpp:134-137).
+extern "C" int fthe_debug_direct_y(fthe_key *k, fthe_ctx *c, uint64_t rng_seed, uint64_t index0, size_t count,
+                                   uint32_t *yp, uint32_t *yq) {
+    if (!k || !c || !rng_seed || (count && (!yp || !yq))) return FTHE_ERR_ARG;
+    if (k->device != c->device) return FTHE_ERR_ARG;
+    if (!k->priv) return FTHE_ERR_NOPRIV;
+    if (!count) return FTHE_OK;
+    HIPOK(hipSetDevice(c->device));
+    const RngKey rk = make_rng_key(rng_seed, 0);
+    RngKey rq = rk; rq.nonce ^= kYqStream;
+    const size_t words = count * (size_t)k->pq_w;
+    DevBuf d;
+    int rc = d.ensure(2 * words * 4);
+    if (rc) return rc;
+    uint32_t *dp = (uint32_t *)d.p, *dq = dp + words;
+    const dim3 grid((unsigned)((count + 255) / 256));
+    hipLaunchKernelGGL(k_rng_r, grid, dim3(256), 0, c->stream, k->d_pqwords, k->pq_w, (int)k->p.bits(), rk, index0,
+                       count, dp);
+    hipLaunchKernelGGL(k_rng_r, grid, dim3(256), 0, c->stream, k->d_pqwords + k->pq_w, k->pq_w, (int)k->q.bits(), rq,
+                       index0, count, dq);
+    HIPOK(hipGetLastError());
+    HIPOK(hipMemcpyAsync(yp, dp, words * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipMemcpyAsync(yq, dq, words * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    return FTHE_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1703,8 +1772,7 @@ int fb_ensure(fthe_key *k, fthe_ctx *c) {
     // h uniform in [1, n) from /dev/urandom
     gmp_randstate_t st;
     gmp_randinit_default(st);
-    Mpz seed; mpz_set_ui(seed, urandom64()); mpz_mul_2exp(seed, seed, 64); mpz_add_ui(seed, seed, urandom64());
-    gmp_randseed(st, seed);
+    seed_gmp_state(st, 0, 0);
     Mpz h, nm1; mpz_sub_ui(nm1, k->n, 1);
     mpz_urandomm(h, st, nm1); mpz_add_ui(h, h, 1);
     gmp_randclear(st);
@@ -1752,11 +1820,7 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
     if ((rc = c->scratch.ensure(2 * dig_bytes))) return rc;
     uint8_t *dig_p = (uint8_t *)c->scratch.p, *dig_q = dig_p + dig_bytes;
     RngKey rk{};
-    if (!alpha) {
-        uint64_t sd = rng_seed ? rng_seed : urandom64();
-        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(sd); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
-        rk.nonce = splitmix64(sd) ^ 0x6669786564626173ull;     // a stream apart from k_rng_r's
-    }
+    if (!alpha) rk = make_rng_key(rng_seed, 0x6669786564626173ull);
     if (crt) {
         Lc.fill(SL_C1, k->c_nRp); Lc.fill(SL_C3, k->c_nRq);
         Lc.fill(SL_T1, k->c_qinvRp2);
@@ -1881,11 +1945,15 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
     X.ready = false;
     gmp_randstate_t st;
     gmp_randinit_default(st);
-    Mpz sd;
-    mpz_set_ui(sd, seed ? seed : urandom64());
-    mpz_mul_2exp(sd, sd, 64);
-    mpz_add_ui(sd, sd, seed ? 0x5845584143544241ull : urandom64());
-    gmp_randseed(st, sd);
+    if (seed) {
+        Mpz sd;
+        mpz_set_ui(sd, seed);
+        mpz_mul_2exp(sd, sd, 64);
+        mpz_add_ui(sd, sd, 0x5845584143544241ull);
+        gmp_randseed(st, sd);
+    } else {
+        seed_gmp_state(st, 0, 0);       // 256 bits of /dev/urandom
+    }
     X.nwin = (int)((std::max(k->p.bits(), k->q.bits()) + 15) / 16);
     X.ew = 4 * ((k->spq.S + 3) / 4);
     X.nb = k->order_known ? 1 : 3;
@@ -2153,11 +2221,15 @@ extern "C" int fthe_key_public_bases(fthe_key *k, uint64_t seed, uint32_t *hs, i
     if (!hs) return FTHE_OK;
     gmp_randstate_t st;
     gmp_randinit_default(st);
-    Mpz sd;
-    mpz_set_ui(sd, seed ? seed : urandom64());
-    mpz_mul_2exp(sd, sd, 64);
-    mpz_add_ui(sd, sd, seed ? 0x5055424241534553ull : urandom64());
-    gmp_randseed(st, sd);
+    if (seed) {
+        Mpz sd;
+        mpz_set_ui(sd, seed);
+        mpz_mul_2exp(sd, sd, 64);
+        mpz_add_ui(sd, sd, 0x5055424241534553ull);
+        gmp_randseed(st, sd);
+    } else {
+        seed_gmp_state(st, 0, 0);       // 256 bits of /dev/urandom
+    }
     Mpz t[3], span, g;
     const int full = 16 * ((k->n_bits + 64 + 15) / 16);
     int eb[3] = {full, full, full};
@@ -2229,11 +2301,7 @@ static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
     if ((rc = c->scratch.ensure(dig_bytes))) return rc;
     uint8_t *dig = (uint8_t *)c->scratch.p;
     RngKey rk{};
-    if (!y) {
-        uint64_t sd = rng_seed ? rng_seed : urandom64();
-        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(sd); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
-        rk.nonce = splitmix64(sd) ^ 0x7075626c69636273ull;     // streams apart from the other modes'
-    }
+    if (!y) rk = make_rng_key(rng_seed, 0x7075626c69636273ull);
     Lc.fill(SL_C1, k->c_nRn2);
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
@@ -2281,11 +2349,7 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
     uint8_t *dig[2] = {(uint8_t *)c->scratch.p, (uint8_t *)c->scratch.p + dig_bytes};
     uint32_t *ytmp = (uint32_t *)((uint8_t *)c->scratch.p + 2 * dig_bytes);
     RngKey rk{};
-    if (!y) {
-        uint64_t sd = rng_seed ? rng_seed : urandom64();
-        for (int i = 0; i < 8; i += 2) { uint64_t v = splitmix64(sd); rk.k[i] = (uint32_t)v; rk.k[i + 1] = (uint32_t)(v >> 32); }
-        rk.nonce = splitmix64(sd) ^ 0x6578616374626173ull;     // streams apart from k_rng_r's and k_rng_digits'
-    }
+    if (!y) rk = make_rng_key(rng_seed, 0x6578616374626173ull);
     Lc.fill(SL_C1, k->c_nRp); Lc.fill(SL_C3, k->c_nRq);
     Lc.fill(SL_T1, k->c_qinvRp2);
     const size_t exp_bytes = (size_t)X.nwin * L * 2;
@@ -2350,7 +2414,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
     // each Montgomery product spread over a quad of lanes (~3x less latency per exponentiation), and
     // hand c^(P-1) mod P^2 back to the s74 layout for the unchanged L-function / CRT tail.
     const int vi = variant_index(k->spq.S);
-    const bool quad = k->slat.S && count > 0 && count <= dec_quad_max();
+    const bool quad = k->slat.S && count > 0 && count <= dec_quad_max() && count <= chunk_lanes();
     const bool split = !quad && !short_pt && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
@@ -3079,12 +3143,25 @@ extern "C" int fthe_decrypt(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t
     return decrypt_host(k, c, ct, count, m_low, m_full, false);
 }
 
+// Staging buffers of the shared queues above this many bytes are released after their batch
+// (one large shared call must not pin a second copy of its ciphertexts for the key's lifetime).
+constexpr size_t kCoalesceKeepBytes = (size_t)64 << 20;
+template <class V> static void trim(V &v) {
+    if (v.capacity() * sizeof(typename V::value_type) > kCoalesceKeepBytes) { V().swap(v); }
+}
+
 // One leader runs everything pending (its own request included) as at most two batched calls
-// (full / short), then hands leadership to a caller still waiting.
-static void coalesced_batch(fthe_key *k, Coalescer *co, const std::vector<DecReq *> &batch) {
+// (full / short), then hands leadership to a caller still waiting.  A lone request runs straight
+// on the caller's buffers (no staging copy).
+static void coalesced_batch_impl(fthe_key *k, Coalescer *co, const std::vector<DecReq *> &batch) {
     const size_t cw = 2 * (size_t)k->n_words, nw = k->n_words;
     int rc0 = FTHE_OK;
     if (!co->ctx) rc0 = fthe_ctx_create(k->device, &co->ctx);
+    if (batch.size() == 1) {
+        DecReq *r = batch[0];
+        r->rc = rc0 ? rc0 : decrypt_host(k, co->ctx, r->ct, r->count, r->m_low, r->m_full, r->short_pt);
+        return;
+    }
     for (int kind = 0; kind < 2; kind++) {
         size_t tot = 0;
         bool want_full = false;
@@ -3112,13 +3189,31 @@ static void coalesced_batch(fthe_key *k, Coalescer *co, const std::vector<DecReq
             at += r->count;
         }
     }
+    trim(co->ct); trim(co->lo); trim(co->full);
+}
+
+// Nothing may leave the C ABI by exception, and the leader must always mark its batch done and
+// hand over (fthe_decrypt_shared): allocation failures (staging vectors, copy threads) become
+// FTHE_ERR_NOMEM for every request of the batch.
+static void coalesced_batch(fthe_key *k, Coalescer *co, const std::vector<DecReq *> &batch) {
+    try {
+        coalesced_batch_impl(k, co, batch);
+    } catch (...) {
+        for (DecReq *r : batch) r->rc = FTHE_ERR_NOMEM;
+        try { trim(co->ct); trim(co->lo); trim(co->full); } catch (...) {}
+    }
 }
 
 // Encrypt side of the queue: requests grouped by flags, fresh device randomness per batch.
-static void coalesced_encrypt(fthe_key *k, Coalescer *co, const std::vector<EncReq *> &batch) {
+static void coalesced_encrypt_impl(fthe_key *k, Coalescer *co, const std::vector<EncReq *> &batch) {
     const size_t cw = 2 * (size_t)k->n_words;
     int rc0 = FTHE_OK;
     if (!co->ectx) rc0 = fthe_ctx_create(k->device, &co->ectx);
+    if (batch.size() == 1) {
+        EncReq *r = batch[0];
+        r->rc = rc0 ? rc0 : encrypt_host(k, co->ectx, r->m, 0, r->count, nullptr, 0, 0, r->out, r->flags);
+        return;
+    }
     std::vector<int> kinds;
     for (EncReq *r : batch)
         if (std::find(kinds.begin(), kinds.end(), r->flags) == kinds.end()) kinds.push_back(r->flags);
@@ -3141,11 +3236,21 @@ static void coalesced_encrypt(fthe_key *k, Coalescer *co, const std::vector<EncR
             at += r->count;
         }
     }
+    trim(co->em); trim(co->eout);
+}
+
+static void coalesced_encrypt(fthe_key *k, Coalescer *co, const std::vector<EncReq *> &batch) {
+    try {
+        coalesced_encrypt_impl(k, co, batch);
+    } catch (...) {
+        for (EncReq *r : batch) r->rc = FTHE_ERR_NOMEM;
+        try { trim(co->em); trim(co->eout); } catch (...) {}
+    }
 }
 
 static Coalescer *key_coalescer(fthe_key *k) {
     std::lock_guard<std::mutex> g(k->co_mu);
-    if (!k->co) k->co.reset(new Coalescer);
+    if (!k->co) k->co.reset(new (std::nothrow) Coalescer);
     return k->co.get();
 }
 
@@ -3155,9 +3260,10 @@ extern "C" int fthe_decrypt_shared(fthe_key *k, const uint32_t *ct, size_t count
     if (!k->priv) return FTHE_ERR_NOPRIV;
     if (!count) return FTHE_OK;
     Coalescer *co = key_coalescer(k);
+    if (!co) return FTHE_ERR_NOMEM;
     DecReq r{ct, count, m_low, m_full, short_pt != 0};
     std::unique_lock<std::mutex> lk(co->mu);
-    co->pending.push_back(&r);
+    try { co->pending.push_back(&r); } catch (...) { return FTHE_ERR_NOMEM; }
     for (;;) {
         if (r.done) return r.rc;
         if (!co->leader) {
@@ -3310,9 +3416,10 @@ extern "C" int fthe_encrypt_shared(fthe_key *k, const uint64_t *m, size_t count,
     if (!k || ((!m || !out) && count)) return FTHE_ERR_ARG;
     if (!count) return FTHE_OK;
     Coalescer *co = key_coalescer(k);
+    if (!co) return FTHE_ERR_NOMEM;
     EncReq r{m, count, out, flags};
     std::unique_lock<std::mutex> lk(co->mu);
-    co->epending.push_back(&r);
+    try { co->epending.push_back(&r); } catch (...) { return FTHE_ERR_NOMEM; }
     for (;;) {
         if (r.done) return r.rc;
         if (!co->eleader) {

@@ -334,6 +334,19 @@ class Paillier:
                    "encrypt")
         return out
 
+    def direct_y(self, seed, index0, count):
+        """(y_p, y_q) words ((count, pq_words) uint32 each) that encrypt_u64[_dev](r=None, seed=seed)
+        draws for ciphertexts [index0, index0 + count) on the key holder's direct-y path
+        (fthe_debug_direct_y, test hook): r = CRT(y_p^(q^-1 mod p-1), y_q^(p^-1 mod q-1))."""
+        if not seed:
+            raise ValueError("direct_y needs the nonzero seed of the encrypt call")
+        pw = (max(self.p.bit_length(), self.q.bit_length()) + 31) // 32
+        yp = np.zeros((count, pw), dtype=np.uint32)
+        yq = np.zeros((count, pw), dtype=np.uint32)
+        _lib.check(self.lib.fthe_debug_direct_y(self._key, self.dev.ctx, int(seed), int(index0), int(count),
+                                                _ptr(yp), _ptr(yq)), "debug_direct_y")
+        return yp, yq
+
     def decrypt_u64(self, c, full=False, short=False):
         """Low 64 bits of m = L(c^lambda mod n^2) mu mod n (paillier.cpp:153-156).
         short: plaintexts known to be < p (FedTree's codec values and their sums):

@@ -384,6 +384,19 @@ int fthe_wire_decode(const uint8_t *in, size_t len, int words, uint32_t *g, uint
 int fthe_encode_fixed_dev(fthe_ctx *ctx, const float *x, size_t count, uint64_t *m);
 int fthe_decode_fixed_dev(fthe_ctx *ctx, const uint64_t *m, size_t count, float *x);
 
+/* ---- test hook: the randomness of the direct-y CRT encrypt ----------------
+ * A key holder's fthe_encrypt_u64[_dev] with r == NULL draws, per ciphertext,
+ * y_p uniform in [1, p) and y_q uniform in [1, q) and computes
+ * (1 + m n) y_P^P mod P^2 for P = p, q: the encryption under
+ * r = CRT(y_p^(q^-1 mod p-1) mod p, y_q^(p^-1 mod q-1) mod q).  This returns the
+ * (y_p, y_q) a call with this nonzero rng_seed draws for ciphertexts
+ * [index0, index0 + count) (the draws depend on the index only, not on the
+ * chunking), pq_words = words of max(p, q) each, little-endian, into host yp /
+ * yq (count * pq_words words), so tests can pin device-drawn ciphertexts
+ * against PowerMod(g, m, n^2) PowerMod(r, n, n^2) (paillier.cpp:134-137). */
+int fthe_debug_direct_y(fthe_key *key, fthe_ctx *ctx, uint64_t rng_seed, uint64_t index0, size_t count,
+                        uint32_t *yp, uint32_t *yq);
+
 /* ---- profiling hooks: time of the last call's kernels on the stream ------ */
 double fthe_last_kernel_ms(fthe_ctx *ctx);
 /* Montgomery products executed by the last call (for roofline accounting). */

@@ -252,4 +252,18 @@ class RefGMP:
         lib.ref_shared_r.argtypes = [P, ctypes.c_int, P]
         lib.ref_encrypt_batch.argtypes = [P, ctypes.c_int, P, ctypes.c_long, P, ctypes.c_int]
         lib.ref_num_threads.restype = ctypes.c_int
+        lib.ref_key_from_primes.restype = P
+        lib.ref_key_from_primes.argtypes = [P, P, ctypes.c_int]
+        lib.ref_decrypt_batch.argtypes = [P, ctypes.c_int, P, ctypes.c_long, P, ctypes.c_int]
+        lib.ref_add_batch.argtypes = [P, ctypes.c_int, P, P, ctypes.c_long, P, ctypes.c_int]
+        lib.ref_merge_batch.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_long, P, ctypes.c_int]
         self.lib = lib
+
+    def key_from_primes(self, p, q):
+        """Handle of a Paillier_GMP holding the key of primes p, q (ints); free with lib.ref_free."""
+        w = (max(p.bit_length(), q.bit_length()) + 31) // 32
+        pw, qw = to_words(p, w), to_words(q, w)
+        h = self.lib.ref_key_from_primes(pw.ctypes.data, qw.ctypes.data, w)
+        if not h:
+            raise ValueError("reference key: mu not invertible")
+        return h

@@ -7,6 +7,7 @@
 #include "FedTree/Encryption/paillier_gmp.h"   // /root/reference/include
 #include <cstring>
 #include <cstdint>
+#include <vector>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -115,6 +116,103 @@ void ref_mul(void *h, int nw, const uint32_t *x, uint64_t y, uint32_t *out) {
     exp_words(out, 2 * nw, r);
     mpz_clear(a); mpz_clear(e); mpz_clear(r);
 }
+// A Paillier_GMP whose fields hold the key of primes p, q (w words each): the state
+// Paillier_GMP::keyGen leaves behind (paillier_gmp.cpp:185-210) -- n, n^2, g = n + 1,
+// the p, q fields holding p - 1, q - 1, lambda = lcm(p-1, q-1),
+// mu = L(g^lambda mod n^2)^-1 mod n -- for injected primes, so the CPU baseline runs
+// the reference's own encrypt / decrypt / add on the bench's key.  NULL if mu is not
+// invertible.
+void *ref_key_from_primes(const uint32_t *pw, const uint32_t *qw, int w) {
+    Paillier_GMP *k = new Paillier_GMP();
+    mpz_t P, Q, t;
+    mpz_init(P); mpz_init(Q); mpz_init(t);
+    imp_words(P, pw, w); imp_words(Q, qw, w);
+    mpz_mul(k->n, P, Q);
+    mpz_add_ui(k->generator, k->n, 1);
+    mpz_sub_ui(k->p, P, 1);
+    mpz_sub_ui(k->q, Q, 1);
+    mpz_lcm(k->lambda, k->p, k->q);
+    mpz_mul(k->n_square, k->n, k->n);
+    k->key_length = (uint32_t)(2 * mpz_sizeinbase(k->n, 2));      // GMP semantics: n has key_length / 2 bits
+    mpz_powm(t, k->generator, k->lambda, k->n_square);
+    k->L_function(k->mu, t, k->n);
+    int ok = mpz_invert(k->mu, k->mu, k->n);
+    mpz_clear(P); mpz_clear(Q); mpz_clear(t);
+    if (!ok) { delete k; return nullptr; }
+    return k;
+}
+
+static void set_threads(int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+}
+
+// Server::decrypt_gh_pairs' CPU loop (server.h:105-109): OpenMP over elements, each one
+// Paillier_GMP::decrypt (paillier_gmp.cpp:75-85, PowerMod(c, lambda, n^2), no CRT).
+// out: low 64 bits of each plaintext.
+void ref_decrypt_batch(void *h, int nw, const uint32_t *c, long count, uint64_t *out, int threads) {
+    Paillier_GMP *k = (Paillier_GMP *)h;
+    set_threads(threads);
+    #pragma omp parallel for schedule(dynamic, 4)
+    for (long i = 0; i < count; i++) {
+        mpz_t cz, m; mpz_init(cz);
+        imp_words(cz, c + (size_t)i * 2 * nw, 2 * nw);
+        k->decrypt(m, cz);
+        uint64_t lo = 0; size_t cnt = 0;
+        uint32_t w[2] = {0, 0};
+        if (mpz_sizeinbase(m, 2) <= 64) mpz_export(w, &cnt, -1, 4, 0, 0, m);
+        else { mpz_t t; mpz_init(t); mpz_fdiv_r_2exp(t, m, 64); mpz_export(w, &cnt, -1, 4, 0, 0, t); mpz_clear(t); }
+        lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        out[i] = lo;
+        mpz_clear(cz); mpz_clear(m);
+    }
+}
+
+// Pairwise homomorphic adds, Paillier_GMP::add (paillier_gmp.cpp:16-21), OpenMP over elements.
+void ref_add_batch(void *h, int nw, const uint32_t *a, const uint32_t *b, long count, uint32_t *out, int threads) {
+    Paillier_GMP *k = (Paillier_GMP *)h;
+    set_threads(threads);
+    #pragma omp parallel for schedule(static)
+    for (long i = 0; i < count; i++) {
+        mpz_t x, y, r; mpz_init(x); mpz_init(y);
+        imp_words(x, a + (size_t)i * 2 * nw, 2 * nw);
+        imp_words(y, b + (size_t)i * 2 * nw, 2 * nw);
+        k->add(r, x, y);
+        exp_words(out + (size_t)i * 2 * nw, 2 * nw, r);
+        mpz_clear(x); mpz_clear(y); mpz_clear(r);
+    }
+}
+
+// The k-party merge of merge_histograms_server_propose (hist_tree_builder.cpp:1026-1037):
+// for each party after the first, `omp parallel for` over bins of dest = dest + src, each a
+// Paillier_GMP::add into a fresh result (non-aliased).  x: k * count rows (party-major);
+// out: count rows, starting as party 0's histogram.  (k - 1) * count adds.
+void ref_merge_batch(void *h, int nw, const uint32_t *x, int kparties, long count, uint32_t *out, int threads) {
+    Paillier_GMP *k = (Paillier_GMP *)h;
+    set_threads(threads);
+    const size_t cw = 2 * (size_t)nw;
+    std::vector<__mpz_struct> acc(count);
+    #pragma omp parallel for schedule(static)
+    for (long j = 0; j < count; j++) { mpz_init(&acc[j]); imp_words(&acc[j], x + (size_t)j * cw, (int)cw); }
+    for (int i = 1; i < kparties; i++) {
+        const uint32_t *src = x + (size_t)i * count * cw;
+        #pragma omp parallel for schedule(static)
+        for (long j = 0; j < count; j++) {
+            mpz_t y, r; mpz_init(y);
+            imp_words(y, src + (size_t)j * cw, (int)cw);
+            mpz_t a; a[0] = acc[j];
+            k->add(r, a, y);
+            mpz_swap(&acc[j], r);
+            mpz_clear(y); mpz_clear(r);
+        }
+    }
+    #pragma omp parallel for schedule(static)
+    for (long j = 0; j < count; j++) { exp_words(out + (size_t)j * cw, (int)cw, &acc[j]); mpz_clear(&acc[j]); }
+}
+
 // The r every Paillier_GMP::encrypt call draws (paillier_gmp.cpp:40-52 and
 // paillier_gpu.cu:262-272): first nonzero mpz_urandomm(n) of a freshly
 // initialised, unseeded MT state.  Restated with the same GMP calls so the

@@ -1,0 +1,53 @@
+"""bench.py's multi-rank harness on the CPU: `python bench.py --gpus 2` (no torchrun) spawns
+the two rank processes itself, they rendezvous over gloo on 127.0.0.1, time the steps
+between barriers, gather per-rank times and rank 0 prints one line with n_gpus = 2.
+--dry-run replaces the GPU step with a sleep, so nothing here touches a device."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       env=env, timeout=240)
+    return r
+
+
+def test_spawns_n_ranks():
+    r = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout                    # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["dry_run"]
+    per = line["per_rank"]
+    assert sorted(p["rank"] for p in per) == [0, 1]
+    assert sorted(p["local_rank"] for p in per) == [0, 1]
+    assert len({p["pid"] for p in per}) == 2             # two processes
+    assert line["elapsed_max_s"] == max(p["elapsed_s"] for p in per)
+    assert line["elapsed_max_s"] >= 3 * 0.02
+
+
+def test_single_rank_default():
+    r = _run(["--steps", "1", "--warmup", "0", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["n_gpus"] == 1 and len(line["per_rank"]) == 1
+
+
+def test_world_size_must_match_gpus():
+    r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def test_failing_rank_fails_the_launch():
+    """Rank 1 dies before the rendezvous: the parent ends rank 0 (blocked in the rendezvous)
+    and exits with rank 1's status instead of hanging."""
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--dry-run"], {"FTHE_BENCH_FAIL_RANK": "1"})
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])

@@ -15,6 +15,16 @@ from conftest import golden_key, load_golden
 pytestmark = pytest.mark.gpu
 
 
+def _run_all(work, T, timeout=120):
+    """Daemon threads; a queue that deadlocks fails the test instead of hanging pytest."""
+    th = [threading.Thread(target=work, args=(i,), daemon=True) for i in range(T)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=timeout)
+    assert not any(t.is_alive() for t in th), "shared queue deadlocked"
+
+
 @pytest.fixture(scope="module")
 def pl():
     from fedtree_amd.paillier import Device, Paillier
@@ -64,11 +74,7 @@ def test_shared_many_threads(pl):
         except Exception as e:
             bad.append((i, repr(e)))
 
-    th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=120)
+    _run_all(work, T)
     assert not bad, bad
 
 
@@ -90,11 +96,7 @@ def test_encrypt_shared_many_threads(pl):
         except Exception as e:
             bad.append((i, repr(e)))
 
-    th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=120)
+    _run_all(work, T)
     assert not bad, bad
     for i in range(T):
         assert np.array_equal(pl.decrypt_u64(outs[i]), ms[i]), i
@@ -110,3 +112,37 @@ def test_shared_public_key_rejected(pl):
     c = pl.encrypt_u64(np.array([1], dtype=np.uint64), seed=1)
     with pytest.raises(_lib.FtheError):
         pub.decrypt_u64_shared(c)
+
+
+def test_shared_errors_do_not_block_other_callers(pl):
+    """Requests that fail inside a merged batch of one key's queue (public-form exact
+    fixed-base without published bases -> FTHE_ERR_UNSUPPORTED) return their error; the other
+    callers of the same batches still get their ciphertexts and nobody hangs."""
+    from fedtree_amd import _lib
+    rng = np.random.default_rng(11)
+    T = 16
+    ms = [rng.integers(0, 2**64, 3, dtype=np.uint64) for _ in range(T)]
+    status, outs = [None] * T, [None] * T
+    go = threading.Barrier(T)
+
+    def work(i):
+        go.wait()
+        try:
+            if i % 4 == 1:        # bad flags for this key: public-form exact fixed-base, no bases published
+                m = np.ascontiguousarray(ms[i])
+                out = np.zeros((len(m), 2 * pl.n_words), np.uint32)
+                status[i] = pl.lib.fthe_encrypt_shared(pl._key, m.ctypes.data, len(m), out.ctypes.data,
+                                                       _lib.FTHE_ENC_FIXED_BASE_EXACT | _lib.FTHE_ENC_PUBLIC)
+            else:
+                outs[i] = pl.encrypt_u64_shared(ms[i])
+                status[i] = 0
+        except Exception as e:    # noqa: BLE001
+            status[i] = repr(e)
+
+    _run_all(work, T)
+    for i in range(T):
+        if i % 4 == 1:
+            assert status[i] == _lib.FTHE_ERR_UNSUPPORTED, (i, status[i])
+        else:
+            assert status[i] == 0, (i, status[i])
+            assert np.array_equal(pl.decrypt_u64(outs[i]), ms[i])

@@ -119,3 +119,52 @@ def test_host_codec_matches_golden():
     assert [int(x) for x in encode_fixed(f)] == g["encode_gmp"]
     dec = decode_fixed(np.array(g["decode_in"], dtype=np.uint64))
     assert [int(x) for x in dec.view(np.uint32)] == g["decode_out_f32_bits"]
+
+
+def _ref_or_skip():
+    try:
+        return pyoracle.RefGMP()
+    except OSError:
+        pytest.skip("oracle/_ref not built (reference sources absent)")
+
+
+def test_ref_key_from_primes_reproduces_reference(gold):
+    """ref_key_from_primes (the CPU baseline's same-key handle) leaves the fields the
+    reference's keyGen leaves, and the reference's own encrypt / decrypt / add / merge run on
+    it reproduce the golden vectors (its unseeded MT draws the same shared r for this n)."""
+    ref = _ref_or_skip()
+    p, q = golden_key(gold)
+    h = ref.key_from_primes(p, q)
+    try:
+        nw = gold["n_words"]
+        assert ref.lib.ref_n_words(h) == nw
+        bufs = [np.zeros(nw, np.uint32) for _ in range(5)]
+        ref.lib.ref_export(h, nw, *[b.ctypes.data for b in bufs])
+        n, pm1, qm1, lam, mu = (pyoracle.from_words(b) for b in bufs)
+        assert (n, pm1, qm1, lam, mu) == (int(gold["n"], 16), int(gold["p_minus_1"], 16), int(gold["q_minus_1"], 16),
+                                          int(gold["lambda"], 16), int(gold["mu"], 16))
+        cases = gold["cases"][:6]
+        ms = np.array([c["m"] for c in cases], dtype=np.uint64)
+        ct = np.zeros((len(ms), 2 * nw), np.uint32)
+        ref.lib.ref_encrypt_batch(h, nw, ms.ctypes.data, len(ms), ct.ctypes.data, 2)
+        want = pyoracle.ints_to_words([int(c["c"], 16) for c in cases], 2 * nw)
+        assert np.array_equal(ct, want)
+        lo = np.zeros(len(ms), np.uint64)
+        ref.lib.ref_decrypt_batch(h, nw, want.ctypes.data, len(ms), lo.ctypes.data, 2)
+        assert np.array_equal(lo, ms)
+        allc = pyoracle.ints_to_words([int(c["c"], 16) for c in gold["cases"]], 2 * nw)
+        a = np.ascontiguousarray(allc[[x["i"] for x in gold["adds"]]])
+        b = np.ascontiguousarray(allc[[x["j"] for x in gold["adds"]]])
+        s = np.zeros_like(a)
+        ref.lib.ref_add_batch(h, nw, a.ctypes.data, b.ctypes.data, len(a), s.ctypes.data, 2)
+        assert [pyoracle.from_words(x) for x in s] == [int(x["c"], 16) for x in gold["adds"]]
+        hist = gold["hist"]
+        x = np.stack([pyoracle.ints_to_words([int(hist["enc_zero"], 16)] * hist["bins"], 2 * nw)] +
+                     [pyoracle.ints_to_words([int(v, 16) for v in hist["ct"][pi]], 2 * nw)
+                      for pi in range(hist["parties"])])
+        x = np.ascontiguousarray(x)
+        out = np.zeros((hist["bins"], 2 * nw), np.uint32)
+        ref.lib.ref_merge_batch(h, nw, x.ctypes.data, x.shape[0], hist["bins"], out.ctypes.data, 2)
+        assert [pyoracle.from_words(v) for v in out] == [int(v, 16) for v in hist["merged"]]
+    finally:
+        ref.lib.ref_free(h)
