@@ -81,6 +81,8 @@ _PROTOS = {
     "fthe_from_mont_dev": (_I, [_P, _P, _P, _SZ, _P]),
     "fthe_add_mont_dev": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "fthe_add": (_I, [_P, _P, _P, _P, _SZ, _P]),
+    "fthe_add_shared": (_I, [_P, _P, _P, _SZ, _P]),
+    "fthe_scalar_mul_u64_shared": (_I, [_P, _P, _U64, _SZ, _P]),
     "fthe_scalar_mul_u64_dev": (_I, [_P, _P, _P, _U64, _SZ, _P]),
     "fthe_scalar_mul_u64": (_I, [_P, _P, _P, _U64, _SZ, _P]),
     "fthe_scalar_mul_words_dev": (_I, [_P, _P, _P, _P, _I, _SZ, _P]),
@@ -103,6 +105,8 @@ _PROTOS = {
     "fthe_reduce_segments": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
     "fthe_reduce_segments_csr_dev": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P]),
     "fthe_histogram_dev": (_I, [_P, _P, _P, _SZ, _I, _P, _I, _P, _I, _P, _SZ, _P]),
+    "fthe_histogram_zero_first_dev": (_I, [_P, _P, _P, _SZ, _I, _P, _I, _P, _I, _P, _SZ, _P, _P]),
+    "fthe_reduce_segments_zero_first_dev": (_I, [_P, _P, _P, _SZ, _P, _P, _SZ, _P, _P]),
     "fthe_encode_fixed_dev": (_I, [_P, _P, _SZ, _P]),
     "fthe_decode_fixed_dev": (_I, [_P, _P, _SZ, _P]),
     "fthe_last_kernel_ms": (ctypes.c_double, [_P]),

@@ -207,6 +207,7 @@ struct fthe_ctx {
     hipFunction_t fn[MAX_VARIANTS] = {};
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
     DevBuf hb[6];                           // histogram CSR / segmented-product plan (device)
+    DevBuf ezm;                             // zero-first folds: Enc(0) rows masked to the populated segments
     DevBuf dec[3];                          // decimal codec: 9-digit chunks, lengths, leading chunk / error flag
     void *cub_tmp = nullptr; size_t cub_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -245,18 +246,24 @@ struct EncReq {
     const uint64_t *m; size_t count; uint32_t *out; int flags;
     int rc = FTHE_OK; bool done = false;
 };
+struct OpReq {                               // fthe_add_shared / fthe_scalar_mul_u64_shared
+    bool mul; const uint32_t *a, *b; uint64_t k; size_t count; uint32_t *out;
+    int rc = FTHE_OK; bool done = false;
+};
 struct Coalescer {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<DecReq *> pending;
     std::vector<EncReq *> epending;          // fthe_encrypt_shared: its own leader and context
-    bool leader = false, eleader = false;
-    fthe_ctx *ctx = nullptr, *ectx = nullptr;   // the key's own contexts, one leader each at a time
-    std::vector<uint32_t> ct, full, eout;
+    std::vector<OpReq *> opending;           // fthe_add_shared / _scalar_mul_u64_shared: a third one
+    bool leader = false, eleader = false, oleader = false;
+    fthe_ctx *ctx = nullptr, *ectx = nullptr, *octx = nullptr;   // the key's own contexts, one leader each
+    std::vector<uint32_t> ct, full, eout, oa, ob, oout;
     std::vector<uint64_t> lo, em;
     ~Coalescer() {
         if (ctx) fthe_ctx_destroy(ctx);
         if (ectx) fthe_ctx_destroy(ectx);
+        if (octx) fthe_ctx_destroy(octx);
     }
 };
 
@@ -2859,6 +2866,20 @@ int reduce_segments_csr(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64
 }
 }  // namespace
 
+// out[s] <- out[s] * enc_zero[s] for every populated segment s (seg: device, nseg + 1): the Enc(0)
+// the reference folds into a bin on its first add (Q10).  Empty segments keep the integer 1.
+static int fold_zero_first(fthe_key *k, fthe_ctx *c, const int64_t *seg_dev, size_t nseg, const uint32_t *enc_zero,
+                           uint32_t *out) {
+    const int cw = 2 * k->n_words;
+    int rc;
+    if ((rc = c->ezm.ensure(nseg * (size_t)cw * 4))) return rc;
+    hipLaunchKernelGGL(k_zero_first_rows, dim3((unsigned)((nseg * cw + 255) / 256)), dim3(256), 0, c->stream,
+                       enc_zero, seg_dev, nseg, cw, (uint32_t *)c->ezm.p);
+    const uint32_t *xs[2] = {out, (const uint32_t *)c->ezm.p};
+    Mpz R2; mpz_powm_ui(R2, k->mn2.m.R, 2ul, k->n2);
+    return rowprod_impl(k, c, xs, 2, nseg, out, R2);          // row-wise, alias-safe
+}
+
 extern "C" int fthe_reduce_segments_csr_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
                                             const int64_t *seg_ptr, const int64_t *idx, size_t nseg, uint32_t *out) {
     if (!k || !c || !seg_ptr || (nseg && !out)) return FTHE_ERR_ARG;
@@ -2879,9 +2900,9 @@ extern "C" int fthe_reduce_segments_csr_dev(fthe_key *k, fthe_ctx *c, const uint
 // bin) segments from dense_bin_id (atomic count, scan, atomic scatter), then the
 // segmented K-way product.  out[p*n_bins + cut[f] + bid] = prod x[p*count + iid]
 // over the selected iid with bin_ids[iid*n_col + f] == bid != max_num_bin.
-extern "C" int fthe_histogram_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, int planes,
-                                  const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
-                                  const int32_t *inst, size_t n_sel, uint32_t *out) {
+static int histogram_impl(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, int planes,
+                          const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
+                          const int32_t *inst, size_t n_sel, const uint32_t *enc_zero, uint32_t *out) {
     if (!k || !c || !cut_col_ptr || n_col <= 0 || planes <= 0 || (!inst && n_sel > count)) return FTHE_ERR_ARG;
     if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
     if (cut_col_ptr[0] != 0) return FTHE_ERR_ARG;
@@ -2922,7 +2943,23 @@ extern "C" int fthe_histogram_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, s
         hipLaunchKernelGGL(k_hist_scatter, dim3(gb), dim3(256), 0, st, bin_ids, n_col, d_cut, max_num_bin, inst, n_sel,
                            planes, n_bins, count, seg, cursor, idx);
     // io[0] (idx) and hb[1] (seg) stay untouched by the product passes (io[1]/io[2], hb[2..5])
-    return reduce_segments_csr(k, c, x, seg, idx, nseg, total, out);
+    if ((rc = reduce_segments_csr(k, c, x, seg, idx, nseg, total, out))) return rc;
+    return enc_zero ? fold_zero_first(k, c, seg, nseg, enc_zero, out) : FTHE_OK;
+}
+
+extern "C" int fthe_histogram_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, int planes,
+                                  const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
+                                  const int32_t *inst, size_t n_sel, uint32_t *out) {
+    return histogram_impl(k, c, x, count, planes, bin_ids, n_col, cut_col_ptr, max_num_bin, inst, n_sel, nullptr, out);
+}
+
+extern "C" int fthe_histogram_zero_first_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count, int planes,
+                                             const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr,
+                                             int max_num_bin, const int32_t *inst, size_t n_sel,
+                                             const uint32_t *enc_zero, uint32_t *out) {
+    if (!enc_zero) return FTHE_ERR_ARG;
+    return histogram_impl(k, c, x, count, planes, bin_ids, n_col, cut_col_ptr, max_num_bin, inst, n_sel, enc_zero,
+                          out);
 }
 
 // Segmented inclusive scan: out[t] = prod_{t' in [seg_start(t), t]} x[t'] mod n^2, the
@@ -2970,6 +3007,21 @@ extern "C" int fthe_scan_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t *
         bufsel = 3 - bufsel;
     }
     return end_call(c, gp.Lc);
+}
+
+// Segmented product with the reference's Enc(0)-first semantics: out[s] = enc_zero[s] * prod(members)
+// for a populated segment, 1 for an empty one.  seg_ptr / idx host arrays as fthe_reduce_segments_dev.
+extern "C" int fthe_reduce_segments_zero_first_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
+                                                   const int64_t *seg_ptr, const int64_t *idx, size_t nseg,
+                                                   const uint32_t *enc_zero, uint32_t *out) {
+    if (!enc_zero && nseg) return FTHE_ERR_ARG;
+    int rc = fthe_reduce_segments_dev(k, c, x, count, seg_ptr, idx, nseg, out);
+    if (rc || !nseg) return rc;
+    if ((rc = c->hb[1].ensure((nseg + 1) * 8))) return rc;
+    HIPOK(hipMemcpyAsync(c->hb[1].p, seg_ptr, (nseg + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    rc = fold_zero_first(k, c, (const int64_t *)c->hb[1].p, nseg, enc_zero, out);
+    HIPOK(hipStreamSynchronize(c->stream));                 // seg_ptr is the caller's host array
+    return rc;
 }
 
 extern "C" int fthe_reduce_segments(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,
@@ -3436,4 +3488,91 @@ extern "C" int fthe_encrypt_shared(fthe_key *k, const uint64_t *m, size_t count,
         }
         co->cv.wait(lk);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Shared ciphertext add / scalar mul: GHPair::operator+, +=, - of the USE_HIP build
+// (common.h:150-337) call these once per GHPair from FedTree's OpenMP workers
+// (hist_tree_builder.cpp:574-591, 1031-1047); the key's third queue merges the concurrent
+// calls into one launch per operation kind (adds together, muls per exponent).  Inputs are
+// staged before any output is written, so out may alias a or b (fixes SURVEY Q11).
+static void coalesced_ops_impl(fthe_key *k, Coalescer *co, const std::vector<OpReq *> &batch) {
+    const size_t cw = 2 * (size_t)k->n_words;
+    int rc0 = FTHE_OK;
+    if (!co->octx) rc0 = fthe_ctx_create(k->device, &co->octx);
+    // kinds: adds (mul == false), then one group per distinct exponent
+    std::vector<std::pair<bool, uint64_t>> kinds;
+    for (OpReq *r : batch) {
+        std::pair<bool, uint64_t> kd{r->mul, r->mul ? r->k : 0};
+        if (std::find(kinds.begin(), kinds.end(), kd) == kinds.end()) kinds.push_back(kd);
+    }
+    for (const auto &kd : kinds) {
+        size_t tot = 0;
+        for (OpReq *r : batch) if (r->mul == kd.first && (!kd.first || r->k == kd.second)) tot += r->count;
+        int rc = rc0;
+        if (!rc) {
+            co->oa.resize(tot * cw); co->oout.resize(tot * cw);
+            if (!kd.first) co->ob.resize(tot * cw);
+            size_t at = 0;
+            for (OpReq *r : batch) {
+                if (r->mul != kd.first || (kd.first && r->k != kd.second)) continue;
+                memcpy(&co->oa[at * cw], r->a, r->count * cw * 4);
+                if (!kd.first) memcpy(&co->ob[at * cw], r->b, r->count * cw * 4);
+                at += r->count;
+            }
+            rc = kd.first ? fthe_scalar_mul_u64(k, co->octx, co->oa.data(), kd.second, tot, co->oout.data())
+                          : fthe_add(k, co->octx, co->oa.data(), co->ob.data(), tot, co->oout.data());
+        }
+        size_t at = 0;
+        for (OpReq *r : batch) {
+            if (r->mul != kd.first || (kd.first && r->k != kd.second)) continue;
+            r->rc = rc;
+            if (!rc) memcpy(r->out, &co->oout[at * cw], r->count * cw * 4);
+            at += r->count;
+        }
+    }
+    trim(co->oa); trim(co->ob); trim(co->oout);
+}
+
+static int op_shared(fthe_key *k, OpReq &r) {
+    Coalescer *co = key_coalescer(k);
+    if (!co) return FTHE_ERR_NOMEM;
+    std::unique_lock<std::mutex> lk(co->mu);
+    try { co->opending.push_back(&r); } catch (...) { return FTHE_ERR_NOMEM; }
+    for (;;) {
+        if (r.done) return r.rc;
+        if (!co->oleader) {
+            co->oleader = true;
+            std::vector<OpReq *> batch;
+            batch.swap(co->opending);                // includes r
+            lk.unlock();
+            try {
+                coalesced_ops_impl(k, co, batch);
+            } catch (...) {
+                for (OpReq *q : batch) q->rc = FTHE_ERR_NOMEM;
+            }
+            lk.lock();
+            for (OpReq *q : batch) q->done = true;
+            co->oleader = false;
+            co->cv.notify_all();
+            return r.rc;
+        }
+        co->cv.wait(lk);
+    }
+}
+
+extern "C" int fthe_add_shared(fthe_key *k, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+    if (!k || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (!count) return FTHE_OK;
+    OpReq r{false, a, b, 0, count, out};
+    return op_shared(k, r);
+}
+
+extern "C" int fthe_scalar_mul_u64_shared(fthe_key *k, const uint32_t *x, uint64_t e, size_t count, uint32_t *out) {
+    if (!k || ((!x || !out) && count)) return FTHE_ERR_ARG;
+    if (!k->pub_ok) return FTHE_ERR_UNSUPPORTED;
+    if (!count) return FTHE_OK;
+    OpReq r{true, x, nullptr, e, count, out};
+    return op_shared(k, r);
 }

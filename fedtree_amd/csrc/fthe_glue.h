@@ -40,6 +40,7 @@ __global__ void k_hist_scatter(const uint8_t *bin, int n_col, const int32_t *cut
 __global__ void k_group_counts(const int64_t *seg, size_t nseg, int K, int64_t *ng);
 __global__ void k_plan_groups(const int64_t *seg, const int64_t *members, size_t nseg, const int64_t *gptr, size_t G,
                               int K, int64_t *gidx);
+__global__ void k_zero_first_rows(const uint32_t *ez, const int64_t *seg, size_t nseg, int cw, uint32_t *ezm);
 __global__ void k_u64_to_i64(const unsigned long long *a, int64_t *b, size_t n);
 int exclusive_scan_i64(const int64_t *in, int64_t *out, size_t n, void *&tmp, size_t &tmp_bytes, hipStream_t st);
 // fthe_dec.hip: decimal wire strings on the device

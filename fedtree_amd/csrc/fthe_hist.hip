@@ -98,4 +98,16 @@ int exclusive_scan_i64(const int64_t *in, int64_t *out, size_t n, void *&tmp, si
     return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, n, st) == hipSuccess ? 0 : -2;
 }
 
+// The reference's first `hist[bin] = hist[bin] + gh[iid]` into an unencrypted zero encrypts that zero
+// (GHPair::operator+, common.h:156-160), so a populated bin is Enc(0) * prod(members).
+// ezm[s] = enc_zero[s] for a populated segment (seg[s+1] > seg[s]) and the integer 1 for an empty
+// one, which keeps the reference's unencrypted zero; one thread per word.
+__global__ void k_zero_first_rows(const uint32_t *__restrict__ ez, const int64_t *__restrict__ seg, size_t nseg,
+                                  int cw, uint32_t *__restrict__ ezm) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg * (size_t)cw) return;
+    const size_t s = t / (size_t)cw, w = t - s * (size_t)cw;
+    ezm[t] = seg[s + 1] > seg[s] ? ez[t] : (uint32_t)(w == 0);
+}
+
 }  // namespace fthe

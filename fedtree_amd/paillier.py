@@ -388,6 +388,23 @@ class Paillier:
         _lib.check(self.lib.fthe_add(self._key, self.dev.ctx, _ptr(a), _ptr(b), len(a), _ptr(out)), "add")
         return out
 
+    def add_shared(self, a, b, out=None):
+        """add_batch through the key's coalescing queue (fthe_add_shared): thread-safe on one
+        Paillier object, concurrent calls share a launch; out may be a or b (alias-safe)."""
+        a = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self._cw())
+        b = np.ascontiguousarray(b, dtype=np.uint32).reshape(-1, self._cw())
+        out = np.zeros_like(a) if out is None else out
+        _lib.check(self.lib.fthe_add_shared(self._key, _ptr(a), _ptr(b), len(a), _ptr(out)), "add_shared")
+        return out
+
+    def scalar_mul_shared(self, x, k, out=None):
+        """scalar_mul through the key's coalescing queue (fthe_scalar_mul_u64_shared)."""
+        x = np.ascontiguousarray(x, dtype=np.uint32).reshape(-1, self._cw())
+        out = np.zeros_like(x) if out is None else out
+        _lib.check(self.lib.fthe_scalar_mul_u64_shared(self._key, _ptr(x), int(k), len(x), _ptr(out)),
+                   "scalar_mul_shared")
+        return out
+
     def sub_batch(self, a, b):
         """a * b^(2^64-1) mod n^2: GHPair::operator- with both sides encrypted
         (common.h:311-317), one fused device program."""
@@ -528,19 +545,36 @@ class Paillier:
         return out
 
     @_stream_ordered
-    def histogram_dev(self, x, count, planes, bin_ids, cut_col_ptr, max_num_bin, out, inst=None):
+    def histogram_dev(self, x, count, planes, bin_ids, cut_col_ptr, max_num_bin, out, inst=None, enc_zero=None):
         """Node histogram on the device (hist_tree_builder.cpp:565-595, :640-664).
         x: device (planes*count, 2nw) ciphertexts (g plane, h plane); bin_ids: device
         uint8 (count, n_col); inst: device int32 instance ids of the node or None;
-        out: device (planes*n_bins, 2nw)."""
+        out: device (planes*n_bins, 2nw).  enc_zero: device (planes*n_bins, 2nw) Enc(0) rows folded
+        into every populated bin -- the reference's first add into an unencrypted zero
+        (common.h:156-160; fthe_histogram_zero_first_dev)."""
         cut = np.ascontiguousarray(cut_col_ptr, dtype=np.int32)
         n_col = len(cut) - 1
         n_sel = inst.numel() if inst is not None else count
-        _lib.check(self.lib.fthe_histogram_dev(
-            self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), int(count), int(planes),
-            ctypes.c_void_p(bin_ids.data_ptr()), n_col, _ptr(cut), int(max_num_bin),
-            ctypes.c_void_p(inst.data_ptr()) if inst is not None else None, int(n_sel),
-            ctypes.c_void_p(out.data_ptr())), "histogram_dev")
+        args = [self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), int(count), int(planes),
+                ctypes.c_void_p(bin_ids.data_ptr()), n_col, _ptr(cut), int(max_num_bin),
+                ctypes.c_void_p(inst.data_ptr()) if inst is not None else None, int(n_sel)]
+        if enc_zero is None:
+            _lib.check(self.lib.fthe_histogram_dev(*args, ctypes.c_void_p(out.data_ptr())), "histogram_dev")
+        else:
+            _lib.check(self.lib.fthe_histogram_zero_first_dev(*args, ctypes.c_void_p(enc_zero.data_ptr()),
+                                                              ctypes.c_void_p(out.data_ptr())), "histogram_zero_first")
+        return out
+
+    @_stream_ordered
+    def reduce_segments_zero_first_dev(self, x, seg_ptr, enc_zero, out, idx=None):
+        """reduce_segments_dev with an Enc(0) row per segment folded into every populated one
+        (the reference's Q10 sequence, fthe_reduce_segments_zero_first_dev)."""
+        seg = np.ascontiguousarray(seg_ptr, dtype=np.int64)
+        ix = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+        cnt = x.numel() // self._cw()
+        _lib.check(self.lib.fthe_reduce_segments_zero_first_dev(
+            self._key, self.dev.ctx, ctypes.c_void_p(x.data_ptr()), cnt, _ptr(seg), _ptr(ix), len(seg) - 1,
+            ctypes.c_void_p(enc_zero.data_ptr()), ctypes.c_void_p(out.data_ptr())), "reduce_segments_zero_first")
         return out
 
     def encrypt_words(self, m, r=None, seed=0, public=False, fixed_base_exact=False):

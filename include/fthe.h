@@ -260,6 +260,16 @@ int fthe_add_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t
 int fthe_add(fthe_key *key, fthe_ctx *ctx, const uint32_t *a, const uint32_t *b,
              size_t count, uint32_t *out);
 
+/* Coalescing host-resident add / scalar mul for many concurrent single-pair callers of one key:
+ * GHPair::operator+, += and - of the USE_HIP build (common.h:150-337; integration/fthe_ghpair_key.h)
+ * from FedTree's OpenMP loops (hist_tree_builder.cpp:574-591, 1031-1047; tree.cpp:24).  Thread-safe,
+ * no context argument: calls arriving while a batch runs are merged into the next launch (adds
+ * together, scalar muls per exponent) on a context the key owns.  Alias-safe: out may equal a,
+ * b or x (the reference's add(s, s, c) zeroes s).  Same results as fthe_add /
+ * fthe_scalar_mul_u64. */
+int fthe_add_shared(fthe_key *key, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out);
+int fthe_scalar_mul_u64_shared(fthe_key *key, const uint32_t *x, uint64_t k, size_t count, uint32_t *out);
+
 /* ---- Montgomery-resident rows (device; not in the reference) ---------------
  * A fresh add costs two Montgomery products (x y R^-1, then a product by R^2
  * mod n^2).  Rows kept resident in Montgomery form, x R mod n^2 (same 2 n_words
@@ -341,6 +351,20 @@ int fthe_reduce_segments_csr_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x
 int fthe_histogram_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count, int planes,
                        const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
                        const int32_t *inst, size_t n_sel, uint32_t *out);
+
+/* The reference's exact sequence for a bin: its accumulator starts as an unencrypted
+ * zero GHPair, and the first `hist[bin] = hist[bin] + gh[iid]` encrypts that zero with a fresh r
+ * (GHPair::operator+, common.h:156-160), so a populated bin is Enc(0) * prod(members) mod n^2.
+ * enc_zero: device, one Enc(0) row per segment (planes * n_bins rows for the histogram; a fresh
+ * encryption each, e.g. fthe_encrypt_u64_dev of zeros, or the reference's shared r to reproduce
+ * its ciphertexts); folded into every populated segment, while an empty one stays the integer 1.
+ * Same arguments otherwise as fthe_histogram_dev / fthe_reduce_segments_dev. */
+int fthe_histogram_zero_first_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count, int planes,
+                                  const uint8_t *bin_ids, int n_col, const int32_t *cut_col_ptr, int max_num_bin,
+                                  const int32_t *inst, size_t n_sel, const uint32_t *enc_zero, uint32_t *out);
+int fthe_reduce_segments_zero_first_dev(fthe_key *key, fthe_ctx *ctx, const uint32_t *x, size_t count,
+                                        const int64_t *seg_ptr, const int64_t *idx, size_t nseg,
+                                        const uint32_t *enc_zero, uint32_t *out);
 
 /* Segmented inclusive scan: out[t] = prod of x[seg_start(t) .. t] mod n^2 --
  * the inclusive_scan_by_key of the histogram over (node, feature)

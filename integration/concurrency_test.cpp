@@ -21,11 +21,11 @@ int main(int argc, char **argv) {
     Paillier_HIP server;
     server.keygen(bits);
     const std::string mode = argc > 4 ? argv[4] : "default";
-    if (mode == "exact") server.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;
+    if (mode == "exact") server.enc_mode = Paillier_HIP::EncMode::FixedBaseExact;
     if (mode == "public_exact") server.publish_bases();  // the party encrypts from the published bases
     Paillier_HIP party;
     party = server;                                   // public part, shared by the party threads
-    if (mode == "public_exact") party.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;
+    if (mode == "public_exact") party.enc_mode = Paillier_HIP::EncMode::FixedBaseExact;
     std::atomic<int> bad{0}, done{0};
     std::vector<std::thread> th;
     for (int t = 0; t < T; t++)

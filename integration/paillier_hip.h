@@ -30,42 +30,11 @@
 #include <vector>
 
 #include "fthe.h"
+#include "fthe_ghpair_key.h"
 #include "FedTree/syncarray.h"
 #include "FedTree/common.h"
-#include "FedTree/Encryption/paillier_gmp.h"
 
 namespace fthe_shim {
-// Engine status codes become exceptions.  The reference aborts on engine errors (CUDA_CHECK ->
-// CHECK_EQ, exit(1); common.h:47-52, paillier_gpu.cu:13-16): uncaught, an exception does the same
-// (std::terminate), and a caller that wants to recover can catch it.  Define FTHE_SHIM_ABORT to
-// print and abort() instead, as LOG(FATAL) would.
-inline void check(int st, const char *what) {
-    if (st == FTHE_OK) return;
-#ifdef FTHE_SHIM_ABORT
-    std::fprintf(stderr, "fthe: %s: %s\n", what, fthe_strerror(st));
-    std::abort();
-#else
-    throw std::runtime_error(std::string(what) + ": " + fthe_strerror(st));
-#endif
-}
-// One engine context per host thread (the boundary is entered from OpenMP
-// regions, FLtrainer.cpp:275-306); device from FTHE_DEVICE (default 0).
-inline fthe_ctx *thread_ctx() {
-    static thread_local fthe_ctx *c = nullptr;
-    if (!c) {
-        const char *d = std::getenv("FTHE_DEVICE");
-        check(fthe_ctx_create(d ? std::atoi(d) : 0, &c), "fthe_ctx_create");
-    }
-    return c;
-}
-// mpz <-> little-endian u32 words (paillier_gpu.cu:7,18 order)
-inline void to_words(const mpz_t x, uint32_t *w, int nw) {
-    size_t cnt = 0;
-    for (int i = 0; i < nw; i++) w[i] = 0;
-    if (mpz_sizeinbase(x, 2) > (size_t)nw * 32) throw std::runtime_error("operand does not fit");
-    mpz_export(w, &cnt, -1, 4, 0, 0, x);
-}
-inline void from_words(mpz_t x, const uint32_t *w, int nw) { mpz_import(x, (size_t)nw, -1, 4, 0, 0, w); }
 // The per-element mpz marshalling of a large batch on several host threads (a few hundred ns
 // per ciphertext; at the engine's rates it would otherwise dominate a batch call).  Small batches
 // stay on the calling thread, which may itself be one of FedTree's OpenMP workers.
@@ -93,21 +62,39 @@ inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 
 
 class Paillier_HIP {
 public:
-    // Encryption mode of encrypt(): FTHE_ENC_DEFAULT (per-ciphertext exponentiation) or
-    // FTHE_ENC_FIXED_BASE_EXACT (precomputed generator tables, the same ciphertext
-    // distribution, ~4x the rate on the key holder; include/fthe.h).  Not in the reference.
-    int enc_flags = FTHE_ENC_DEFAULT;
-    // Key generation flags of keygen(): 0 (the reference's unconstrained random primes) or
-    // FTHE_KEYGEN_KNOWN_ORDER (p - 1, q - 1 factored: one generator per prime in the exact
-    // fixed-base mode, ~2.6x faster again).  Not in the reference.
-    int keygen_flags = 0;
+    // Encryption mode of encrypt().  The modes give the reference's ciphertext distribution
+    // (paillier.cpp:127-137: r uniform in Z_n^*); the build must opt in (FTHE_ENABLE_NONREFERENCE_MODES)
+    // before a mode that does not can even be named.
+    enum class EncMode {
+        Default,              // one exponentiation per ciphertext
+        FixedBaseExact,       // precomputed generator tables, the same distribution, ~4x the rate on the key
+                              // holder; parties with published bases (publish_bases) ~5.6x (include/fthe.h)
+#ifdef FTHE_ENABLE_NONREFERENCE_MODES
+        FixedBaseSubgroup,    // r = h^alpha for one h per key: NOT the reference's distribution (r^n ranges
+                              // over a subgroup of the n-th residues; FTHE_ENC_FIXED_BASE)
+#endif
+    };
+    EncMode enc_mode = EncMode::Default;
+    // Key generation of keygen().
+    enum class KeygenMode {
+        Reference,            // unconstrained random primes of keyLength / 2 bits (paillier.cpp:43-62)
+#ifdef FTHE_ENABLE_NONREFERENCE_MODES
+        KnownOrder,           // p - 1, q - 1 factored (FTHE_KEYGEN_KNOWN_ORDER): NOT the reference's prime
+                              // distribution; one generator per prime in FixedBaseExact (~2.6x faster again)
+#endif
+    };
+    KeygenMode keygen_mode = KeygenMode::Reference;
     // decrypt() with plaintexts known to be < p -- every GHPair codec value and any sum of fewer
     // than 2^900 of them at P-2048 -- takes the p half of the CRT only (fthe_decrypt_short,
     // ~2x the decrypts/s, the same low 64 bits).  Not in the reference; off by default.
     bool dec_short = false;
-    Paillier_HIP() : key_length(2048) {}
+    // key_length = bits of n (the NTL meaning).  The default is the reference GPU build's
+    // key: Paillier_GPU::keygen() is paillier_cpu.keyGen(BITS = 1024), GMP semantics, a 512-bit n
+    // (paillier_gpu.cu:119-121, paillier_gpu.h:13), which is what homo_init's USE_CUDA branch
+    // (server.h:58-60) gets when it calls keygen() unchanged.  keygen(keylength) honours
+    // FLParam.key_length instead.
+    Paillier_HIP() : key_length(512) {}
     Paillier_HIP(const Paillier_HIP &o) : key_length(o.key_length) { copy_public(o); }
-    ~Paillier_HIP() { if (key_) fthe_key_destroy(key_); }
 
     // Paillier_GPU::operator= (paillier_gpu.h:32-37): public part, re-uploaded.
     Paillier_HIP &operator=(const Paillier_HIP &source) {
@@ -117,48 +104,54 @@ public:
 
     // Key holder: publish checked fixed-base bases with the public key (fthe_key_public_bases).
     // Parties that receive this key by operator= build their tables from them, and their
-    // encrypt() with enc_flags = FTHE_ENC_FIXED_BASE_EXACT (Party::encrypt_histogram) then draws
-    // r^n from the tables (~5.6x the per-ciphertext rate at P-2048).  Not in the reference.
+    // encrypt() with enc_mode = FixedBaseExact (Party::encrypt_histogram) then draws r^n from the
+    // tables (within 3 * 2^-64 of the reference's distribution).  Not in the reference.
     void publish_bases() {
         int nb = 0;
-        fthe_shim::check(fthe_key_public_bases(key_, 0, nullptr, &nb, nullptr), "public_bases");
-        bases_.assign((size_t)nb * 2 * fthe_key_n_words(key_), 0);
+        fthe_shim::check(fthe_key_public_bases(key(), 0, nullptr, &nb, nullptr), "public_bases");
+        bases_.assign((size_t)nb * 2 * fthe_key_n_words(key()), 0);
         base_bits_.assign(nb, 0);
-        fthe_shim::check(fthe_key_public_bases(key_, 0, bases_.data(), &nb, base_bits_.data()), "public_bases");
+        fthe_shim::check(fthe_key_public_bases(key(), 0, bases_.data(), &nb, base_bits_.data()), "public_bases");
         nbases_ = nb;
     }
 
-    // Paillier_GPU::keygen (paillier_gpu.cu:119-121); key_length = bits of n.
+    // Paillier_GPU::keygen (paillier_gpu.cu:119-121) with this object's key_length (bits of n).
     void keygen() { keygen((int)key_length); }
     void keygen(int keyLength) {
         key_length = (uint32_t)keyLength;
-        if (key_) fthe_key_destroy(key_);
-        key_ = nullptr;
-        bases_.clear();
-        base_bits_.clear();
-        nbases_ = 0;
-        fthe_shim::check(fthe_key_generate_ex(fthe_shim::thread_ctx(), keyLength, 0, keygen_flags, &key_), "keygen");
-        export_cpu();
+        reset_bases();
+        fthe_key *k = nullptr;
+        fthe_shim::check(fthe_key_generate_ex(fthe_shim::thread_ctx(), keyLength, 0, keygen_flags(), &k), "keygen");
+        adopt(fthe_key_adopt(k));
     }
-    void parameters_cpu_to_gpu() {      // keys live on the device from creation
-        if (!key_ && mpz_sgn(paillier_cpu.n)) {
-            std::vector<uint32_t> w(words(paillier_cpu.n));
-            fthe_shim::to_words(paillier_cpu.n, w.data(), (int)w.size());
-            fthe_shim::check(fthe_key_from_n(fthe_shim::thread_ctx(), w.data(), (int)w.size(), &key_), "key_from_n");
-        }
+    // Injected primes (the key of a reference run, test fixtures): fthe_key_from_primes.
+    void key_from_primes(const mpz_t p, const mpz_t q) {
+        const int w = (int)std::max(fthe_shim::words_of(p), fthe_shim::words_of(q));
+        std::vector<uint32_t> pw(w), qw(w);
+        fthe_shim::to_words(p, pw.data(), w);
+        fthe_shim::to_words(q, qw.data(), w);
+        reset_bases();
+        fthe_key *k = nullptr;
+        fthe_shim::check(fthe_key_from_primes(fthe_shim::thread_ctx(), pw.data(), qw.data(), w, &k), "key_from_primes");
+        adopt(fthe_key_adopt(k));
+        key_length = (uint32_t)mpz_sizeinbase(paillier_cpu.n, 2);
+        paillier_cpu.key_length = key_length;
     }
+    // Paillier_GPU::parameters_cpu_to_gpu (paillier_gpu.cu:77-117): engine keys live on the device from
+    // creation (keygen, key_from_primes, operator=), so there is nothing left to upload.
+    void parameters_cpu_to_gpu() {}
 
     // Paillier_GPU::encrypt(SyncArray<GHPair>&) (paillier_gpu.cu:211-313)
     void encrypt(SyncArray<GHPair> &message) {
         auto *d = message.host_data();
         size_t n = message.size();
-        int nw = fthe_key_n_words(key_), cw = 2 * nw;
+        int nw = fthe_key_n_words(key()), cw = 2 * nw;
         std::vector<uint64_t> m(2 * n);
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
         });
         std::vector<uint32_t> c(2 * n * (size_t)cw);
-        fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
+        fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
                                           eff_flags()), "encrypt");
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) {
@@ -172,7 +165,7 @@ public:
     void decrypt(SyncArray<GHPair> &message) {
         auto *d = message.host_data();
         size_t n = message.size();
-        int nw = fthe_key_n_words(key_), cw = 2 * nw;
+        int nw = fthe_key_n_words(key()), cw = 2 * nw;
         std::vector<uint32_t> c(2 * n * (size_t)cw, 0);
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {      // to_words throws only on oversize input
             for (size_t i = b; i < e; i++) {
@@ -182,8 +175,8 @@ public:
             }
         });
         std::vector<uint64_t> m(2 * n);
-        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key_, fthe_shim::thread_ctx(), c.data(), 2 * n,
-                                                                         m.data(), nullptr), "decrypt");
+        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key(), fthe_shim::thread_ctx(), c.data(),
+                                                                         2 * n, m.data(), nullptr), "decrypt");
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++)
                 if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }
@@ -193,45 +186,23 @@ public:
     // Paillier_GPU::decrypt(GHPair&) (paillier_gpu.cu:497-542)
     void decrypt(GHPair &message) {
         if (!message.encrypted) return;
-        int cw = 2 * fthe_key_n_words(key_);
+        int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> c(2 * (size_t)cw);
         fthe_shim::to_words(message.g_enc, &c[0], cw);
         fthe_shim::to_words(message.h_enc, &c[cw], cw);
         uint64_t m[2];
         // Server::decrypt_gh runs this per tree node from OpenMP threads (FLtrainer.cpp:758-764):
         // the key's coalescing queue merges the concurrent pairs into one launch
-        fthe_shim::check(fthe_decrypt_shared(key_, c.data(), 2, m, nullptr, dec_short ? 1 : 0), "decrypt");
+        fthe_shim::check(fthe_decrypt_shared(key(), c.data(), 2, m, nullptr, dec_short ? 1 : 0), "decrypt");
         message.g = fthe_shim::decode(m[0]);
         message.h = fthe_shim::decode(m[1]);
     }
 
-    // Paillier_GPU::add / mul (paillier_gpu.cu:58-68): single values.  Batch
-    // callers should use fthe_add / fthe_reduce_kway directly.
-    void add(mpz_t &result, mpz_t &x, mpz_t &y) {
-        int cw = 2 * fthe_key_n_words(key_);
-        std::vector<uint32_t> a(cw), b(cw), o(cw);
-        fthe_shim::to_words(x, a.data(), cw);
-        fthe_shim::to_words(y, b.data(), cw);
-        fthe_shim::check(fthe_add(key_, fthe_shim::thread_ctx(), a.data(), b.data(), 1, o.data()), "add");
-        fthe_shim::from_words(result, o.data(), cw);
-    }
-    void mul(mpz_t result, mpz_t &x, mpz_t &y) {
-        int cw = 2 * fthe_key_n_words(key_);
-        std::vector<uint32_t> a(cw), o(cw);
-        fthe_shim::to_words(x, a.data(), cw);
-        if (mpz_sgn(y) < 0) throw std::runtime_error("mul: negative exponent");
-        if (mpz_sizeinbase(y, 2) <= 64) {
-            uint64_t k = 0;
-            mpz_export(&k, nullptr, -1, 8, 0, 0, y);
-            fthe_shim::check(fthe_scalar_mul_u64(key_, fthe_shim::thread_ctx(), a.data(), k, 1, o.data()), "mul");
-        } else {                                        // any exponent (Paillier::mul(x, ZZ y))
-            std::vector<uint32_t> e(words(y));
-            fthe_shim::to_words(y, e.data(), (int)e.size());
-            fthe_shim::check(fthe_scalar_mul_words(key_, fthe_shim::thread_ctx(), a.data(), e.data(), (int)e.size(), 1,
-                                                   o.data()), "mul");
-        }
-        fthe_shim::from_words(result, o.data(), cw);
-    }
+    // Paillier_GPU::add / mul (paillier_gpu.cu:58-68): single values, alias-safe, through the key's
+    // shared queue (the GHPair key, paillier_cpu, is the same engine key).  Batch callers should use
+    // the helpers below or fthe_add / fthe_reduce_kway directly.
+    void add(mpz_t &result, mpz_t &x, mpz_t &y) { paillier_cpu.add(result, x, y); }
+    void mul(mpz_t result, mpz_t &x, mpz_t &y) { paillier_cpu.mul(*reinterpret_cast<mpz_t *>(result), x, y); }
 
     // ---- batch helpers for FedTree's HE call sites (not Paillier_GPU members) ----
     // Each replaces a loop of per-pair GHPair operators (CPU GMP, ~11.5 us per add) with one engine call.
@@ -242,9 +213,10 @@ public:
     // missing value, skipped), in instance order: one segmented product over g and h
     // (fthe_reduce_segments).  hist holds cut_col_ptr[n_col] entries; bins without instances are left
     // untouched (unencrypted zero, like the reference's).  A populated bin is the product of its members;
-    // the reference's first += also folds in a fresh Enc(0) (Q10): same plaintext, other randomness.
+    // zero_first also folds a fresh Enc(0) into every populated bin, the reference's exact sequence (its
+    // first += promotes the unencrypted zero accumulator, common.h:156-160).
     void histogram(SyncArray<GHPair> &gh, const unsigned char *dense_bin_id, const int *cut_col_ptr, int n_col,
-                   int max_num_bin, SyncArray<GHPair> &hist) {
+                   int max_num_bin, SyncArray<GHPair> &hist, bool zero_first = false) {
         const size_t n = gh.size(), nb = (size_t)cut_col_ptr[n_col];
         if (hist.size() < nb) throw std::runtime_error("histogram: hist smaller than cut_col_ptr[n_col]");
         std::vector<int64_t> ptr(2 * nb + 1, 0);                 // CSR: g segments, then h segments
@@ -263,10 +235,26 @@ public:
             }
         for (size_t s = 0; s < nb; s++) ptr[nb + s + 1] = tot + ptr[s + 1];    // h rows are n .. 2n-1
         for (int64_t t = 0; t < tot; t++) idx[tot + t] = idx[t] + (int64_t)n;
-        const int cw = 2 * fthe_key_n_words(key_);
+        const int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> x = rows(gh), out(2 * nb * (size_t)cw);
-        fthe_shim::check(fthe_reduce_segments(key_, fthe_shim::thread_ctx(), x.data(), 2 * n, ptr.data(), idx.data(),
+        fthe_shim::check(fthe_reduce_segments(key(), fthe_shim::thread_ctx(), x.data(), 2 * n, ptr.data(), idx.data(),
                                               2 * nb, out.data()), "histogram");
+        if (zero_first) {                                        // Enc(0) * prod, populated bins only
+            std::vector<size_t> pop;
+            for (size_t s = 0; s < nb; s++) if (ptr[s + 1] > ptr[s]) pop.push_back(s);
+            const size_t np = pop.size();
+            std::vector<uint64_t> zero(2 * np, 0);
+            std::vector<uint32_t> ez(2 * np * (size_t)cw), a(2 * np * (size_t)cw);
+            fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), zero.data(), 2 * np, nullptr, 0, 0,
+                                              ez.data(), eff_flags()), "histogram");
+            for (size_t j = 0; j < np; j++)
+                for (int pl = 0; pl < 2; pl++)
+                    std::copy(&out[(pl * nb + pop[j]) * cw], &out[(pl * nb + pop[j] + 1) * cw], &a[(pl * np + j) * cw]);
+            fthe_shim::check(fthe_add(key(), fthe_shim::thread_ctx(), a.data(), ez.data(), 2 * np, a.data()), "histogram");
+            for (size_t j = 0; j < np; j++)
+                for (int pl = 0; pl < 2; pl++)
+                    std::copy(&a[(pl * np + j) * cw], &a[(pl * np + j + 1) * cw], &out[(pl * nb + pop[j]) * cw]);
+        }
         auto *hd = hist.host_data();
         fthe_shim::parallel_for(nb, [&](size_t b, size_t e) {
             for (size_t s = b; s < e; s++)
@@ -283,18 +271,18 @@ public:
         if (k > 64 || parties.empty()) throw std::runtime_error("merge: 1 to 63 parties per call");
         for (auto *pt : parties)
             if (pt->size() != nb) throw std::runtime_error("merge: histogram sizes differ");
-        const int cw = 2 * fthe_key_n_words(key_);
+        const int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> x(k * 2 * nb * (size_t)cw), o(2 * nb * (size_t)cw);
         if (zero_first) {
             std::vector<uint64_t> zero(2 * nb, 0);
-            fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), zero.data(), 2 * nb, nullptr, 0, 0,
+            fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), zero.data(), 2 * nb, nullptr, 0, 0,
                                               x.data(), eff_flags()), "merge");
         }
         for (size_t j = z; j < k; j++) {
             std::vector<uint32_t> r = rows(*parties[j - z]);
             std::copy(r.begin(), r.end(), x.begin() + j * 2 * nb * (size_t)cw);
         }
-        fthe_shim::check(fthe_reduce_kway(key_, fthe_shim::thread_ctx(), x.data(), (int)k, 2 * nb, o.data()), "merge");
+        fthe_shim::check(fthe_reduce_kway(key(), fthe_shim::thread_ctx(), x.data(), (int)k, 2 * nb, o.data()), "merge");
         auto *d = out.host_data();
         fthe_shim::parallel_for(nb, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) set_enc(d[i], &o[i * cw], &o[(nb + i) * cw], cw);
@@ -307,12 +295,12 @@ public:
     void prefix(SyncArray<GHPair> &hist, const int *cut_col_ptr, int n_col) {
         const size_t nb = (size_t)cut_col_ptr[n_col];
         if (hist.size() < nb) throw std::runtime_error("prefix: hist smaller than cut_col_ptr[n_col]");
-        const int cw = 2 * fthe_key_n_words(key_);
+        const int cw = 2 * fthe_key_n_words(key());
         std::vector<int64_t> seg(2 * (size_t)n_col + 1);
         for (int f = 0; f <= n_col; f++) seg[f] = cut_col_ptr[f];
         for (int f = 1; f <= n_col; f++) seg[n_col + f] = (int64_t)nb + cut_col_ptr[f];
         std::vector<uint32_t> x = rows_n(hist, nb), o(2 * nb * (size_t)cw);
-        fthe_shim::check(fthe_scan_segments(key_, fthe_shim::thread_ctx(), x.data(), seg.data(), 2 * (size_t)n_col,
+        fthe_shim::check(fthe_scan_segments(key(), fthe_shim::thread_ctx(), x.data(), seg.data(), 2 * (size_t)n_col,
                                             o.data()), "prefix");
         auto *d = hist.host_data();
         fthe_shim::parallel_for(nb, [&](size_t lo, size_t hi) {
@@ -325,9 +313,9 @@ public:
     void subtract(SyncArray<GHPair> &a, SyncArray<GHPair> &b, SyncArray<GHPair> &out) {
         const size_t n = a.size();
         if (b.size() != n || out.size() != n) throw std::runtime_error("subtract: sizes differ");
-        const int cw = 2 * fthe_key_n_words(key_);
+        const int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> xa = rows(a), xb = rows(b), o(2 * n * (size_t)cw);
-        fthe_shim::check(fthe_sub(key_, fthe_shim::thread_ctx(), xa.data(), xb.data(), 2 * n, o.data()), "subtract");
+        fthe_shim::check(fthe_sub(key(), fthe_shim::thread_ctx(), xa.data(), xb.data(), 2 * n, o.data()), "subtract");
         auto *d = out.host_data();
         fthe_shim::parallel_for(n, [&](size_t lo, size_t hi) {
             for (size_t i = lo; i < hi; i++) set_enc(d[i], &o[i * cw], &o[(n + i) * cw], cw);
@@ -335,19 +323,40 @@ public:
     }
 
     uint32_t key_length;
-    Paillier_GMP paillier_cpu;          // host copy the GHPair operators use (common.h:72)
-    fthe_key *key() const { return key_; }
+    // The GHPair key (common.h:72; server.h:119 and party.h:124 assign it to every encrypted GHPair):
+    // the public part of this object's engine key, whose add / mul / encrypt run on the engine.
+    Paillier_HIP_Pub paillier_cpu;
+    fthe_key *key() const {
+        if (!key_) throw std::runtime_error("Paillier_HIP: no key (keygen() first)");
+        return key_.get();
+    }
 
 private:
-    fthe_key *key_ = nullptr;
+    fthe_key_ref key_;
     std::vector<uint32_t> bases_;          // published fixed-base bases (nbases_ x 2 n_words words)
     std::vector<int> base_bits_;           // and the bits of each base's exponent
     int nbases_ = 0;
-    static size_t words(const mpz_t x) { return (mpz_sizeinbase(x, 2) + 31) / 32; }
+    int keygen_flags() const {
+#ifdef FTHE_ENABLE_NONREFERENCE_MODES
+        if (keygen_mode == KeygenMode::KnownOrder) return FTHE_KEYGEN_KNOWN_ORDER;
+#endif
+        return 0;
+    }
     int eff_flags() const {             // exact fixed-base: p, q (key holder) or published bases (party)
-        int flags = enc_flags;
-        if (!fthe_key_has_private(key_) && !nbases_) flags &= ~FTHE_ENC_FIXED_BASE_EXACT;
-        return flags;
+        switch (enc_mode) {
+            case EncMode::Default: return FTHE_ENC_DEFAULT;
+            case EncMode::FixedBaseExact:
+                return (fthe_key_has_private(key()) || nbases_) ? FTHE_ENC_FIXED_BASE_EXACT : FTHE_ENC_DEFAULT;
+#ifdef FTHE_ENABLE_NONREFERENCE_MODES
+            case EncMode::FixedBaseSubgroup: return FTHE_ENC_FIXED_BASE;
+#endif
+        }
+        return FTHE_ENC_DEFAULT;
+    }
+    void reset_bases() { bases_.clear(); base_bits_.clear(); nbases_ = 0; }
+    void adopt(const fthe_key_ref &k) {
+        key_ = k;
+        paillier_cpu.bind(k, key_length);
     }
     void set_enc(GHPair &p, const uint32_t *g, const uint32_t *h, int cw) const {
         fthe_shim::from_words(p.g_enc, g, cw);
@@ -361,7 +370,7 @@ private:
     std::vector<uint32_t> rows(SyncArray<GHPair> &a) { return rows_n(a, a.size()); }
     std::vector<uint32_t> rows_n(SyncArray<GHPair> &a, size_t n) {       // the first n entries
         auto *d = a.host_data();
-        const int cw = 2 * fthe_key_n_words(key_);
+        const int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> x(2 * n * (size_t)cw, 0);
         std::vector<size_t> plain;
         for (size_t i = 0; i < n; i++)
@@ -374,7 +383,7 @@ private:
                 m[np + j] = fthe_shim::encode(d[plain[j]].h);
             }
             std::vector<uint32_t> c(2 * np * (size_t)cw);
-            fthe_shim::check(fthe_encrypt_u64(key_, fthe_shim::thread_ctx(), m.data(), 2 * np, nullptr, 0, 0, c.data(),
+            fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m.data(), 2 * np, nullptr, 0, 0, c.data(),
                                               eff_flags()), "encrypt");
             for (size_t j = 0; j < np; j++) {
                 std::copy(&c[j * cw], &c[(j + 1) * cw], &x[plain[j] * cw]);
@@ -390,31 +399,24 @@ private:
         });
         return x;
     }
+    // operator= / copy: a public-only engine key of the source's n (Paillier_GPU::operator= keeps the
+    // public part of paillier_cpu and re-uploads it, paillier_gpu.h:32-37) and the published bases.
     void copy_public(const Paillier_HIP &o) {
-        if (key_) fthe_key_destroy(key_);
-        key_ = nullptr;
-        paillier_cpu = o.paillier_cpu;                                    // public part only
-        parameters_cpu_to_gpu();
+        reset_bases();
+        key_.reset();
+        paillier_cpu = Paillier_HIP_Pub();
+        if (!o.key_) return;
+        const int nw = fthe_key_n_words(o.key_.get());
+        std::vector<uint32_t> w(nw);
+        fthe_shim::to_words(o.paillier_cpu.n, w.data(), nw);
+        fthe_key *k = nullptr;
+        fthe_shim::check(fthe_key_from_n(fthe_shim::thread_ctx(), w.data(), nw, &k), "key_from_n");
+        adopt(fthe_key_adopt(k));
         bases_ = o.bases_;                                                // published with n (publish_bases)
         base_bits_ = o.base_bits_;
         nbases_ = o.nbases_;
         if (nbases_)
-            fthe_shim::check(fthe_key_set_public_bases(key_, fthe_shim::thread_ctx(), bases_.data(), nbases_,
+            fthe_shim::check(fthe_key_set_public_bases(key(), fthe_shim::thread_ctx(), bases_.data(), nbases_,
                                                        base_bits_.data()), "set_public_bases");
-    }
-    void export_cpu() {
-        int nw = fthe_key_n_words(key_), hw = (nw + 1) / 2;
-        std::vector<uint32_t> n(nw), lam(nw), mu(nw), p(hw), q(hw);
-        fthe_shim::check(fthe_key_export(key_, n.data(), lam.data(), mu.data(), p.data(), q.data()), "export");
-        fthe_shim::from_words(paillier_cpu.n, n.data(), nw);
-        mpz_mul(paillier_cpu.n_square, paillier_cpu.n, paillier_cpu.n);
-        mpz_add_ui(paillier_cpu.generator, paillier_cpu.n, 1);
-        fthe_shim::from_words(paillier_cpu.lambda, lam.data(), nw);
-        fthe_shim::from_words(paillier_cpu.mu, mu.data(), nw);
-        fthe_shim::from_words(paillier_cpu.p, p.data(), hw);
-        fthe_shim::from_words(paillier_cpu.q, q.data(), hw);
-        mpz_sub_ui(paillier_cpu.p, paillier_cpu.p, 1);                   // the GMP build keeps p-1, q-1 (Q5)
-        mpz_sub_ui(paillier_cpu.q, paillier_cpu.q, 1);
-        paillier_cpu.key_length = key_length;
     }
 };

@@ -9,14 +9,16 @@
 int main(int argc, char **argv) {
     int bits = argc > 1 ? std::atoi(argv[1]) : 1024;
     Paillier_HIP server;                 // Server::paillier
-    if (argc > 2 && std::string(argv[2]) == "exact_known_order") server.keygen_flags = FTHE_KEYGEN_KNOWN_ORDER;
+#ifdef FTHE_ENABLE_NONREFERENCE_MODES
+    if (argc > 2 && std::string(argv[2]) == "exact_known_order") server.keygen_mode = Paillier_HIP::KeygenMode::KnownOrder;
+#endif
     server.keygen(bits);                 // homo_init (NTL semantics: n of `bits` bits)
     const std::string mode = argc > 2 ? argv[2] : "default";
     if (mode == "public_exact") server.publish_bases();          // bases travel with the public key
     Paillier_HIP party;                  // Party::paillier
     party = server;                      // Server::send_key: public part only
     if (mode.rfind("exact", 0) == 0 || mode == "public_exact")  // table-driven randomizer; the party (no p, q)
-        server.enc_flags = party.enc_flags = FTHE_ENC_FIXED_BASE_EXACT;   // uses published bases, else the default
+        server.enc_mode = party.enc_mode = Paillier_HIP::EncMode::FixedBaseExact;   // published bases, else default
     const float g[5] = {0.4f, 1.2f, 0.1f, 0.8f, -0.7f}, h[5] = {0.6f, 1.4f, 0.2f, 1.0f, 0.8f};
     SyncArray<GHPair> gh(5), hist(5);
     for (int i = 0; i < 5; i++) { gh.host_data()[i] = GHPair(g[i], h[i]); hist.host_data()[i] = GHPair(g[i], h[i]); }
@@ -71,6 +73,11 @@ int main(int argc, char **argv) {
         for (int i = 0; i < n; i++) ggh.host_data()[i].encrypted = true;
         SyncArray<GHPair> h1(7), merged(7), sib(7);
         party.histogram(ggh, bins.data(), cut, n_col, missing, h1);   // party side, public key
+        SyncArray<GHPair> hz(7);
+        party.histogram(ggh, bins.data(), cut, n_col, missing, hz, true);   // Enc(0) first (Q10)
+        server.decrypt(hz);
+        for (int s = 0; s < 7; s++)
+            if (std::fabs(hz.host_data()[s].g - want_g[s]) > 1e-5 || std::fabs(hz.host_data()[s].h - want_h[s]) > 1e-5) bad++;
         SyncArray<GHPair> h2(7), h3(7);
         for (int s = 0; s < 7; s++) { h2.host_data()[s] = h1.host_data()[s]; h3.host_data()[s] = h1.host_data()[s]; }
         h3.host_data()[6] = GHPair(0.5f, 0.25f);                        // an unencrypted operand is promoted

@@ -146,3 +146,37 @@ def test_shared_errors_do_not_block_other_callers(pl):
         else:
             assert status[i] == 0, (i, status[i])
             assert np.array_equal(pl.decrypt_u64(outs[i]), ms[i])
+
+
+def test_add_mul_shared_many_threads_alias_safe(pl):
+    """fthe_add_shared / fthe_scalar_mul_u64_shared (GHPair::operator+, +=, - of the USE_HIP build):
+    24 threads on one key, each accumulating in place (out aliases a, the call shape of
+    `paillier.add(g_enc, g_enc, rhs.g_enc)`, common.h:207-229) and subtracting with the all-ones
+    scalar; the results equal the golden reference adds and the batch engine's."""
+    gold = load_golden("ref_gmp_L2048.json")
+    import pyoracle
+    cw = 2 * pl.n_words
+    cts = pyoracle.ints_to_words([int(c["c"], 16) for c in gold["cases"]], cw)
+    adds = gold["adds"]
+    T = 24
+    res, bad = [None] * T, []
+
+    def work(i):
+        try:
+            a = adds[i % len(adds)]
+            acc = np.ascontiguousarray(cts[a["i"]][None].copy())
+            pl.add_shared(acc, cts[a["j"]][None], out=acc)           # in place: acc = acc * c_j
+            neg = pl.scalar_mul_shared(cts[a["j"]][None], 2**64 - 1)
+            back = pl.add_shared(acc, neg)                             # acc * c_j^-1 (low 64 bits)
+            res[i] = (acc.copy(), back)
+        except Exception as e:  # noqa: BLE001
+            bad.append((i, repr(e)))
+
+    _run_all(work, T)
+    assert not bad, bad
+    for i in range(T):
+        a = adds[i % len(adds)]
+        assert pyoracle.from_words(res[i][0][0]) == int(a["c"], 16), i
+        want_back = pl.add_batch(res[i][0], pl.scalar_mul(cts[a["j"]][None], 2**64 - 1))
+        assert np.array_equal(res[i][1], want_back), i
+        assert int(pl.decrypt_u64(res[i][1])[0]) == gold["cases"][a["i"]]["m"] % 2**64

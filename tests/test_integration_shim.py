@@ -1,36 +1,96 @@
-"""The FedTree drop-in class (integration/paillier_hip.h) compiles against
-FedTree-shaped types and links libfthe.so; on a GPU it runs the Server/Party
-HE call sequence (server.h:58-135, party.h:118-142)."""
+"""The FedTree drop-in (integration/paillier_hip.h, integration/fthe_ghpair_key.h) compiles against
+FedTree-shaped types and links libfthe.so; on a GPU it runs the Server/Party HE call sequence
+(server.h:58-135, party.h:118-142) and GHPair's operators (common.h:150-337) on the engine,
+bit-exact against the reference's golden vectors."""
 import os
+import re
 import subprocess
 
 import pytest
 
+import pyoracle
+from conftest import golden_key, load_golden
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INTEG = os.path.join(ROOT, "integration")
+REF_COMMON = "/root/reference/include/FedTree/common.h"
 
 
-def _build(out, src="shim_test.cpp", extra=()):
+def _build(out, src="shim_test.cpp", extra=(), check=True):
     cmd = ["g++", "-O2", "-std=c++17", "-pthread", *extra, "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
            "-I" + os.path.join(ROOT, "include"), "-idirafter", "/opt/conda/include",
            os.path.join(INTEG, src), "-o", out, "-L" + os.path.join(ROOT, "fedtree_amd"), "-lfthe",
            "-Wl,-rpath," + os.path.join(ROOT, "fedtree_amd"), "-l:libgmp.so.10"]
     r = subprocess.run(cmd, capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr
-    return out
+    if check:
+        assert r.returncode == 0, r.stderr
+    return r
+
+
+NONREF = ("-DFTHE_ENABLE_NONREFERENCE_MODES",)
 
 
 def test_shim_compiles_and_links(tmp_path):
-    exe = _build(str(tmp_path / "shim_test"))
-    assert os.path.exists(exe)
-    assert os.path.exists(_build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp"))
-    assert os.path.exists(_build(str(tmp_path / "shim_abort"), extra=("-DFTHE_SHIM_ABORT",)))
+    _build(str(tmp_path / "shim_test"))
+    _build(str(tmp_path / "shim_nonref"), extra=NONREF)
+    _build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp")
+    _build(str(tmp_path / "shim_abort"), extra=("-DFTHE_SHIM_ABORT",))
+    _build(str(tmp_path / "ghpair_test"), "ghpair_test.cpp", extra=("-DFTHE_REFERENCE_SHARED_R",))
+
+
+def test_nonreference_modes_need_the_build_opt_in(tmp_path):
+    """The subgroup randomizer (FTHE_ENC_FIXED_BASE) and known-order primes (FTHE_KEYGEN_KNOWN_ORDER)
+    are not the reference's distributions: without FTHE_ENABLE_NONREFERENCE_MODES the drop-in class
+    cannot even name them; the shared-r compat randomness needs FTHE_REFERENCE_SHARED_R."""
+    src = tmp_path / "nonref.cpp"
+    src.write_text('#include "paillier_hip.h"\nint main() { Paillier_HIP s;\n'
+                   '  s.enc_mode = Paillier_HIP::EncMode::FixedBaseSubgroup;\n'
+                   '  s.keygen_mode = Paillier_HIP::KeygenMode::KnownOrder; return 0; }\n')
+    shr = tmp_path / "sharedr.cpp"
+    shr.write_text('#include "paillier_hip.h"\nint main() { Paillier_HIP_Pub k; mpz_t r; mpz_init(r);\n'
+                   '  k.set_shared_r(r); return 0; }\n')
+
+    def build(path, extra):
+        cmd = ["g++", "-std=c++17", "-fsyntax-only", *extra, "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
+               "-I" + os.path.join(ROOT, "include"), "-idirafter", "/opt/conda/include", str(path)]
+        return subprocess.run(cmd, capture_output=True, text=True)
+
+    r = build(src, ())
+    assert r.returncode != 0 and "FixedBaseSubgroup" in r.stderr and "KnownOrder" in r.stderr
+    assert build(src, NONREF).returncode == 0
+    assert build(shr, ()).returncode != 0
+    assert build(shr, ("-DFTHE_REFERENCE_SHARED_R",)).returncode == 0
+
+
+def _key_calls(text):
+    """`paillier.add(...)` / `paillier.mul(...)` calls with three arguments (the mpz_t forms of the
+    USE_CUDA branches), whitespace removed, comments dropped."""
+    text = re.sub(r"//[^\n]*", "", text)
+    calls = re.findall(r"((?:rhs\.)?paillier\.(?:add|mul)\(([^;()]*)\));", text)
+    return sorted({re.sub(r"\s+", "", c) for c, args in calls if args.count(",") == 2})
+
+
+@pytest.mark.skipif(not os.path.exists(REF_COMMON), reason="reference sources absent (GPU box)")
+def test_mock_operators_make_the_reference_key_calls():
+    """Every key call in the reference's GHPair operator bodies (common.h:150-337, mpz_t branches)
+    appears in the shim's GHPair with the same receiver and arguments, so ghpair_test exercises the
+    reference's call sequence -- including the aliased add(g_enc, g_enc, ...) of operator+=."""
+    ref = open(REF_COMMON).read().splitlines()
+    ref_ops = "\n".join(ref[149:337])
+    mock = open(os.path.join(INTEG, "mock", "FedTree", "common.h")).read()
+    want = _key_calls(ref_ops)
+    assert len(want) >= 12, want
+    have = set(_key_calls(mock))
+    missing = [c for c in want if c not in have]
+    assert not missing, missing
+    assert "paillier.add(g_enc,g_enc,rhs.g_enc)" in want
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["default", "exact", "exact_known_order", "public_exact", "short", "helpers", "big"])
 def test_shim_runs_server_party_flow(tmp_path, mode):
-    exe = _build(str(tmp_path / "shim_test"))
+    exe = str(tmp_path / "shim_test")
+    _build(exe, extra=NONREF if mode == "exact_known_order" else ())
     r = subprocess.run([exe, "1024", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "shim OK" in r.stdout, r.stdout + r.stderr
 
@@ -39,6 +99,53 @@ def test_shim_runs_server_party_flow(tmp_path, mode):
 @pytest.mark.parametrize("mode", ["default", "exact", "public_exact"])
 def test_shim_concurrent_threads_share_one_key(tmp_path, mode):
     """16 host threads, one shared key, a context per thread (the OpenMP call pattern)."""
-    exe = _build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp")
+    exe = str(tmp_path / "concurrency_test")
+    _build(exe, "concurrency_test.cpp")
     r = subprocess.run([exe, "1024", "16", "24", mode], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "concurrency OK" in r.stdout, r.stdout + r.stderr
+
+
+def _hx(v):
+    """Plain lower-case hex (the golden files write 0x-prefixed strings)."""
+    return f"{int(v, 16) if isinstance(v, str) else int(v):x}"
+
+
+def _ghpair_fixture(path, name):
+    g = load_golden(name)
+    p, q = golden_key(g)
+    key = pyoracle.keygen_from_primes(p, q)
+    r = int(g["shared_r"], 16)
+    cts = [int(c["c"], 16) for c in g["cases"]]
+    tok = [f"{p:x}", f"{q:x}", f"{r:x}", str(len(cts))] + [f"{c:x}" for c in cts]
+    tok += [str(len(g["adds"]))]
+    for a in g["adds"]:
+        tok += [str(a["i"]), str(a["j"]), _hx(a["c"])]
+    h = g["hist"]
+    tok += [str(h["parties"]), str(h["bins"])]
+    for pi in range(h["parties"]):
+        tok += [_hx(v) for v in h["ct"][pi]]
+    tok += [_hx(v) for v in h["merged"]]
+    subs = [(12, 13), (0, 2), (3, 1), (5, 5)]
+    tok += [str(len(subs))]
+    for i, j in subs:
+        tok += [str(i), str(j), f"{pyoracle.sub(key, cts[i], cts[j]):x}"]
+    import numpy as np
+    gf, hf, j = np.float32(0.5), np.float32(-0.25), 7
+    mg, mh = (int(pyoracle.encode_fixed(np.array([v]))[0]) for v in (gf, hf))
+    tok += [repr(float(gf)), repr(float(hf)), str(j),
+            f"{pyoracle.add(key, pyoracle.encrypt(key, mg, r), pyoracle.mul(key, cts[j], 2**64 - 1)):x}",
+            f"{pyoracle.add(key, pyoracle.encrypt(key, mh, r), pyoracle.mul(key, cts[j], 2**64 - 1)):x}"]
+    path.write_text(" ".join(tok) + "\n")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_gmp_L1024.json", "ref_gmp_L4096.json"])
+def test_ghpair_operators_bit_exact_on_engine(tmp_path, name):
+    """dest = dest + src, dest += src (aliased), dest - src, add(s, s, c) and the 8-party merge from an
+    unencrypted zero (Q10) through the USE_HIP GHPair key: the reference's golden ciphertexts."""
+    fx = tmp_path / "fixture.txt"
+    _ghpair_fixture(fx, name)
+    exe = str(tmp_path / "ghpair_test")
+    _build(exe, "ghpair_test.cpp", extra=("-DFTHE_REFERENCE_SHARED_R",))
+    r = subprocess.run([exe, str(fx)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ghpair OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -1,0 +1,3 @@
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r02b_pytest_gpu.txt 2>&1 || exit 1
