@@ -82,7 +82,26 @@ struct MontMod {
         nprime = (uint32_t)mpz_get_ui(inv);
         ctx = to_limbs(N, S, B);
         ctx.push_back(nprime);
+        // MULWC (four-lane kernel): quotient-estimate constants, doubles -k1 = -2^32 invN,
+        // -k2 = -2^27 invN, -k3 = -2^59 invN and bias, invN <= 2^(B(S-2)) / N (rounded down).
+        // Meaningful when N >= 2^(B S - 10) (classical_ok); zeros otherwise.
+        double k[4] = {0, 0, 0, 0};
+        if (classical_ok()) {
+            Mpz t; mpz_fdiv_q_2exp(t, N, (mp_bitcnt_t)B * (S - 2) - 64);
+            const double ntop = mpz_get_d(t) * (1.0 + 0x1p-50) * 0x1p-64;     // >= N / 2^(B(S-2))
+            const double inv = 1.0 / ntop * (1.0 - 0x1p-50);
+            k[0] = -inv * 0x1p32; k[1] = -inv * 0x1p27; k[2] = -inv * 0x1p59; k[3] = 0x1p-6;   // negated: -q
+        }
+        for (double d : k) {
+            uint32_t w[2];
+            std::memcpy(w, &d, 8);
+            ctx.push_back(w[0]);
+            ctx.push_back(w[1]);
+        }
     }
+    // the classical MSB-first product (OP_MULWC, tools/msb_model.py) needs the estimate's
+    // ignored columns below 2^-8 of a quotient unit: N >= 2^(B S - 10)
+    bool classical_ok() const { return sh.lanes == 4 && mpz_sizeinbase(N, 2) >= (size_t)(B * S - 10); }
     std::vector<uint32_t> limbs(const mpz_t x) const { return to_limbs(x, S, B); }
     // x * R mod N (Montgomery form of x), as limbs
     std::vector<uint32_t> mont(const mpz_t x) const {
@@ -107,7 +126,12 @@ enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL
                      // four-lane: canonical 128-word rows
                      OP_LOADGD = 14, OP_MULGD = 15,
                      // the same with 16-bit windows (u16 digits, entry j*65536 + digit)
-                     OP_LOADGD16 = 16, OP_MULGD16 = 17 };
+                     OP_LOADGD16 = 16, OP_MULGD16 = 17,
+                     // four-lane kernel, row I/O: X <- row_t X mod N, classical MSB-first (no
+                     // Montgomery factor); X canonical, N >= 2^(B S - 10)
+                     OP_MULWC = 18,
+                     // the same with the gathered row of MULWG t; CANON: X (< 4N) -> X mod N
+                     OP_MULWGC = 19, OP_CANON = 20 };
 
 struct Prog {
     std::vector<uint32_t> w;
@@ -134,6 +158,9 @@ struct Prog {
         else { sqr(n); mul(s); }
     }
     void mulwg(int t) { op(OP_MULWG, t); montmuls += 1; }
+    void mulwc(int t) { op(OP_MULWC, t); montmuls += 1; }
+    void mulwgc(int t) { op(OP_MULWGC, t); montmuls += 1; }
+    void canon() { op(OP_CANON, 0); }
     void loadgd(int j) { op(OP_LOADGD, j); }
     void mulgd(int j) { op(OP_MULGD, j); montmuls += 1; }
     void loadgd16(int j) { op(OP_LOADGD16, j); }

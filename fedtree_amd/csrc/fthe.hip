@@ -601,8 +601,12 @@ static int key_finish(fthe_key *k) {
         // row-I/O forms: canonical rows read / written by the kernel itself (no layout kernels)
         k->rowio = k->sn2.lanes == 4 && 2 * k->n_words == 128 && !getenv("FTHE_NO_ROWIO");
         if (k->rowio) {
+            // fresh add: one classical product a b mod n^2 when the modulus allows it (n of 2048 bits),
+            // else a b R^-1 then the R^2 correction (two Montgomery products); FTHE_ADD_MONT=1: the latter
             Prog aw;
-            aw.loadw(0); aw.mulw(1); aw.mul(SL_C0); aw.storew(2); aw.end();
+            if (k->mn2.m.classical_ok() && !getenv("FTHE_ADD_MONT")) { aw.loadw(0); aw.canon(); aw.mulwc(1); aw.storew(2); }
+            else { aw.loadw(0); aw.mulw(1); aw.mul(SL_C0); aw.storew(2); }
+            aw.end();
             k->pr_add_w = k->add_prog(aw);
             Prog sw;
             sw.loadw(1); sw.mul(SL_C0); sw.pow_ones(64, SL_T0, SL_T1); sw.mulw(0); sw.storew(2); sw.end();
@@ -2607,7 +2611,7 @@ namespace {
 //   from Montgomery: kk = 1, K = 1          -> x R^-1
 //   Montgomery add: kk = 2, no constant     -> (aR)(bR)R^-1 = (ab)R
 static int rowprod_impl(fthe_key *k, fthe_ctx *c, const uint32_t *const *xs, int kk, size_t count, uint32_t *out,
-                        const mpz_t cst) {
+                        const mpz_t cst, bool classical = false) {
     if (!k || !c || kk <= 0 || kk > 64 || (!out && count)) return FTHE_ERR_ARG;
     for (int j = 0; j < kk; j++)
         if (!xs[j] && count) return FTHE_ERR_ARG;
@@ -2623,7 +2627,14 @@ static int rowprod_impl(fthe_key *k, fthe_ctx *c, const uint32_t *const *xs, int
     if (cst) rl = k->mn2.m.limbs(cst);
     else rl.assign(1, 0u);
     Prog p;
-    if (rowio) {
+    // plain products (k-way, cst = R^kk) with a 2048-bit n: classical products, no R^kk correction
+    classical = classical && rowio && kk >= 2 && k->mn2.m.classical_ok() && !getenv("FTHE_ADD_MONT");
+    if (classical) {
+        cst = nullptr;
+        p.loadw(0); p.canon();
+        for (int j = 1; j < kk; j++) p.mulwc(j);
+        p.storew(kk); p.end();
+    } else if (rowio) {
         p.loadw(0);
         for (int j = 1; j < kk; j++) p.mulw(j);
         if (cst) p.mul(SL_C0);
@@ -2668,7 +2679,7 @@ extern "C" int fthe_reduce_kway_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x,
     std::vector<const uint32_t *> xs(kk);
     for (int j = 0; j < kk; j++) xs[j] = x + (size_t)j * count * 2 * k->n_words;
     Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)kk, k->n2);
-    return rowprod_impl(k, c, xs.data(), kk, count, out, Rk);
+    return rowprod_impl(k, c, xs.data(), kk, count, out, Rk, true);
 }
 
 // Montgomery-resident rows: x R mod n^2 in the same 2 n_words-word row layout.  Products of
@@ -2707,7 +2718,11 @@ struct GatherProd {
         Mpz Rk; mpz_powm_ui(Rk, k->mn2.m.R, (unsigned long)K, k->n2);
         std::vector<uint32_t> rl = k->mn2.m.limbs(Rk);
         Prog p;
-        if (k->rowio) {               // rows[0] = source, rows[1..K] = index lists, rows[K+1] = output
+        if (k->rowio && k->mn2.m.classical_ok() && !getenv("FTHE_ADD_MONT")) {
+            p.loadwg(1); p.canon();       // classical products: no R^K correction
+            for (int j = 1; j < K; j++) p.mulwgc(1 + j);
+            p.storew(K + 1); p.end();
+        } else if (k->rowio) {        // rows[0] = source, rows[1..K] = index lists, rows[K+1] = output
             p.loadwg(1);
             for (int j = 1; j < K; j++) p.mulwg(1 + j);
             p.mul(SL_C0);
@@ -2877,7 +2892,7 @@ static int fold_zero_first(fthe_key *k, fthe_ctx *c, const int64_t *seg_dev, siz
                        enc_zero, seg_dev, nseg, cw, (uint32_t *)c->ezm.p);
     const uint32_t *xs[2] = {out, (const uint32_t *)c->ezm.p};
     Mpz R2; mpz_powm_ui(R2, k->mn2.m.R, 2ul, k->n2);
-    return rowprod_impl(k, c, xs, 2, nseg, out, R2);          // row-wise, alias-safe
+    return rowprod_impl(k, c, xs, 2, nseg, out, R2, true);    // row-wise, alias-safe
 }
 
 extern "C" int fthe_reduce_segments_csr_dev(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t count,

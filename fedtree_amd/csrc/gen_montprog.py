@@ -555,7 +555,12 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     NT = Q + U
     NVGPR = TB + 2 * NT
     assert NVGPR <= 256, NVGPR
-    NSGPR = 40
+    NSGPR = 48
+    # MULWC (classical MSB-first product, row I/O shape only): its ring of NTC pairs, the
+    # estimate's double temporaries and the -bias constant in the VGPRs past the ring
+    NTC = Q + 2
+    DF0, DACC, DBIAS = V_TMP, TB + 2 * NTC, TB + 2 * NTC + 2
+    assert DBIAS + 2 <= NVGPR, (DBIAS, NVGPR)
 
     # window position k -> register pair k mod NT (a ring in the ring form)
     def T(k):
@@ -600,6 +605,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_mov_b32 s23, 0x11111111')
     e('  s_waitcnt lgkmcnt(0)')
     e(f'  s_load_dword s12, s[8:9], {hex(4 * S)}')
+    # MULWC quotient-estimate constants (doubles k1, k2, k3, -bias at ctx[S+1 .. S+8])
+    e(f'  s_load_dwordx8 s[36:43], s[8:9], {hex(4 * (S + 1))}')
     # ROW = g*512 + k*128 = wg*32768 + tid*128 (g = wg*64 + tid>>2, k = tid & 3):
     # the lane's quarter of a 128-word row, and an encoding of (g, k) for the slot ops
     e('  s_lshl_b32 s14, s2, 15')
@@ -628,7 +635,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     ops = ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (5, '.Laddslot'), (6, '.Laddsmall'))
     if rowio:
         ops += ((7, '.Lloadw'), (8, '.Lmulw'), (9, '.Lstorew'), (10, '.Lloadwg'), (11, '.Lmulwg'),
-                (14, '.Lloadwd'), (15, '.Lmulwd'), (16, '.Lloadwd16'), (17, '.Lmulwd16'))
+                (14, '.Lloadwd'), (15, '.Lmulwd'), (16, '.Lloadwd16'), (17, '.Lmulwd16'), (18, '.Lmulwc'), (19, '.Lmulwgc'),
+                (20, '.Lcanon'))
     for code, lab in ops:
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
@@ -663,10 +671,12 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
                 step_addr()
         e('  s_waitcnt vmcnt(0)')
 
-    def ripple_quad():
+    def ripple_quad(signed=False):
         """X limbs + a pending 64-bit carry-out in tmp (of this lane) -> carries
         move to the next lane's limb 0 (DPP quad_perm [0,0,1,2]; lane 0 gets
-        none) and ripple until no lane has one (at most 3 passes)."""
+        none) and ripple until no lane has one (at most 3 passes).  signed: the
+        carries are two's-complement (MULWC's columns), shifted arithmetically."""
+        shr = 'v_ashrrev_i64' if signed else 'v_lshrrev_b64'
         lab = f'.Lrq{len(o)}'
         e(f'{lab}_loop:')
         e('  s_nop 1')
@@ -681,7 +691,7 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         for k in range(Q):
             e(f'  v_mad_u64_u32 {tmp}, vcc, {X(k)}, 1, {tmp}')
             e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
-            e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+            e(f'  {shr} {tmp}, {B}, {tmp}')
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 
@@ -693,6 +703,39 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
             e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
             e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
         ripple_quad()
+
+    def canon_once(tag):
+        """X (normalised, < 2N) -> X mod N: D = X - N across the quad (DPP borrow ripple), then
+        select; uses the T registers from TB (free outside a product) and V_AI / V_TMP."""
+        bo, fin, t1 = f"v{V_AI[0]}", f"v{V_AI[1]}", f"v{V_TMP}"
+        for j in range(Q):                         # D = X - N (this quarter), borrow-out bo in {0,-1}
+            e(f'  v_sub_u32_e32 v{D0 + j}, {X(j)}, {NV(j)}')
+            if j:
+                e(f'  v_add_u32_e32 v{D0 + j}, v{D0 + j}, {bo}')
+            e(f'  v_ashrrev_i32_e32 {bo}, 31, v{D0 + j}')
+            e(f'  v_and_b32_e32 v{D0 + j}, {hex(MASK)}, v{D0 + j}')
+        e(f'  v_mov_b32_e32 {fin}, 0')
+        lab = f'.L{tag}_borrow'
+        e(f'{lab}_loop:')
+        e(f'  v_cndmask_b32_e64 {t1}, 0, {bo}, s[20:21]')            # lane 3: borrow out of the number
+        e(f'  v_or_b32_e32 {fin}, {fin}, {t1}')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp {t1}, {bo} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 {bo}, {t1}, 0, s[22:23]')            # borrow into lane k from lane k-1
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, {bo}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        for j in range(Q):
+            e(f'  v_add_u32_e32 v{D0 + j}, v{D0 + j}, {bo}')
+            e(f'  v_ashrrev_i32_e32 {bo}, 31, v{D0 + j}')
+            e(f'  v_and_b32_e32 v{D0 + j}, {hex(MASK)}, v{D0 + j}')
+        e(f'  s_branch {lab}_loop')
+        e(f'{lab}_done:')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp {t1}, {fin} quad_perm:[3,3,3,3] {DPP}')
+        e(f'  v_cmp_eq_u32_e32 vcc, 0, {t1}')                      # no borrow: X >= N -> X - N
+        for j in range(Q):
+            e(f'  v_cndmask_b32_e32 {X(j)}, {X(j)}, v{D0 + j}, vcc')
 
     e('.Lloadx:')
     load_quarter(X)
@@ -887,6 +930,29 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_mov_b32 s19, 0')
     e('  s_branch .Lmontmul')
 
+    # MULWC t: X <- row_t * X mod N, classical (no Montgomery factor): the pairwise add of two
+    # canonical ciphertexts in one product.  Needs X < N (canonical) and N >= 2^(B S - 10).
+    e('.Lmulwc:')
+    row_ptr()
+    live_mask()
+    load_row_limbs(lambda j: f"v{A0 + j}")
+    restore_exec()
+    write_a(lambda j: f"v{A0 + j}")
+    e('  s_branch .Lmontmul_msb')
+
+    # MULWGC t: the same with the gathered row of MULWG t (idx list at rows[t], idx < 0 -> 1)
+    e('.Lmulwgc:')
+    load_gather_limbs(lambda j: f"v{A0 + j}")
+    restore_exec()
+    write_a(lambda j: f"v{A0 + j}")
+    e('  s_branch .Lmontmul_msb')
+
+    # CANON: X (normalised limbs, < 4N: any 4096-bit row) -> X mod N, the precondition of MULWC
+    e('.Lcanon:')
+    for r in range(3):
+        canon_once(f'cn{r}')
+    e('  s_branch .Lprog')
+
     for wide in (False, True):
         sfx = "16" if wide else ""
         e(f'.Lloadwd{sfx}:')
@@ -904,35 +970,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('.Lstorew:')
     row_ptr()
     live_mask()
-    bo, fin, t1 = f"v{V_AI[0]}", f"v{V_AI[1]}", f"v{V_TMP}"
-    for j in range(Q):                         # D = X - N (this quarter), borrow-out bo in {0,-1}
-        e(f'  v_sub_u32_e32 v{D0 + j}, {X(j)}, {NV(j)}')
-        if j:
-            e(f'  v_add_u32_e32 v{D0 + j}, v{D0 + j}, {bo}')
-        e(f'  v_ashrrev_i32_e32 {bo}, 31, v{D0 + j}')
-        e(f'  v_and_b32_e32 v{D0 + j}, {hex(MASK)}, v{D0 + j}')
-    e(f'  v_mov_b32_e32 {fin}, 0')
-    lab = '.Lsw_borrow'
-    e(f'{lab}_loop:')
-    e(f'  v_cndmask_b32_e64 {t1}, 0, {bo}, s[20:21]')            # lane 3: borrow out of the number
-    e(f'  v_or_b32_e32 {fin}, {fin}, {t1}')
-    e('  s_nop 1')
-    e(f'  v_mov_b32_dpp {t1}, {bo} quad_perm:[0,0,1,2] {DPP}')
-    e(f'  v_cndmask_b32_e64 {bo}, {t1}, 0, s[22:23]')            # borrow into lane k from lane k-1
-    e(f'  v_cmp_ne_u32_e32 vcc, 0, {bo}')
-    e('  s_nop 4')
-    e(f'  s_cbranch_vccz {lab}_done')
-    for j in range(Q):
-        e(f'  v_add_u32_e32 v{D0 + j}, v{D0 + j}, {bo}')
-        e(f'  v_ashrrev_i32_e32 {bo}, 31, v{D0 + j}')
-        e(f'  v_and_b32_e32 v{D0 + j}, {hex(MASK)}, v{D0 + j}')
-    e(f'  s_branch {lab}_loop')
-    e(f'{lab}_done:')
-    e('  s_nop 1')
-    e(f'  v_mov_b32_dpp {t1}, {fin} quad_perm:[3,3,3,3] {DPP}')
-    e(f'  v_cmp_eq_u32_e32 vcc, 0, {t1}')                      # no borrow: X >= N -> X - N
-    for j in range(Q):
-        e(f'  v_cndmask_b32_e32 {X(j)}, {X(j)}, v{D0 + j}, vcc')
+    canon_once('sw')
+    bo, t1 = f"v{V_AI[0]}", f"v{V_TMP}"
     # own bit stream -> words U_i (bits [32i, 32i+32) of this quarter)
     for i in range(32):
         lo, hi = 32 * i, 32 * i + 31
@@ -1011,6 +1050,135 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
         e(f'  v_cndmask_b32_e64 {Thi(u + Q)}, {Thi(u + Q)}, 0, s[20:21]')
         e('  s_waitcnt lgkmcnt(0)')
 
+    def emit_montmul_msb():
+        """X <- A X mod N, MSB first (tools/msb_model.py is the bit-exact model).  Window positions
+        0..S-1 of signed 64-bit columns + the top TT (position S), lane k owning [kQ, kQ+Q) and lane 3
+        also TT; offset o of a lane at step t lives in ring pair (o - t) mod NTC, so the shift up by
+        one position per step is a relabelling plus one 64-bit DPP hand-off per lane.  Per step
+        (i = S-1-t): hand off; + a_i X; fold W = TT 2^B + col[S-1]; q = trunc(W_hi k3 + W_lo k2 +
+        col[S-2]_hi k1 - bias) in double (lane 3, broadcast); - q N (v_mad_i64_i32).  Then the
+        columns are normalised with signed carries: X in [0, 2N), canonicalised by STOREW."""
+        def R(o, u):
+            k = (o - u) % NTC
+            return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
+
+        def Rlo(o, u):
+            return f"v{TB + 2 * ((o - u) % NTC)}"
+
+        def Rhi(o, u):
+            return f"v{TB + 2 * ((o - u) % NTC) + 1}"
+
+        STEPC = NTC
+        assert STEPC % 2 == 0
+        NTRIPC, TLC = S // STEPC, S % STEPC
+        q = f"v{V_Q}"
+        d0 = f"v[{DF0}:{DF0 + 1}]"
+        acc = f"v[{DACC}:{DACC + 1}]"
+        bias = f"v[{DBIAS}:{DBIAS + 1}]"
+        cur = [0]                       # V_LDSI - column base, in LDS rows
+
+        def move_cursor(to_row):
+            d = (to_row - cur[0]) * RB_
+            if d > 0:
+                e(f'  v_add_u32_e32 v{V_LDSI}, {hex(d)}, v{V_LDSI}')
+            elif d < 0:
+                e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(-d)}, v{V_LDSI}')
+            cur[0] = to_row
+
+        def step(u, i, prefetch):
+            """one MSB step at ring phase u reading a_i (already in V_AI[u % 2])"""
+            ai = f"v{V_AI[u % 2]}"
+            nai = f"v{V_AI[(u + 1) % 2]}"
+            # 1. shift: lane k's offset Q -> lane k+1's new offset 0; lane 0 gets 0; offset Q stays
+            #    only on lane 3 (TT), zero elsewhere
+            e(f'  v_mov_b32_dpp {Rlo(0, u)}, {Rlo(Q, u)} quad_perm:[3,0,1,2] {DPP}')
+            e(f'  v_mov_b32_dpp {Rhi(0, u)}, {Rhi(Q, u)} quad_perm:[3,0,1,2] {DPP}')
+            e(f'  v_cndmask_b32_e64 {Rlo(0, u)}, {Rlo(0, u)}, 0, s[22:23]')
+            e(f'  v_cndmask_b32_e64 {Rhi(0, u)}, {Rhi(0, u)}, 0, s[22:23]')
+            e(f'  v_cndmask_b32_e64 {Rlo(Q, u)}, 0, {Rlo(Q, u)}, s[20:21]')
+            e(f'  v_cndmask_b32_e64 {Rhi(Q, u)}, 0, {Rhi(Q, u)}, s[20:21]')
+            # 2. + a_i X, the top two columns first (lane 3's estimate)
+            order = [Q - 1, Q - 2] + list(range(Q - 3, -1, -1))
+            est = [
+                f'  v_lshlrev_b64 {d0}, {B}, {R(Q, u)}',                              # W: fold TT
+                f'  v_lshl_add_u64 {R(Q - 1, u)}, {d0}, 0, {R(Q - 1, u)}',           # (shift 0 only: a 0-4 field)
+                # -q = trunc(bias - V invN) with the constants negated on the host: trunc toward
+                # zero of a value in (-2^29, 2^-6] is -floor(V invN - bias), or 0 when that is < 0
+                f'  v_cvt_f64_i32_e32 {d0}, {Rhi(Q - 2, u)}',
+                f'  v_fma_f64 {acc}, {d0}, s[36:37], {bias}',
+                f'  v_cvt_f64_u32_e32 {d0}, {Rlo(Q - 1, u)}',
+                f'  v_fma_f64 {acc}, {d0}, s[38:39], {acc}',
+                f'  v_cvt_f64_i32_e32 {d0}, {Rhi(Q - 1, u)}',
+                f'  v_fma_f64 {acc}, {d0}, s[40:41], {acc}',
+                f'  v_cvt_i32_f64_e32 {q}, {acc}',
+                None, None,                                   # DPP read-after-VALU-write spacing
+                f'  v_mov_b32_dpp {q}, {q} quad_perm:[3,3,3,3] {DPP}',
+            ]
+            ei = 0
+            for n, j in enumerate(order):
+                e(f'  v_mad_u64_u32 {R(j, u)}, vcc, {ai}, {X(j)}, {R(j, u)}')
+                if n >= 1:
+                    while ei < len(est):
+                        ins = est[ei]
+                        ei += 1
+                        if ins is not None:
+                            e(ins)
+                            break
+                        else:
+                            break
+                if n == 12 and prefetch is not None:
+                    e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(prefetch - cur[0]) * RB_}')
+            for ins in est[ei:]:
+                if ins is not None:
+                    e(ins)
+                else:
+                    e('  s_nop 0')
+            # 3. - q N
+            for j in range(Q - 1, -1, -1):
+                e(f'  v_mad_i64_i32 {R(j, u)}, vcc, {q}, {NV(j)}, {R(j, u)}')
+            e('  s_waitcnt lgkmcnt(0)')
+
+        e('.Lmontmul_msb:')
+        for k in range(NTC):
+            e(f'  v_mov_b64_e32 v[{TB + 2 * k}:{TB + 2 * k + 1}], 0')
+        e(f'  v_mov_b32_e32 v{DBIAS}, 0')
+        e(f'  v_mov_b32_e32 v{DBIAS + 1}, 0x3f900000')            # +2^-6
+        # trips of STEPC steps from the top limb down; the cursor sits one row below the trip's
+        # lowest limb so every read (and the next step's prefetch) has a non-negative offset
+        first = S - 1
+        move_cursor(first - STEPC)                                # row below trip 0's lowest limb
+        e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI} offset:{(first - cur[0]) * RB_}')
+        e('  s_waitcnt lgkmcnt(0)')
+        # NTRIPC full trips, then the first TLC steps of one more (the same code: after NTRIPC trips
+        # the cursor row is TLC - 1 - STEPC, so step u reads limb TLC - 1 - u); the last trip leaves
+        # after step TLC - 1 (its prefetch of "limb -1" lands outside the wave's rows and is unused)
+        assert TLC > 0
+        e(f'  s_mov_b32 s18, {NTRIPC + 1}')
+        e('.Ltripc:')
+        base = cur[0]
+        for u in range(STEPC):
+            i = base + STEPC - u                                  # limb read at this step (trip 0)
+            step(u, i, i - 1)
+            if u == TLC - 1:
+                e('  s_cmp_eq_u32 s18, 1')
+                e('  s_cbranch_scc1 .Ltripc_done')
+        e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(STEPC * RB_)}, v{V_LDSI}')
+        e('  s_sub_u32 s18, s18, 1')
+        e('  s_branch .Ltripc')
+        e('.Ltripc_done:')
+        cur[0] -= NTRIPC * STEPC
+        move_cursor(0)
+        # normalise the signed columns (window phase u = TLC - 1) into X, then across lanes
+        ue = TLC - 1 if TLC else STEPC - 1
+        e(f'  v_mov_b64_e32 {tmp}, 0')
+        for k in range(Q):
+            e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {R(k, ue)}')
+            e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+            e(f'  v_ashrrev_i64 {tmp}, {B}, {tmp}')
+        ripple_quad(signed=True)
+        canon_once('mc')                                          # [0, 2N) -> canonical: chainable
+        e('  s_branch .Lprog')
+
     e('.Lmontmul:')
     for k in range(Q):
         e(f'  v_mov_b64_e32 {T(k)}, 0')
@@ -1049,6 +1217,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     e('  s_cbranch_scc1 .Lprog')
     e('  s_sub_u32 s19, s19, 1')
     e('  s_branch .Lsqr_loop')
+    if rowio:
+        emit_montmul_msb()
     e('.Lend:')
     e('  s_endpgm')
     e(f'.Lfunc_end_{name}:')
