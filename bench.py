@@ -46,7 +46,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
-PMC_FILE = "r01j_pmc.json"
+PMC_FILE = "r02g_pmc.json"
 
 
 def parse():
@@ -610,17 +610,22 @@ def run(a, world):
         dev.sync()
         add_s = lib.fthe_last_kernel_ms(dev.ctx) * 1e-3
         secondary["p2048_add_per_s"] = round(na / add_s)
+        prods = lib.fthe_last_montmuls(dev.ctx) / na          # 4096-bit products per add (1: classical MULWC)
         # the add kernel's HBM side (north star): algorithmic bytes (2 rows in, 1 out, 512 B each)
         # over the live launch time, and the PMC-measured bytes of a full-chunk launch
         pk = pmc.get("add", {}).get("fthe_montprog_s152", {})
         rate = na / add_s
         secondary["p2048_add_hbm"] = {"algorithmic_GBps": round(na * 1536 / add_s / 1e9, 1),
                                       "pmc_GBps": pk.get("hbm_GBps"), "pmc_VALUBusy": pk.get("VALUBusy"),
-                                      "peak_GBps": 8000, "bound": "valu (2 Montgomery products of 4096 bits per add)",
-                                      # VALU roofline in three units: executed MADs (2 products of
-                                      # 2*152^2 at radix 2^27), two products at W(128), the survey's one W(128)
-                                      "valu_frac_executed": round(rate * 2 * 2 * 152 * 152 / PEAK_MAC_S, 4),
-                                      "valu_frac_two_products": round(rate * 2 * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4),
+                                      "pmc_source": f"profiles/{PMC_FILE}" if pk else None,
+                                      "peak_GBps": 8000,
+                                      "bound": f"valu ({prods:g} product(s) of 4096 bits per add: classical MSB-first "
+                                               "x y mod n^2, no R^2 correction)",
+                                      # VALU roofline: executed MADs (2*152^2 per product at radix
+                                      # 2^27) and the survey's unit, one W(128) = 2*128^2+128 MACs per add
+                                      "products_per_add": prods,
+                                      "executed_over_algorithmic_macs": round(prods * 2 * 152 * 152 / (2 * 128 * 128 + 128), 3),
+                                      "valu_frac_executed": round(rate * prods * 2 * 152 * 152 / PEAK_MAC_S, 4),
                                       "valu_frac_survey_unit": round(rate * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4)}
         # the same adds on Montgomery-resident rows (x R mod n^2, include/fthe.h): one product per add
         # instead of two; rows converted in/out once per chain (conversion not in this rate)

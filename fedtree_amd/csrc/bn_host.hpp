@@ -158,8 +158,9 @@ struct Prog {
         else { sqr(n); mul(s); }
     }
     void mulwg(int t) { op(OP_MULWG, t); montmuls += 1; }
-    void mulwc(int t) { op(OP_MULWC, t); montmuls += 1; }
-    void mulwgc(int t) { op(OP_MULWGC, t); montmuls += 1; }
+    // canon: canonical output (X < N), required when another MULWC / MULWGC follows
+    void mulwc(int t, bool canon = false) { op(OP_MULWC, (uint32_t)t | (canon ? 0x100u : 0u)); montmuls += 1; }
+    void mulwgc(int t, bool canon = false) { op(OP_MULWGC, (uint32_t)t | (canon ? 0x100u : 0u)); montmuls += 1; }
     void canon() { op(OP_CANON, 0); }
     void loadgd(int j) { op(OP_LOADGD, j); }
     void mulgd(int j) { op(OP_MULGD, j); montmuls += 1; }

@@ -2632,7 +2632,7 @@ static int rowprod_impl(fthe_key *k, fthe_ctx *c, const uint32_t *const *xs, int
     if (classical) {
         cst = nullptr;
         p.loadw(0); p.canon();
-        for (int j = 1; j < kk; j++) p.mulwc(j);
+        for (int j = 1; j < kk; j++) p.mulwc(j, j + 1 < kk);
         p.storew(kk); p.end();
     } else if (rowio) {
         p.loadw(0);
@@ -2720,7 +2720,7 @@ struct GatherProd {
         Prog p;
         if (k->rowio && k->mn2.m.classical_ok() && !getenv("FTHE_ADD_MONT")) {
             p.loadwg(1); p.canon();       // classical products: no R^K correction
-            for (int j = 1; j < K; j++) p.mulwgc(1 + j);
+            for (int j = 1; j < K; j++) p.mulwgc(1 + j, j + 1 < K);
             p.storew(K + 1); p.end();
         } else if (k->rowio) {        // rows[0] = source, rows[1..K] = index lists, rows[K+1] = output
             p.loadwg(1);

@@ -933,6 +933,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     # MULWC t: X <- row_t * X mod N, classical (no Montgomery factor): the pairwise add of two
     # canonical ciphertexts in one product.  Needs X < N (canonical) and N >= 2^(B S - 10).
     e('.Lmulwc:')
+    e('  s_lshr_b32 s19, s15, 8')                # arg bit 8: canonical output (chained products)
+    e('  s_and_b32 s15, s15, 0xff')
     row_ptr()
     live_mask()
     load_row_limbs(lambda j: f"v{A0 + j}")
@@ -942,6 +944,8 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
 
     # MULWGC t: the same with the gathered row of MULWG t (idx list at rows[t], idx < 0 -> 1)
     e('.Lmulwgc:')
+    e('  s_lshr_b32 s19, s15, 8')
+    e('  s_and_b32 s15, s15, 0xff')
     load_gather_limbs(lambda j: f"v{A0 + j}")
     restore_exec()
     write_a(lambda j: f"v{A0 + j}")
@@ -950,7 +954,15 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
     # CANON: X (normalised limbs, < 4N: any 4096-bit row) -> X mod N, the precondition of MULWC
     e('.Lcanon:')
     for r in range(3):
+        # skip the remaining rounds once every quad's top limb is below N's (then X < N):
+        # the case of every ciphertext (< n^2 <= N) after at most one round
+        e(f'  v_cmp_lt_u32_e32 vcc, {X(Q - 1)}, {NV(Q - 1)}')
+        e('  s_nop 4')
+        e('  s_and_b64 s[26:27], vcc, s[20:21]')
+        e('  s_cmp_eq_u64 s[26:27], s[20:21]')
+        e('  s_cbranch_scc1 .Lcanon_done')
         canon_once(f'cn{r}')
+    e('.Lcanon_done:')
     e('  s_branch .Lprog')
 
     for wide in (False, True):
@@ -1089,19 +1101,23 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
             """one MSB step at ring phase u reading a_i (already in V_AI[u % 2])"""
             ai = f"v{V_AI[u % 2]}"
             nai = f"v{V_AI[(u + 1) % 2]}"
-            # 1. shift: lane k's offset Q -> lane k+1's new offset 0; lane 0 gets 0; offset Q stays
-            #    only on lane 3 (TT), zero elsewhere
-            e(f'  v_mov_b32_dpp {Rlo(0, u)}, {Rlo(Q, u)} quad_perm:[3,0,1,2] {DPP}')
-            e(f'  v_mov_b32_dpp {Rhi(0, u)}, {Rhi(Q, u)} quad_perm:[3,0,1,2] {DPP}')
-            e(f'  v_cndmask_b32_e64 {Rlo(0, u)}, {Rlo(0, u)}, 0, s[22:23]')
-            e(f'  v_cndmask_b32_e64 {Rhi(0, u)}, {Rhi(0, u)}, 0, s[22:23]')
-            e(f'  v_cndmask_b32_e64 {Rlo(Q, u)}, 0, {Rlo(Q, u)}, s[20:21]')
-            e(f'  v_cndmask_b32_e64 {Rhi(Q, u)}, 0, {Rhi(Q, u)}, s[20:21]')
+            # 1. shift.  Lane 3 (exec = lane 3 alone): fold TT (offset Q, the old position S-1) into
+            #    its new offset Q-1 as TT 2^B (the estimate's W; the a_i X term is added below, the
+            #    order is immaterial) and clear it.  Then one rotation hands every lane's offset Q to
+            #    lane k+1's new offset 0 -- lane 0 receives lane 3's cleared TT, i.e. 0.  (DPP must not
+            #    run under a partial exec: a disabled source lane would not be read.)
+            e('  s_mov_b64 exec, s[20:21]')
+            e(f'  v_lshlrev_b64 {d0}, {B}, {R(Q, u)}')
+            e(f'  v_lshl_add_u64 {R(Q - 1, u)}, {d0}, 0, {R(Q - 1, u)}')      # (shift field: 0-4 only)
+            e(f'  v_mov_b64_e32 {R(Q, u)}, 0')
+            e('  s_mov_b64 exec, -1')
             # 2. + a_i X, the top two columns first (lane 3's estimate)
             order = [Q - 1, Q - 2] + list(range(Q - 3, -1, -1))
+            hand = [                                     # after two MADs: the DPP source was just written
+                f'  v_mov_b32_dpp {Rlo(0, u)}, {Rlo(Q, u)} quad_perm:[3,0,1,2] {DPP}',
+                f'  v_mov_b32_dpp {Rhi(0, u)}, {Rhi(Q, u)} quad_perm:[3,0,1,2] {DPP}',
+            ]
             est = [
-                f'  v_lshlrev_b64 {d0}, {B}, {R(Q, u)}',                              # W: fold TT
-                f'  v_lshl_add_u64 {R(Q - 1, u)}, {d0}, 0, {R(Q - 1, u)}',           # (shift 0 only: a 0-4 field)
                 # -q = trunc(bias - V invN) with the constants negated on the host: trunc toward
                 # zero of a value in (-2^29, 2^-6] is -floor(V invN - bias), or 0 when that is < 0
                 f'  v_cvt_f64_i32_e32 {d0}, {Rhi(Q - 2, u)}',
@@ -1117,6 +1133,9 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
             ei = 0
             for n, j in enumerate(order):
                 e(f'  v_mad_u64_u32 {R(j, u)}, vcc, {ai}, {X(j)}, {R(j, u)}')
+                if n == 1:
+                    for ins in hand:
+                        e(ins)
                 if n >= 1:
                     while ei < len(est):
                         ins = est[ei]
@@ -1176,7 +1195,9 @@ def gen_quad(S: int, B: int, U: int, name: str) -> str:
             e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
             e(f'  v_ashrrev_i64 {tmp}, {B}, {tmp}')
         ripple_quad(signed=True)
-        canon_once('mc')                                          # [0, 2N) -> canonical: chainable
+        e('  s_cmp_eq_u32 s19, 0')                                # [0, 2N) -> canonical when chained
+        e('  s_cbranch_scc1 .Lprog')
+        canon_once('mc')
         e('  s_branch .Lprog')
 
     e('.Lmontmul:')

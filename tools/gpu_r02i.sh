@@ -1,0 +1,5 @@
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/r02i_pytest_gpu.txt 2>&1 || exit 1
+timeout -k 10 700 python bench.py --steps 3 --warmup 1 > gpurun_out/r02i_bench.json 2> gpurun_out/r02i_bench.err || exit 2
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02i_trace -o bench -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-secondary > gpurun_out/r02i_bench_under_rocprof.json 2> gpurun_out/r02i_rocprof.err || exit 3
