@@ -46,7 +46,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
-PMC_FILE = "r02g_pmc.json"
+PMC_FILE = "r02l_pmc.json"
 
 
 def parse():
@@ -514,6 +514,39 @@ def run(a, world):
                                               "pairs_per_s": round(nthr / ms * 1e3), "ok": all(ok),
                                               "note": "fthe_decrypt_shared: concurrent single-pair calls on one key "
                                                       "merged into one launch (group commit)"}
+        # GHPair::operator+ in the USE_HIP build: one Paillier_HIP_Pub::add -> fthe_add_shared per call
+        # (integration/fthe_ghpair_key.h), serially and from 32 threads on one key
+        rows = pl.encrypt_u64(np.arange(1, 65, dtype=np.uint64), seed=77)
+        acc = rows[:1].copy()
+        pl.add_shared(acc, rows[1:2], out=acc)
+        nser = 200
+        t0 = time.perf_counter()
+        for i in range(nser):
+            pl.add_shared(acc, rows[1 + i % 63:2 + i % 63], out=acc)
+        ser_us = (time.perf_counter() - t0) / nser * 1e6
+        nthr, per = 32, 50
+        accs = [rows[i:i + 1].copy() for i in range(nthr)]
+        go = threading.Barrier(nthr + 1)
+
+        def _adds(i):
+            go.wait()
+            for j in range(per):
+                pl.add_shared(accs[i], rows[(i + j) % 64:(i + j) % 64 + 1], out=accs[i])
+
+        ths = [threading.Thread(target=_adds, args=(i,)) for i in range(nthr)]
+        for t in ths:
+            t.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for t in ths:
+            t.join()
+        conc_s = time.perf_counter() - t0
+        secondary["ghpair_operator_add"] = {
+            "serial_us_per_add": round(ser_us, 1), "threads": nthr,
+            "concurrent_adds_per_s": round(nthr * per / conc_s),
+            "note": "one ciphertext add per call through the key's coalescing queue, as GHPair::operator+ / += "
+                    "issue them (host rows in and out, one four-lane product launch per merged batch); the "
+                    "batch entry points (merge, histogram, reduce_segments) are the throughput path"}
         # key generation (homo_init; re-run every round in the vertical simulation, FLtrainer.cpp:556):
         # host prime search on up to 16 threads + device key set-up
         t0 = time.perf_counter()

@@ -333,6 +333,7 @@ struct fthe_key {
     int c_p = -1, c_q = -1, c_2p = -1, c_pinv = -1, c_qinv2 = -1, c_hRp = -1, c_hRq = -1, c_qinvRp = -1;
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
+    bool add_classical = false;               // pr_add_w is one classical product (no R^2 constant)
     PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_pl, pr_dec_ql, pr_enc_pl, pr_enc_ql, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
 
@@ -604,7 +605,8 @@ static int key_finish(fthe_key *k) {
             // fresh add: one classical product a b mod n^2 when the modulus allows it (n of 2048 bits),
             // else a b R^-1 then the R^2 correction (two Montgomery products); FTHE_ADD_MONT=1: the latter
             Prog aw;
-            if (k->mn2.m.classical_ok() && !getenv("FTHE_ADD_MONT")) { aw.loadw(0); aw.canon(); aw.mulwc(1); aw.storew(2); }
+            k->add_classical = k->mn2.m.classical_ok() && !getenv("FTHE_ADD_MONT");
+            if (k->add_classical) { aw.loadw(0); aw.canon(); aw.mulwc(1); aw.storew(2); }
             else { aw.loadw(0); aw.mulw(1); aw.mul(SL_C0); aw.storew(2); }
             aw.end();
             k->pr_add_w = k->add_prog(aw);
@@ -2567,7 +2569,7 @@ static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t
                       : begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
-    Lc.fill(SL_C0, k->c_R2n2);
+    if (sub || !k->rowio || !k->add_classical) Lc.fill(SL_C0, k->c_R2n2);    // the classical add needs no R^2
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
