@@ -350,7 +350,8 @@ def run(a, world):
     wa = argparse.Namespace(**vars(a))
     wa.warmup = 0                                    # warm-up done above, before profiling is enabled
     elapsed_rank = timed_steps(lambda i: step(a.warmup + i), wa, world, sync)
-    kms, launches, lane_mm, lanes, ems, elaunch, amacs = (ctypes.c_double() for _ in range(7))
+    kms, launches, lane_mm, lanes, ems, elaunch, amacs, xmacs = (ctypes.c_double() for _ in range(8))
+    _lib.check(lib.fthe_prof_exec_macs(dev.ctx, ctypes.byref(xmacs)), "prof_exec_macs")
     _lib.check(lib.fthe_prof_read(dev.ctx, ctypes.byref(kms), ctypes.byref(launches), ctypes.byref(lane_mm),
                                   ctypes.byref(lanes), ctypes.byref(ems), ctypes.byref(elaunch),
                                   ctypes.byref(amacs)))
@@ -366,10 +367,11 @@ def run(a, world):
     enc_total = world * enc_rank
     value = enc_total / elapsed
 
-    # -- roofline of the dominant kernel family (montprog s37 + s74, per-launch HIP
-    # events on the engine stream, this rank).  Algorithmic work = the Montgomery
-    # products the programs perform x W(s) = 2 s^2 + s MACs on s = 32-bit words of
-    # the modulus (SURVEY.md 8(d) unit), accumulated per launch by the engine.
+    # -- roofline of the dominant kernel family (the exponentiation kernels, per-launch HIP
+    # events on the engine stream, this rank).  Algorithmic work = the 32-bit MACs of the
+    # executed algorithm, accumulated per launch by the engine: W(s) = 2 s^2 + s per Montgomery
+    # product on s = 32-bit words of the modulus (SURVEY.md 8(d) unit), and the P-adic kernel's
+    # own count per squaring / product mod P^2 (fthe.hip padic_alg: digit products + Barretts).
     alg_macs = amacs.value
     k_s = kms.value * 1e-3
     achieved = alg_macs / k_s / 1e12
@@ -384,20 +386,32 @@ def run(a, world):
             "survey_alg_macs_per_crt_encrypt_direct": ALG_MACS_PER_CRT_ENC,
             "montmuls_per_encrypt": round(lane_mm.value / enc_rank, 1),
             "kernel_share_of_step": round(k_s / elapsed_rank, 4)}
-    for S in (37, 74, 152):
+    # exponentiation kernels: the Montgomery program kernels and the P-adic one (pseudo-variant 1037)
+    for S, kname in ((37, "fthe_montprog_s37"), (74, "fthe_montprog_s74"), (152, "fthe_montprog_s152"),
+                     (1037, "fthe_padic_k37")):
         vms, vn = ctypes.c_double(), ctypes.c_double()
         lib.fthe_prof_variant(dev.ctx, S, ctypes.byref(vms), ctypes.byref(vn))
         if vn.value:
-            roof["avg_expo_launch_ms_by_kernel"][f"fthe_montprog_s{S}"] = round(vms.value / vn.value, 3)
+            roof["avg_expo_launch_ms_by_kernel"][kname] = round(vms.value / vn.value, 3)
     roof["kernel"] = " + ".join(roof["avg_expo_launch_ms_by_kernel"]) or "fthe_montprog"
-    # HBM traffic per full-chunk s74 launch from the committed PMC passes
+    if xmacs.value:
+        # the P-adic kernel in issue terms: its v_mad instructions (radix 2^28, counted per program by the
+        # engine) over its own launch time, against the same 39.3 T/s issue peak
+        vms, vn = ctypes.c_double(), ctypes.c_double()
+        lib.fthe_prof_variant(dev.ctx, 1037, ctypes.byref(vms), ctypes.byref(vn))
+        rate = xmacs.value / (vms.value * 1e-3) if vms.value else 0.0
+        roof["padic_executed_mads_per_encrypt"] = round(xmacs.value / enc_rank)
+        roof["padic_frac_executed_mads"] = round(rate / PEAK_MAC_S, 4)
+        roof["padic_frac_of_measured_mad_peak"] = round(rate / MEASURED_MAD_S, 4)
+    expo_kernel = "fthe_padic_k37" if "fthe_padic_k37" in roof["avg_expo_launch_ms_by_kernel"] else "fthe_montprog_s74"
+    # HBM traffic per full-chunk exponentiation launch from the committed PMC passes
     # (tools/pmc_round.sh; 2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section)
     pmc = {}
     prof_hbm = os.path.join(ROOT, "profiles", PMC_FILE)
     if os.path.exists(prof_hbm):
         pmc = json.load(open(prof_hbm))
-        roof["traffic"] = pmc.get("enc", {}).get("fthe_montprog_s74", {}).get("hbm_bytes_per_launch")
-        roof["traffic_source"] = f"profiles/{PMC_FILE} (s74 full-chunk launch)"
+        roof["traffic"] = pmc.get("enc", {}).get(expo_kernel, {}).get("hbm_bytes_per_launch")
+        roof["traffic_source"] = f"profiles/{PMC_FILE} ({expo_kernel} full-chunk launch)"
     # what the traffic is: SURVEY 8(d) algorithmic bytes (772 B per encrypt, half per prime launch) vs the
     # operand reads of the one-lane design (each window multiplication reads a 296-B table entry per lane)
     lanes = 393216

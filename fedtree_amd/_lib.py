@@ -115,6 +115,7 @@ _PROTOS = {
     "fthe_debug_direct_y": (_I, [_P, _P, _U64, _U64, _SZ, _P, _P]),
     "fthe_prof_enable": (_I, [_P, _I]),
     "fthe_prof_variant": (_I, [_P, _I, _P, _P]),
+    "fthe_prof_exec_macs": (_I, [_P, _P]),
     "fthe_prof_read": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
 }
 

@@ -131,18 +131,24 @@ enum Op : uint32_t { OP_END = 0, OP_LOADX = 1, OP_STOREX = 2, OP_SQR = 3, OP_MUL
                      // Montgomery factor); X canonical, N >= 2^(B S - 10)
                      OP_MULWC = 18,
                      // the same with the gathered row of MULWG t; CANON: X (< 4N) -> X mod N
-                     OP_MULWGC = 19, OP_CANON = 20 };
+                     OP_MULWGC = 19, OP_CANON = 20,
+                     // P-adic kernel (gen_padic.py): plain X (2K limbs) <-> base-P digits;
+                     // its LOADX / STOREX / SQR / MUL move and multiply digits
+                     OP_LOADP = 22, OP_STOREP = 23 };
 
 struct Prog {
     std::vector<uint32_t> w;
     double montmuls = 0;   // Montgomery products per lane (roofline accounting)
+    double squarings = 0;  // of which squarings (the P-adic kernel's algorithmic MAC count differs)
     // one-lane kernels: pow()/pow_ones() prefetch each multiplier into LDS
     // (PREFA) ahead of the squarings that precede it, then MULA
     bool lds_a = false;
     void op(Op o, uint32_t a) { w.push_back(o); w.push_back(a); }
     void loadx(int s) { op(OP_LOADX, s); }
     void storex(int s) { op(OP_STOREX, s); }
-    void sqr(int n) { if (n > 0) { op(OP_SQR, n); montmuls += n; } }
+    void sqr(int n) { if (n > 0) { op(OP_SQR, n); montmuls += n; squarings += n; } }
+    void loadp(int s) { op(OP_LOADP, s); }
+    void storep(int s) { op(OP_STOREP, s); }
     void mul(int s) { op(OP_MUL, s); montmuls += 1; }
     void addslot(int s) { op(OP_ADDSLOT, s); }
     void addsmall(uint32_t k) { op(OP_ADDSMALL, k); }

@@ -40,9 +40,12 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 4;
-// s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency)
-const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4}};
+constexpr int MAX_VARIANTS = 5;
+// s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency);
+// kPadicS: the P-adic exponentiation kernel mod P^2 (gen_padic.py, digits of 37 limbs), which runs
+// on the s74 slots (its "S" here only names the variant)
+constexpr int kPadicS = 1037, kPadicK = 37;
+const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4}, {kPadicS, 28, 1}};
 constexpr Shape kLatShape{80, 27, 4};
 
 int variant_index(int S) {
@@ -222,13 +225,15 @@ struct fthe_ctx {
     size_t prof_used = 0;
     double prof_lane_mm = 0;      // sum over launches of live lanes x products
     double prof_alg_macs = 0;     // sum over launches of live lanes x products x W(s), SURVEY 8(d)
+    double prof_exec_macs = 0;    // P-adic launches: v_mad instructions x live lanes
     double prof_launch_lanes = 0; // sum over launches of live lanes
 };
 
 // Device copy of one Montgomery modulus.
 struct DevMod {
     MontMod m;
-    uint32_t *d_ctx = nullptr;     // N limbs (S) + nprime
+    uint32_t *d_ctx = nullptr;     // N limbs (S) + nprime; P-adic: -P limbs, mu limbs
+    int kernel_S = 0;              // kPadicS: the P-adic kernel on m's slot shape (m.N = P^2)
     // SURVEY 8(d) work unit: W(s) = 2 s^2 + s 32x32 MACs per Montgomery
     // product on s = ceil(bits/32) u32 limbs (algorithmic, kernel-independent)
     double w_alg() const {
@@ -281,6 +286,10 @@ struct fthe_key {
     // small-batch decrypt on the four-lane s80 kernel (each product spread over a quad of lanes)
     Shape slat{0, 0, 0};
     DevMod mp2l, mq2l;
+    // P-adic exponentiation kernel mod p^2, q^2 (gen_padic.py): the CRT encrypt's y^P and the
+    // decrypt's c^(P-1); s74 programs before / after it convert to and from Montgomery form
+    bool padic = false;
+    DevMod mpA, mqA;
     int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1, cl_nRp = -1, cl_nRq = -1;
     int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
     int kp = 0, kq = 0;             // limbs of p, q
@@ -297,7 +306,8 @@ struct fthe_key {
     int pq_w = 0;
     ~fthe_key() {
         co.reset();
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l}) if (d->d_ctx) (void)hipFree(d->d_ctx);
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA})
+            if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
         if (d_nwords) (void)hipFree(d_nwords);
@@ -315,7 +325,8 @@ struct fthe_key {
     }
     uint32_t *cst(int h) const { return d_consts + const_off[h]; }
     // programs
-    struct PH { size_t off = 0; double mm = 0; };
+    // alg: algorithmic MACs per lane if not mm x W(s); exec: v_mad per lane (P-adic programs)
+    struct PH { size_t off = 0; double mm = 0, alg = -1, exec = -1; };
     PH add_prog(const Prog &p) {
         PH h; h.off = host_progs.size(); h.mm = p.montmuls;
         host_progs.insert(host_progs.end(), p.w.begin(), p.w.end());
@@ -336,6 +347,9 @@ struct fthe_key {
     bool add_classical = false;               // pr_add_w is one classical product (no R^2 constant)
     PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_pl, pr_dec_ql, pr_enc_pl, pr_enc_ql, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
+    // P-adic form of stage B: the exponentiation (P-adic kernel), then the rest on s74
+    PH prP_enc_p, prP_enc_q, prP_encB_p, prP_encB_q, prP_encB_p_nt;
+    PH prP_dec_pre_p, prP_dec_pre_q, prP_dec_p, prP_dec_q, prP_dec_post_p, prP_dec_post_q;
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
     // r^n = hs^alpha with hs = h^n mod n^2 for one random h per key: 8-bit-window
@@ -451,7 +465,8 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         if (!blob) return FTHE_ERR_HIP;
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
-        snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
+        if (kVariants[i].S == kPadicS) snprintf(name, sizeof name, "fthe_padic_k%d", kPadicK);
+        else snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
         HIPOK(hipFuncGetAttribute(&c->static_lds[i], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, c->fn[i]));
     }
@@ -517,6 +532,15 @@ extern "C" int fthe_prof_enable(fthe_ctx *c, int on) {
     if (!c) return FTHE_ERR_ARG;
     c->prof = on != 0;
     c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0; c->prof_alg_macs = 0;
+    c->prof_exec_macs = 0;
+    return FTHE_OK;
+}
+
+extern "C" int fthe_prof_exec_macs(fthe_ctx *c, double *exec_macs) {
+    if (!c || !exec_macs) return FTHE_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipStreamSynchronize(c->stream));
+    *exec_macs = c->prof_exec_macs;
     return FTHE_OK;
 }
 
@@ -543,7 +567,7 @@ extern "C" int fthe_prof_read(fthe_ctx *c, double *kernel_ms, double *launches, 
     if (lane_montmuls) *lane_montmuls = c->prof_lane_mm;
     if (lanes) *lanes = c->prof_launch_lanes;
     if (alg_macs) *alg_macs = c->prof_alg_macs;
-    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0; c->prof_alg_macs = 0; c->prof_alg_macs = 0;
+    c->prof_used = 0; c->prof_lane_mm = 0; c->prof_launch_lanes = 0; c->prof_alg_macs = 0; c->prof_exec_macs = 0;
     return FTHE_OK;
 }
 
@@ -554,6 +578,48 @@ static int upload_mod(DevMod &d, const mpz_t N, Shape sh) {
     if (hipMalloc(&d.d_ctx, d.m.ctx.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(d.d_ctx, d.m.ctx.data(), d.m.ctx.size() * 4, hipMemcpyHostToDevice));
     return FTHE_OK;
+}
+
+// P-adic kernel constants for P (gen_padic.py): -P in K radix-2^28 limbs (int32), 3 zero words,
+// mu = floor(2^(56 K) / P) in K + 1 limbs.  Runs on the s74 slots: m is P^2 on that shape (slot
+// strides, roofline units).  Needs b^(K-1) <= P and 5P, 50P < b^K: P of 1009..1030 bits.
+static bool padic_ok(const mpz_t P, Shape sh) {
+    const size_t b = mpz_sizeinbase(P, 2);
+    return sh.S == 2 * kPadicK && sh.B == 28 && sh.lanes == 1 && b >= 1009 && b <= 1030 &&
+           !getenv("FTHE_NO_PADIC");
+}
+static int upload_padic(DevMod &d, const mpz_t P, Shape sh) {
+    Mpz P2; mpz_mul(P2, P, P);
+    d.m.init(P2, sh);
+    const int K = kPadicK;
+    std::vector<uint32_t> w(2 * K + 4, 0u), l = to_limbs(P, K, 28);
+    for (int j = 0; j < K; j++) w[j] = (uint32_t)(-(int32_t)l[j]);
+    Mpz mu; mpz_set_ui(mu, 1); mpz_mul_2exp(mu, mu, 56 * K); mpz_fdiv_q(mu, mu, P);
+    std::vector<uint32_t> ml = to_limbs(mu, K + 1, 28);
+    std::copy(ml.begin(), ml.end(), w.begin() + K + 3);
+    if (hipMalloc(&d.d_ctx, w.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    HIPOK(hipMemcpy(d.d_ctx, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    d.kernel_S = kPadicS;
+    return FTHE_OK;
+}
+// Algorithmic 32-bit MACs of a P-adic program (SURVEY 8(d) units, the executed algorithm): s = words
+// of P; squaring s^2 (2 x0 x1) + s(s+1)/2 (x0^2) + 2 Barretts, product 3 s^2 + 2 Barretts, a Barrett
+// (s+1)(s+2)/2 (upper half of q1 mu) + s(s+1)/2 (lower half of q3 P); LOADP one Barrett, STOREP s^2.
+static double padic_alg(const Prog &p, const mpz_t P) {
+    const double s = (double)((mpz_sizeinbase(P, 2) + 31) / 32);
+    const double bar = (s + 1) * (s + 2) / 2 + s * (s + 1) / 2;
+    const double sq = s * s + s * (s + 1) / 2 + 2 * bar, mul = 3 * s * s + 2 * bar;
+    return p.squarings * sq + (p.montmuls - p.squarings) * mul + bar + s * s;
+}
+// v_mad instructions per lane of the same program in the kernel (K = 37 radix-2^28 limbs per digit),
+// as emitted by gen_padic.py: a Barrett is K(K+1)/2 + 2K + 1 (q2 columns K-1..2K) + K(K+1)/2 + K
+// (r columns 0..K-1, one init MAD each); squaring K^2 + K(K+1)/2 + 2 Barretts, product 3 K^2 +
+// 2 Barretts, LOADP one Barrett, STOREP K^2 + K (5,108 / 7,143 / 1,518 / 1,406 at K = 37).
+static double padic_exec(const Prog &p) {
+    const double K = kPadicK;
+    const double bar = K * (K + 1) + 3 * K + 1;
+    const double sq = K * K + K * (K + 1) / 2 + 2 * bar, mul = 3 * K * K + 2 * bar;
+    return p.squarings * sq + (p.montmuls - p.squarings) * mul + bar + K * K + K;
 }
 
 static int key_finish(fthe_key *k) {
@@ -710,6 +776,39 @@ static int key_finish(fthe_key *k) {
                 e.end();
                 (side ? k->pr_enc_q : k->pr_enc_p) = k->add_prog(e);
             }
+            // P-adic stage B (P of 1009..1030 bits: Paillier-2048): y^P mod P^2 on the P-adic kernel
+            // (1.4x the products/s of the Montgomery s74 program), then (1 + m n) y^P and the CRT tail
+            // on s74 after one product into Montgomery form.  FTHE_NO_PADIC=1: the s74 programs above.
+            k->padic = padic_ok(k->p, sh) && padic_ok(k->q, sh);
+            if (k->padic) {
+                if ((rc = upload_padic(k->mpA, k->p, sh))) return rc;
+                if ((rc = upload_padic(k->mqA, k->q, sh))) return rc;
+                for (int side = 0; side < 2; side++) {
+                    const Mpz &P = side ? k->q : k->p;
+                    Prog a;                                          // P-adic kernel
+                    a.loadp(side ? SL_T4 : SL_T3);
+                    a.pow(P, SL_TAB, SL_SQ, wB);                     // y^P mod P^2 (< 6 P^2)
+                    a.storep(SL_SAVED); a.end();
+                    fthe_key::PH ha = k->add_prog(a);
+                    ha.alg = padic_alg(a, P);
+                    ha.exec = padic_exec(a);
+                    (side ? k->prP_enc_q : k->prP_enc_p) = ha;
+                    Prog e;                                          // s74
+                    e.loadx(SL_SAVED); e.mul(side ? SL_C2 : SL_C0);  // y^P R
+                    e.storex(SL_SAVED);
+                    e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1);
+                    e.addsmall(1); e.mul(SL_SAVED);                  // (1 + m n) r^n mod P^2
+                    if (side) {
+                        e.storex(SL_OUTQ);
+                    } else {
+                        Prog nt = e; nt.storex(SL_OUTP); nt.end();
+                        k->prP_encB_p_nt = k->add_prog(nt);
+                        crt_tail(e);
+                    }
+                    e.end();
+                    (side ? k->prP_encB_q : k->prP_encB_p) = k->add_prog(e);
+                }
+            }
         }
         // --- CRT decrypt constants
         k->c_p = k->add_const(L_(k->p));
@@ -754,6 +853,29 @@ static int key_finish(fthe_key *k) {
             d.mul(SL_T5);                                        // * 1 -> out of Montgomery
             d.storex(side ? SL_OUTQ : SL_OUTP); d.end();
             (side ? k->pr_dec_q : k->pr_dec_p) = k->add_prog(d);
+        }
+        // the same with c^(P-1) on the P-adic kernel: c mod P^2 on s74 (< 2 P^2, plain), the
+        // exponentiation, then back to a residue < 2 P^2 on s74 for the L-function tail
+        for (int side = 0; side < 2 && k->padic; side++) {
+            Prog d;
+            d.loadx(SL_IN1); d.mul(side ? SL_C3 : SL_C1);
+            d.storex(SL_T0);
+            d.loadx(SL_IN0); d.mul(side ? SL_C2 : SL_C0);
+            d.addslot(SL_T0);                                    // c R mod P^2 (< 4 P^2)
+            d.mul(SL_T5);                                        // c mod P^2 (< 2 P^2)
+            d.storex(SL_SAVED); d.end();
+            (side ? k->prP_dec_pre_q : k->prP_dec_pre_p) = k->add_prog(d);
+            const Mpz &Pm1 = side ? qm1 : pm1;
+            Prog a;
+            a.loadp(SL_SAVED); a.pow(Pm1, SL_TAB, SL_SQ, k->w_dec); a.storep(SL_SAVED); a.end();
+            fthe_key::PH ha = k->add_prog(a);
+            ha.alg = padic_alg(a, side ? k->q : k->p);
+            ha.exec = padic_exec(a);
+            (side ? k->prP_dec_q : k->prP_dec_p) = ha;
+            Prog t;
+            t.loadx(SL_SAVED); t.mul(side ? SL_C2 : SL_C0); t.mul(SL_T5);   // (X R) * 1 R^-1: X mod P^2 < 2 P^2
+            t.storex(side ? SL_OUTQ : SL_OUTP); t.end();
+            (side ? k->prP_dec_post_q : k->prP_dec_post_p) = k->add_prog(t);
         }
         // the same exponentiations on the four-lane s80 kernel, for batches that leave the chip idle
         if (S == 74 && !getenv("FTHE_NO_QUAD_DEC") && p2.bits() + 8 <= (size_t)kLatShape.S * kLatShape.B &&
@@ -1066,7 +1188,7 @@ constexpr int kSpreadLds = 84 * 1024;   // > 80 KB: one workgroup per CU (gfx950
 
 int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, const DevMod &mod, double lane_mm,
                     size_t live, const void *const *rows = nullptr, int nrows = 0, hipStream_t st = nullptr,
-                    bool spread = false) {
+                    bool spread = false, double lane_alg = -1, double lane_exec = -1) {
     if (!st) st = c->stream;
     struct {
         void *s; const void *p; const void *cx; uint32_t ls, ss; uint32_t live, pad; const void *rows[16];
@@ -1076,7 +1198,7 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     for (int i = 0; i < nrows; i++) args.rows[i] = rows[i];
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    int vi = variant_index(S);
+    int vi = variant_index(mod.kernel_S ? mod.kernel_S : S);
     if (vi < 0) return FTHE_ERR_UNSUPPORTED;
     // only the workgroups that hold live elements (slot strides stay those of L)
     if (live > (size_t)L) return FTHE_ERR_ARG;
@@ -1108,7 +1230,8 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     if (ev) {
         HIPOK(hipEventRecord(ev->second, st));
         c->prof_lane_mm += lane_mm * (double)live;
-        c->prof_alg_macs += lane_mm * (double)live * mod.w_alg();
+        c->prof_alg_macs += (lane_alg >= 0 ? lane_alg : lane_mm * mod.w_alg()) * (double)live;
+        if (lane_exec >= 0) c->prof_exec_macs += lane_exec * (double)live;
         c->prof_launch_lanes += (double)live;
     }
     return FTHE_OK;
@@ -1135,7 +1258,8 @@ struct Launch {
     dim3 grid() const { return dim3((unsigned)(L / 256)); }
     int prog(const fthe_key::PH &ph, const DevMod &mod, const void *const *rows = nullptr, int nrows = 0) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
-        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows, st, spread);
+        int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows, st, spread, ph.alg,
+                                 ph.exec);
         if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;
@@ -1151,6 +1275,22 @@ struct Launch {
         hipLaunchKernelGGL(k_fill_const, grid(), dim3(256), 0, st ? st : c->stream, k->cst(h), slot(s), S, L);
     }
 };
+
+// CRT stage B of the encrypt (side 0: p, 1: q; nt: the p program without the CRT tail) and the
+// decrypt's c^(P-1) mod P^2: P-adic exponentiation + s74 programs when the key has them.
+int enc_stage_b(Launch &L, const fthe_key *k, int side, bool nt = false) {
+    const DevMod &m2 = side ? k->mq2 : k->mp2;
+    if (!k->padic) return L.prog(side ? k->pr_enc_q : (nt ? k->pr_enc_p_nt : k->pr_enc_p), m2);
+    if (int rc = L.prog(side ? k->prP_enc_q : k->prP_enc_p, side ? k->mqA : k->mpA)) return rc;
+    return L.prog(side ? k->prP_encB_q : (nt ? k->prP_encB_p_nt : k->prP_encB_p), m2);
+}
+int dec_pow(Launch &L, const fthe_key *k, int side) {
+    const DevMod &m2 = side ? k->mq2 : k->mp2;
+    if (!k->padic) return L.prog(side ? k->pr_dec_q : k->pr_dec_p, m2);
+    if (int rc = L.prog(side ? k->prP_dec_pre_q : k->prP_dec_pre_p, m2)) return rc;
+    if (int rc = L.prog(side ? k->prP_dec_q : k->prP_dec_p, side ? k->mqA : k->mpA)) return rc;
+    return L.prog(side ? k->prP_dec_post_q : k->prP_dec_post_p, m2);
+}
 
 int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots, Shape sh,
                size_t chunk = 0) {
@@ -1478,9 +1618,9 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                 pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lq.slot(SL_T4), S, L, Lc.B);
                 HIPOK(hipEventRecord(c->ev_fork, c->stream));
                 HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-                if ((rc = Lq.prog(k->pr_enc_q, k->mq2))) return rc;
+                if ((rc = enc_stage_b(Lq, k, 1))) return rc;
                 HIPOK(hipEventRecord(c->ev_join, c->side));
-                if ((rc = Lc.prog(k->pr_enc_p_nt, k->mp2))) return rc;
+                if ((rc = enc_stage_b(Lc, k, 0, true))) return rc;
                 HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
                 hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lq.slot(SL_OUTQ),
                                    k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
@@ -1492,10 +1632,10 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                 if (pipe && (rc = pipe->after(off, cnt))) return rc;
                 continue;
             }
-            if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
+            if ((rc = enc_stage_b(Lc, k, 1))) return rc;
             hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
                                k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;          // ends with h = (cp - cq) q^-2 in T2
+            if ((rc = enc_stage_b(Lc, k, 0))) return rc;                 // ends with h = (cp - cq) q^-2 in T2
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
                         k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
@@ -1521,10 +1661,10 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                                Lc.slot(SL_T3), S, L);
             hipLaunchKernelGGL(k_copy_limbs, Lc.grid(), dim3(256), 0, c->stream, L1.slot(SL_OUTQ), L1.S,
                                Lc.slot(SL_T4), S, L);
-            if ((rc = Lc.prog(k->pr_enc_q, k->mq2))) return rc;
+            if ((rc = enc_stage_b(Lc, k, 1))) return rc;
             hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
                                k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = Lc.prog(k->pr_enc_p, k->mp2))) return rc;          // ends with h = (cp - cq) q^-2 in T2
+            if ((rc = enc_stage_b(Lc, k, 0))) return rc;                 // ends with h = (cp - cq) q^-2 in T2
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
@@ -2496,10 +2636,10 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
                 pack_rows(c->stream, src, cw, cnt, Lc.B * S, Lq.slot(SL_IN1), S, L, Lc.B);
                 HIPOK(hipEventRecord(c->ev_fork, c->stream));
                 HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-                if ((rc = Lq.prog(k->pr_dec_q, k->mq2))) return rc;
+                if ((rc = dec_pow(Lq, k, 1))) return rc;
                 HIPOK(hipEventRecord(c->ev_join, c->side));
             }
-            if ((rc = Lc.prog(k->pr_dec_p, k->mp2))) return rc;
+            if ((rc = dec_pow(Lc, k, 0))) return rc;
         }
         if (short_pt) {
             // plaintext < p: m = m_p = L_p(c^(p-1) mod p^2) h_p mod p, the q half and the CRT skipped
@@ -2518,7 +2658,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         }
         if (split) {
             HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-        } else if (!quad && (rc = Lc.prog(k->pr_dec_q, k->mq2))) {
+        } else if (!quad && (rc = dec_pow(Lc, k, 1))) {
             return rc;
         }
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,

@@ -434,16 +434,21 @@ double fthe_last_montmuls(fthe_ctx *ctx);
  *   lanes          sum over launches of live lanes
  *   expo_ms/_launches  the same restricted to exponentiation launches
  *                  (programs of >= 64 products per lane)
- *   alg_macs       algorithmic work of those launches: live lanes x products x
- *                  W(s), W(s) = 2 s^2 + s with s = 32-bit words of the modulus
- *                   -- independent of the kernel's radix */
+ *   alg_macs       algorithmic work of those launches in 32-bit MACs: live lanes x
+ *                  products x W(s), W(s) = 2 s^2 + s with s = 32-bit words of the
+ *                  modulus, and for the P-adic kernel its own count
+ *                  (digit products + Barrett reductions) -- independent of the radix */
 int    fthe_prof_enable(fthe_ctx *ctx, int on);
 int    fthe_prof_read(fthe_ctx *ctx, double *kernel_ms, double *launches,
                       double *lane_montmuls, double *lanes,
                       double *expo_ms, double *expo_launches, double *alg_macs);
-/* Per kernel variant (limb count S: 37, 74, 152) exponentiation-launch time and
- * count of the last fthe_prof_read window. */
+/* Per kernel variant (limb count S: 37, 74, 152, 80; 1037 = the P-adic kernel mod
+ * p^2 / q^2) exponentiation-launch time and count of the last fthe_prof_read window. */
 int    fthe_prof_variant(fthe_ctx *ctx, int S, double *expo_ms, double *expo_launches);
+/* Multiply-add instructions (v_mad, per lane, summed over live lanes) the P-adic
+ * kernel's launches executed since the last fthe_prof_enable / fthe_prof_read;
+ * read it before fthe_prof_read, which resets it. */
+int    fthe_prof_exec_macs(fthe_ctx *ctx, double *exec_macs);
 /* limb count S of the radix-2^28 kernel used for a modulus of `bits` bits
  * (0 if unsupported). */
 int    fthe_kernel_limbs(int bits);

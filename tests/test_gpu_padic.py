@@ -1,0 +1,87 @@
+"""The P-adic exponentiation kernel (fthe_padic_k37) behind the key holder's CRT encrypt
+and decrypt at Paillier-2048: the same ciphertexts and plaintexts as the Montgomery s74 programs it
+replaces (FTHE_NO_PADIC=1 at key set-up restores those), for injected r at the extremes and random r,
+and its launches really run (profiling counters of the variant).  Integer work: exact equality.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20261016
+
+
+@pytest.fixture(scope="module")
+def keys():
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    pa = Paillier(dev).keygen(2048, seed=SEED)
+    os.environ["FTHE_NO_PADIC"] = "1"
+    try:
+        pm = Paillier.from_primes(pa.p, pa.q, dev)
+    finally:
+        del os.environ["FTHE_NO_PADIC"]
+    return dev, pa, pm
+
+
+def _r_words(pl, rs):
+    return pyoracle.ints_to_words(rs, pl.n_words)
+
+
+def test_injected_r_same_ciphertexts_as_montgomery(keys, coracle):
+    dev, pa, pm = keys
+    rng = np.random.default_rng(SEED)
+    n = pa.modulus
+    cnt = 3000
+    rs = [1, 2, n - 1, n - 2] + [int.from_bytes(rng.bytes(256), "little") % (n - 1) + 1 for _ in range(cnt - 4)]
+    m = rng.integers(0, 2**63, cnt, dtype=np.uint64)
+    m[:4] = [0, 1, 2**63 - 1, 2**62]
+    rw = _r_words(pa, rs)
+    ca = pa.encrypt_u64(m, r=rw)
+    cm = pm.encrypt_u64(m, r=rw)
+    assert np.array_equal(ca, cm)
+    pw = (max(pa.p.bit_length(), pa.q.bit_length()) + 31) // 32
+    ok = coracle.key(pyoracle.to_words(pa.p, pw), pyoracle.to_words(pa.q, pw))
+    idx = np.r_[0:8, cnt - 8:cnt]
+    assert np.array_equal(ca[idx], ok.encrypt_batch(m[idx], rw[idx]))
+    assert np.array_equal(pa.decrypt_u64(ca), m)
+    assert np.array_equal(pm.decrypt_u64(ca), m)
+
+
+def test_device_randomness_same_as_montgomery_and_decrypts(keys):
+    dev, pa, pm = keys
+    rng = np.random.default_rng(SEED + 1)
+    for cnt in (40000, 70000):                   # the split path (<= 65,536 lanes) and the chunked one
+        m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+        ca = pa.encrypt_u64(m, seed=SEED + cnt)
+        cm = pm.encrypt_u64(m, seed=SEED + cnt)
+        assert np.array_equal(ca, cm), cnt
+        assert np.array_equal(pa.decrypt_u64(ca), m)
+        assert np.array_equal(pa.decrypt_u64(ca, short=False, full=False), pm.decrypt_u64(ca))
+        full_a = pa.decrypt_u64(ca[:256], full=True)
+        full_m = pm.decrypt_u64(ca[:256], full=True)
+        assert np.array_equal(full_a, full_m)
+
+
+def test_padic_launches_run(keys):
+    dev, pa, pm = keys
+    lib = dev.lib
+    m = np.arange(70000, dtype=np.uint64)
+    lib.fthe_prof_enable(dev.ctx, 1)
+    pa.encrypt_u64(m, seed=3)
+    x = ctypes.c_double()
+    assert lib.fthe_prof_exec_macs(dev.ctx, ctypes.byref(x)) == 0
+    vals = [ctypes.c_double() for _ in range(7)]
+    assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
+    ms, nl = ctypes.c_double(), ctypes.c_double()
+    assert lib.fthe_prof_variant(dev.ctx, 1037, ctypes.byref(ms), ctypes.byref(nl)) == 0
+    lib.fthe_prof_enable(dev.ctx, 0)
+    assert nl.value == 2 and ms.value > 0                 # y_p^p and y_q^q, one launch each
+    # v_mad per lane: 1,024 squarings x 5,108 + ~180 products x 7,143 + LOADP / STOREP, per prime
+    per_lane = x.value / (2 * 70000)
+    assert 6.0e6 < per_lane < 7.0e6, per_lane

@@ -1,0 +1,73 @@
+"""CPU checks of the P-adic kernel's arithmetic: the bit-exact model (tools/padic_model.py)
+at the digit bounds, and the generated gfx950 assembly itself run on the single-lane emulator
+(tools/asm_emu.py) for LOADP / SQR / MUL / STOREP against Python integers and the model."""
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "fedtree_amd", "csrc"))
+
+import padic_model as pm  # noqa: E402
+
+K = 37
+
+
+def _key(rng, bits):
+    return pm.PadicKey(rng.getrandbits(bits) | (1 << (bits - 1)) | 1, K)
+
+
+def test_model_products_at_digit_bounds():
+    rng = random.Random(11)
+    for bits in (1009, 1024, 1030):
+        key = _key(rng, bits)
+        P, P2 = key.P, key.P * key.P
+        hi = pm.limbs(5 * P - 1, K)
+        for a0, a1, b0, b1 in ((hi, hi, hi, hi),
+                               tuple(pm.limbs(rng.randrange(5 * P), K) for _ in range(4))):
+            A = pm.value(a0) + pm.value(a1) * P
+            B = pm.value(b0) + pm.value(b1) * P
+            z0, z1 = pm.mul(key, a0, a1, b0, b1)
+            assert (pm.value(z0) + pm.value(z1) * P) % P2 == A * B % P2
+            pm.check_digit(key, z0)
+            pm.check_digit(key, z1)
+            z0, z1 = pm.sqr(key, a0, a1)
+            assert (pm.value(z0) + pm.value(z1) * P) % P2 == A * A % P2
+            pm.check_digit(key, z0)
+            pm.check_digit(key, z1)
+
+
+def test_generated_assembly_on_emulator():
+    from asm_emu import Emu, M32
+    from gen_padic import gen_padic
+    asm = gen_padic(K, 28, "fthe_padic_k37")
+    rng = random.Random(5)
+    key = _key(rng, 1024)
+    P, P2 = key.P, key.P * key.P
+    S, L = 2 * K, 256
+    KA, CTX, PROG, SLOTS = 0x100, 0x1000, 0x2000, 0x100000
+    X, Y = rng.randrange(P2), rng.randrange(P2)
+    # LOADP 0 -> STOREX 2; LOADP 1 -> MUL 2 -> SQR 1 -> STOREX 3; STOREP 4
+    prog = [22, 0, 2, 2, 22, 1, 4, 2, 3, 1, 2, 3, 23, 4, 0, 0]
+    em = Emu(asm)
+    for i, v in enumerate([SLOTS, 0, PROG, 0, CTX, 0, L * 4, S * L * 4, L, 0]):
+        em.mem[KA + 4 * i] = v
+    for i, w in enumerate([(-x) & M32 for x in pm.limbs(P, K)] + [0, 0, 0] + key.mu):
+        em.mem[CTX + 4 * i] = w
+    for i, w in enumerate(prog):
+        em.mem[PROG + 4 * i] = w
+    for slot, val in ((0, X), (1, Y)):
+        for k, limb in enumerate(pm.limbs(val, S)):
+            em.mem[SLOTS + slot * S * L * 4 + k * L * 4] = limb
+    em.s[0], em.s[1], em.s[2] = KA, 0, 0
+    em.v[0] = 0
+    em.run("fthe_padic_k37")
+    rd = lambda slot: [em.mem.get(SLOTS + slot * S * L * 4 + k * L * 4, 0) for k in range(S)]
+    x0, x1 = pm.loadp(key, X)
+    assert rd(2) == x0 + x1                                    # raw digits of LOADP, as the model's
+    y0, y1 = pm.loadp(key, Y)
+    z0, z1 = pm.sqr(key, *pm.mul(key, y0, y1, x0, x1))
+    assert rd(3) == z0 + z1                                    # MUL then SQR, limb for limb
+    out = pm.value(rd(4))
+    assert out % P2 == (X * Y) ** 2 % P2 and out < 6 * P2      # STOREP: x0 + x1 P
