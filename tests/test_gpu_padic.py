@@ -62,10 +62,11 @@ def test_device_randomness_same_as_montgomery_and_decrypts(keys):
         cm = pm.encrypt_u64(m, seed=SEED + cnt)
         assert np.array_equal(ca, cm), cnt
         assert np.array_equal(pa.decrypt_u64(ca), m)
-        assert np.array_equal(pa.decrypt_u64(ca, short=False, full=False), pm.decrypt_u64(ca))
-        full_a = pa.decrypt_u64(ca[:256], full=True)
-        full_m = pm.decrypt_u64(ca[:256], full=True)
-        assert np.array_equal(full_a, full_m)
+        assert np.array_equal(pa.decrypt_u64(ca, short=True), m)
+        la, fa = pa.decrypt_u64(ca, full=True)
+        lm, fm = pm.decrypt_u64(ca, full=True)
+        assert np.array_equal(la, lm) and np.array_equal(fa, fm)
+        assert np.array_equal(fa[:, :2].copy().view(np.uint64).ravel(), m) and not fa[:, 2:].any()
 
 
 def test_padic_launches_run(keys):
