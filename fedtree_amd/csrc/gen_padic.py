@@ -39,7 +39,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gen_montprog import _descriptor  # noqa: E402
 
-NCH = int(os.environ.get("FTHE_GEN_PADIC_CHAINS", "2"))     # independent accumulator chains per column
+NCH = int(os.environ.get("FTHE_GEN_PADIC_CHAINS", "2"))     # accumulator chains per column (PAIR off)
+PAIR = not os.environ.get("FTHE_GEN_PADIC_NOPAIR")             # two columns side by side, one chain each
 
 
 def gen_padic(K: int, B: int, name: str) -> str:
@@ -99,53 +100,77 @@ def gen_padic(K: int, B: int, name: str) -> str:
              out:   register for the limb (None: carry only)
              last:  keep the whole accumulator (low word) as the limb, no carry out
              nocarry: the limb is masked but no carry leaves the column (mod b^n)
-        The carry of the first column is 0."""
+        The carry of the first column is 0.  PAIR: two adjacent columns accumulate side by side, one
+        chain each (no chain-combining instruction); else NCH chains per column."""
         mad = 'v_mad_i64_i32' if signed else 'v_mad_u64_u32'
         shr = 'v_ashrrev_i64' if signed else 'v_lshrrev_b64'
-        pending = []                             # tail instructions of the previous column
+        pending = []                             # tail instructions of the previous group
 
         def flush(n):
             for _ in range(min(n, len(pending))):
                 e(pending.pop(0))
 
-        for ci, col in enumerate(cols):
-            s = ci % 2
-            terms = col['terms']
-            used = [False] * NCH
-            for t, (a, b) in enumerate(terms):
-                ch = t % NCH
-                src2 = acc(s, ch) if used[ch] else '0'
-                used[ch] = True
-                e(f'  {mad} {acc(s, ch)}, vcc, {a}, {b}, {src2}')
-                if t % 2 == 1:
-                    flush(1)
-            flush(len(pending))
-            tail = []
-            nch = sum(used)
-            a0 = acc(s, 0)
-            for ch in range(1, NCH):
-                if used[ch]:
-                    tail.append(f'  v_lshl_add_u64 {a0}, {acc(s, ch)}, 0, {a0}')
+        def tail_of(ci, col, chains):
+            """tail of column ci whose term sum is in chains[0] (+ the other used chains)"""
+            t = []
+            a0 = chains[0][0]
+            lo0 = chains[0][1]
+            used = [c for c in chains if c[2]]
+            for c in used[1:]:
+                t.append(f'  v_lshl_add_u64 {a0}, {c[0]}, 0, {a0}')
             first = ci == 0
-            if nch == 0:
+            if not used:
                 if col.get('sq'):
                     raise AssertionError("square term without cross terms")
-                src = '0' if first else carry
-                tail.append(f'  v_mov_b64_e32 {a0}, {src}')
+                t.append(f'  v_mov_b64_e32 {a0}, {"0" if first else carry}')
             elif col.get('dbl'):
-                tail.append(f'  v_lshl_add_u64 {a0}, {a0}, 1, {"0" if first else carry}')
+                t.append(f'  v_lshl_add_u64 {a0}, {a0}, 1, {"0" if first else carry}')
             elif not first:
-                tail.append(f'  v_lshl_add_u64 {a0}, {a0}, 0, {carry}')
+                t.append(f'  v_lshl_add_u64 {a0}, {a0}, 0, {carry}')
             if col.get('sq'):
                 x = col['sq']
-                tail.append(f'  {mad} {a0}, vcc, {x}, {x}, {a0}')
+                t.append(f'  {mad} {a0}, vcc, {x}, {x}, {a0}')
             if col.get('out') is not None:
                 if col.get('last'):
-                    tail.append(f'  v_mov_b32_e32 {col["out"]}, {acclo(s, 0)}')
+                    t.append(f'  v_mov_b32_e32 {col["out"]}, {lo0}')
                 else:
-                    tail.append(f'  v_and_b32_e32 {col["out"]}, {hex(MASK)}, {acclo(s, 0)}')
+                    t.append(f'  v_and_b32_e32 {col["out"]}, {hex(MASK)}, {lo0}')
             if not col.get('last') and not col.get('nocarry'):
-                tail.append(f'  {shr} {carry}, {B}, {a0}')
+                t.append(f'  {shr} {carry}, {B}, {a0}')
+            return t
+
+        group = 2 if PAIR else 1
+        for gi in range(0, len(cols), group):
+            s = (gi // group) % 2
+            members = list(range(gi, min(gi + group, len(cols))))
+            if PAIR:
+                # member m accumulates in chain m of set s
+                streams = [[(acc(s, m), cols[ci]['terms'])] for m, ci in enumerate(members)]
+            else:
+                ci = members[0]
+                streams = [[(acc(s, ch), cols[ci]['terms'][ch::NCH])] for ch in range(NCH)]
+            # interleave the multiply-adds of all streams
+            seqs = [st[0] for st in streams]
+            used = [False] * len(seqs)
+            n = 0
+            for t in range(max(len(q[1]) for q in seqs) if seqs else 0):
+                for k, (ac, terms) in enumerate(seqs):
+                    if t < len(terms):
+                        a_, b_ = terms[t]
+                        e(f'  {mad} {ac}, vcc, {a_}, {b_}, {ac if used[k] else "0"}')
+                        used[k] = True
+                        n += 1
+                        if n % 2 == 0:
+                            flush(1)
+            flush(len(pending))
+            tail = []
+            if PAIR:
+                for m, ci in enumerate(members):
+                    a_ = acc(s, m)
+                    tail += tail_of(ci, cols[ci], [(a_, acclo(s, m), used[m])])
+            else:
+                ci = members[0]
+                tail += tail_of(ci, cols[ci], [(acc(s, ch), acclo(s, ch), used[ch]) for ch in range(NCH)])
             pending = tail
         flush(len(pending))
 
