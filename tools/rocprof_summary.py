@@ -67,7 +67,7 @@ def pmc(dirs, out):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 kn = r.get("Kernel_Name", "")
-                if not kn.startswith("fthe_montprog"):
+                if not kn.startswith(("fthe_montprog", "fthe_padic")):
                     continue
                 key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                 agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
@@ -115,7 +115,7 @@ def pmc_round(tag, out):
                 acc = {}
                 for r in csv.DictReader(open(f)):
                     kn = r["Kernel_Name"]
-                    if not kn.startswith("fthe_montprog"):
+                    if not kn.startswith(("fthe_montprog", "fthe_padic")):
                         continue
                     key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                     acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
