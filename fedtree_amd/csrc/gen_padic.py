@@ -40,7 +40,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gen_montprog import _descriptor  # noqa: E402
 
 NCH = int(os.environ.get("FTHE_GEN_PADIC_CHAINS", "2"))     # accumulator chains per column (PAIR off)
-PAIR = not os.environ.get("FTHE_GEN_PADIC_NOPAIR")             # two columns side by side, one chain each
+PAIR = not os.environ.get("FTHE_GEN_PADIC_NOPAIR")             # adjacent columns side by side, one chain each
+GROUP = int(os.environ.get("FTHE_GEN_PADIC_GROUP", "2"))       # columns side by side (PAIR)
 
 
 def gen_padic(K: int, B: int, name: str) -> str:
@@ -49,8 +50,9 @@ def gen_padic(K: int, B: int, name: str) -> str:
     # ---- VGPR plan ---------------------------------------------------------
     V_TID, V_GOFF = 0, 1
     V_TMP = 8                                   # v[8:9]
-    ACC0 = 10                                   # 2 column sets x NCH chains, 64-bit each
-    CARRY = ACC0 + 4 * NCH                      # v[CARRY:CARRY+1]
+    NACC = max(NCH, GROUP) if PAIR else NCH     # accumulators per column set
+    ACC0 = 10                                   # 2 column sets x NACC accumulators, 64-bit each
+    CARRY = ACC0 + 4 * NACC                     # v[CARRY:CARRY+1]
     BK = (CARRY + 2 + 1) & ~1                   # banks start even
     KB = K + (K & 1)                            # bank size (even)
     BANK = [BK + KB * i for i in range(4)]
@@ -77,11 +79,11 @@ def gen_padic(K: int, B: int, name: str) -> str:
         return f"v[{n}:{n + 1}]"
 
     def acc(s, ch):
-        n = ACC0 + 2 * (NCH * s + ch)
+        n = ACC0 + 2 * (NACC * s + ch)
         return f"v[{n}:{n + 1}]"
 
     def acclo(s, ch):
-        return f"v{ACC0 + 2 * (NCH * s + ch)}"
+        return f"v{ACC0 + 2 * (NACC * s + ch)}"
 
     carry = f"v[{CARRY}:{CARRY + 1}]"
     carrylo = f"v{CARRY}"
@@ -139,7 +141,7 @@ def gen_padic(K: int, B: int, name: str) -> str:
                 t.append(f'  {shr} {carry}, {B}, {a0}')
             return t
 
-        group = 2 if PAIR else 1
+        group = GROUP if PAIR else 1
         for gi in range(0, len(cols), group):
             s = (gi // group) % 2
             members = list(range(gi, min(gi + group, len(cols))))
@@ -189,7 +191,10 @@ def gen_padic(K: int, B: int, name: str) -> str:
         return cols
 
     # ---- Barrett: T (2K limbs) -> q3 (K limbs), r = (T - q3 P) mod b^K in place of T[0..K-1]
-    def barrett(T, q3):
+    def barrett(T, q3, rout=None):
+        """q3 = the truncated-Barrett quotient of T by P, r = (T - q3 P) mod b^K into rout (default:
+        in place of T[0..K-1]; rout may not alias q3)"""
+        rout = rout or T[:K]
         q1 = T[K - 1:2 * K]                      # K + 1 limbs
         cols = []
         for c in range(K - 1, 2 * K + 1):
@@ -208,7 +213,7 @@ def gen_padic(K: int, B: int, name: str) -> str:
                 j = c - i
                 if 0 <= j < K:
                     terms.append((q3[i], NP(j)))
-            cols.append({'terms': terms, 'out': T[c], 'last': False})
+            cols.append({'terms': terms, 'out': rout[c], 'last': False})
         cols[-1]['nocarry'] = True
         columns(cols, signed=True)
 
@@ -345,10 +350,8 @@ def gen_padic(K: int, B: int, name: str) -> str:
     # LOADP slot: plain X -> T -> (q3, r) -> x0 = r, x1 = q3
     e('.Lloadp:')
     load_limbs(TT)
-    barrett(TT, X0)                              # q3 -> bank 0, r -> bank 1
-    move_digit(Y0, X0)
-    move_digit(X0, X1)
-    move_digit(X1, Y0)
+    barrett(TT, Y0, X0)                          # q3 -> bank 2, r -> bank 0 (x0)
+    move_digit(X1, Y0)                           # x1 = q3
     e('  s_branch .Lprog')
 
     # STOREP slot: x0 + x1 P = x0 - (-x1)(... ) with -P in SGPRs: (-x1_i)(-P_j)
@@ -367,17 +370,14 @@ def gen_padic(K: int, B: int, name: str) -> str:
     e('.Lend:')
     e('  s_endpgm')
 
-    # shared reduction of SQR and MUL: T (banks 1, 3) -> q3 = u1 (bank 0), r = u0 (bank 1);
-    # V += u1; V -> q3' (bank 2), r' (V[0..K-1]); x0 <- u0, x1 <- r'
+    # shared reduction of SQR and MUL: T (banks 1, 3) -> q3 = u1 (bank 2), r = u0 into bank 0;
+    # V += u1; V -> q3' (bank 3), r' into bank 1: the digits land where the next op reads them
     e('.Lreduce:')
-    barrett(TT, X0)
+    barrett(TT, Y0, X0)                          # u1 -> bank 2 (y0 / unused), u0 -> bank 0 (x0 is dead)
     e('.Lreduce_v:')
     for i in range(K):
-        e(f'  v_add_u32_e32 {VV[i]}, {VV[i]}, {X0[i]}')
-    barrett(VV, Y0)
-    e('.Lreduce_mv:')
-    move_digit(X0, X1)
-    move_digit(X1, VV[:K])
+        e(f'  v_add_u32_e32 {VV[i]}, {VV[i]}, {Y0[i]}')
+    barrett(VV, Y1, X1)                          # q3' -> bank 3 (T's top, consumed), r' -> bank 1 (x1)
     e('  s_setpc_b64 s[12:13]')
 
     e(f'.Lfunc_end_{name}:')
