@@ -48,8 +48,7 @@ def gen_padic(K: int, B: int, name: str) -> str:
     MASK = (1 << B) - 1
     assert 2 <= NCH <= 4
     # ---- VGPR plan ---------------------------------------------------------
-    V_TID, V_GOFF = 0, 1
-    V_TMP = 8                                   # v[8:9]
+    V_TID, V_GOFF = 0, 1                        # v2..v9 unused
     NACC = max(NCH, GROUP) if PAIR else NCH     # accumulators per column set
     ACC0 = 10                                   # 2 column sets x NACC accumulators, 64-bit each
     CARRY = ACC0 + 4 * NACC                     # v[CARRY:CARRY+1]
@@ -86,7 +85,6 @@ def gen_padic(K: int, B: int, name: str) -> str:
         return f"v{ACC0 + 2 * (NACC * s + ch)}"
 
     carry = f"v[{CARRY}:{CARRY + 1}]"
-    carrylo = f"v{CARRY}"
     NP = lambda j: f"s{SNP + j}"                # -P_j
     MU = lambda j: f"s{SMU + j}"
 
