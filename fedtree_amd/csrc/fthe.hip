@@ -40,12 +40,14 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 5;
+constexpr int MAX_VARIANTS = 6;
 // s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency);
-// kPadicS: the P-adic exponentiation kernel mod P^2 (gen_padic.py, digits of 37 limbs), which runs
-// on the s74 slots (its "S" here only names the variant)
-constexpr int kPadicS = 1037, kPadicK = 37;
-const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4}, {kPadicS, 28, 1}};
+// 1000 + K: the P-adic exponentiation kernels mod P^2 (gen_padic.py, digits of K limbs, slots of 2K
+// limbs; the "S" here only names the variant): K = 37 runs on the s74 slots of Paillier-2048,
+// K = 19 on slots of its own (38 limbs) for Paillier-1024
+constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19;
+const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4},
+                                       {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}};
 constexpr Shape kLatShape{80, 27, 4};
 
 int variant_index(int S) {
@@ -289,6 +291,7 @@ struct fthe_key {
     // P-adic exponentiation kernel mod p^2, q^2 (gen_padic.py): the CRT encrypt's y^P and the
     // decrypt's c^(P-1); s74 programs before / after it convert to and from Montgomery form
     bool padic = false;
+    bool padic_own_slots = false;   // the P-adic kernel's slots are not the CRT region's (K = 19)
     DevMod mpA, mqA;
     int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1, cl_nRp = -1, cl_nRq = -1;
     int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
@@ -465,7 +468,7 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         if (!blob) return FTHE_ERR_HIP;
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
-        if (kVariants[i].S == kPadicS) snprintf(name, sizeof name, "fthe_padic_k%d", kPadicK);
+        if (kVariants[i].S > 1000) snprintf(name, sizeof name, "fthe_padic_k%d", kVariants[i].S - 1000);
         else snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
         HIPOK(hipFuncGetAttribute(&c->static_lds[i], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, c->fn[i]));
@@ -580,26 +583,32 @@ static int upload_mod(DevMod &d, const mpz_t N, Shape sh) {
     return FTHE_OK;
 }
 
-// P-adic kernel constants for P (gen_padic.py): -P in K radix-2^28 limbs (int32), 3 zero words,
-// mu = floor(2^(56 K) / P) in K + 1 limbs.  Runs on the s74 slots: m is P^2 on that shape (slot
-// strides, roofline units).  Needs b^(K-1) <= P and 5P, 50P < b^K: P of 1009..1030 bits.
-static bool padic_ok(const mpz_t P, Shape sh) {
+// P-adic kernel constants for P (gen_padic.py): -P in K radix-2^28 limbs (int32), zero words up to
+// a multiple of 4 SGPRs, mu = floor(2^(56 K) / P) in K + 1 limbs; m is P^2 on the kernel's slot
+// shape (2K limbs: slot strides, roofline units).  The digit size K for the CRT half shape sh:
+//   K = 37 on the s74 slots (Paillier-2048): b^36 <= P and 50 P < b^37 -> P of 1009..1030 bits;
+//   K = 19 on 38-limb slots of its own (Paillier-1024, sh = s37): P of 505..516 bits, which also
+//     keeps its < 6 P^2 results within the 37 limbs of the s37 slots they are copied back to.
+// 0: no P-adic kernel for this P.
+static int padic_digits(const mpz_t P, Shape sh) {
+    if (getenv("FTHE_NO_PADIC") || sh.B != 28 || sh.lanes != 1) return 0;
     const size_t b = mpz_sizeinbase(P, 2);
-    return sh.S == 2 * kPadicK && sh.B == 28 && sh.lanes == 1 && b >= 1009 && b <= 1030 &&
-           !getenv("FTHE_NO_PADIC");
+    if (sh.S == 2 * kPadicK && b >= 1009 && b <= 1030) return kPadicK;
+    if (sh.S == 37 && b >= 505 && b <= 516) return kPadicSmallK;
+    return 0;
 }
-static int upload_padic(DevMod &d, const mpz_t P, Shape sh) {
+static int upload_padic(DevMod &d, const mpz_t P, int K) {
     Mpz P2; mpz_mul(P2, P, P);
-    d.m.init(P2, sh);
-    const int K = kPadicK;
-    std::vector<uint32_t> w(2 * K + 4, 0u), l = to_limbs(P, K, 28);
+    d.m.init(P2, Shape{2 * K, 28, 1});
+    const int pad = ((20 + K + 3) & ~3) - 20 - K;          // gen_padic.py: mu from an aligned SGPR
+    std::vector<uint32_t> w((size_t)2 * K + 1 + pad, 0u), l = to_limbs(P, K, 28);
     for (int j = 0; j < K; j++) w[j] = (uint32_t)(-(int32_t)l[j]);
     Mpz mu; mpz_set_ui(mu, 1); mpz_mul_2exp(mu, mu, 56 * K); mpz_fdiv_q(mu, mu, P);
     std::vector<uint32_t> ml = to_limbs(mu, K + 1, 28);
-    std::copy(ml.begin(), ml.end(), w.begin() + K + 3);
+    std::copy(ml.begin(), ml.end(), w.begin() + K + pad);
     if (hipMalloc(&d.d_ctx, w.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(d.d_ctx, w.data(), w.size() * 4, hipMemcpyHostToDevice));
-    d.kernel_S = kPadicS;
+    d.kernel_S = 1000 + K;
     return FTHE_OK;
 }
 // Algorithmic 32-bit MACs of a P-adic program (SURVEY 8(d) units, the executed algorithm): s = words
@@ -615,8 +624,8 @@ static double padic_alg(const Prog &p, const mpz_t P) {
 // as emitted by gen_padic.py: a Barrett is K(K+1)/2 + 2K + 1 (q2 columns K-1..2K) + K(K+1)/2 + K
 // (r columns 0..K-1, one init MAD each); squaring K^2 + K(K+1)/2 + 2 Barretts, product 3 K^2 +
 // 2 Barretts, LOADP one Barrett, STOREP K^2 + K (5,108 / 7,143 / 1,518 / 1,406 at K = 37).
-static double padic_exec(const Prog &p) {
-    const double K = kPadicK;
+static double padic_exec(const Prog &p, int Kd) {
+    const double K = Kd;
     const double bar = K * (K + 1) + 3 * K + 1;
     const double sq = K * K + K * (K + 1) / 2 + 2 * bar, mul = 3 * K * K + 2 * bar;
     return p.squarings * sq + (p.montmuls - p.squarings) * mul + bar + K * K + K;
@@ -779,10 +788,12 @@ static int key_finish(fthe_key *k) {
             // P-adic stage B (P of 1009..1030 bits: Paillier-2048): y^P mod P^2 on the P-adic kernel
             // (1.4x the products/s of the Montgomery s74 program), then (1 + m n) y^P and the CRT tail
             // on s74 after one product into Montgomery form.  FTHE_NO_PADIC=1: the s74 programs above.
-            k->padic = padic_ok(k->p, sh) && padic_ok(k->q, sh);
+            const int Kd = padic_digits(k->p, sh);
+            k->padic = Kd && padic_digits(k->q, sh) == Kd;
+            k->padic_own_slots = k->padic && 2 * Kd != sh.S;      // Paillier-1024: 38-limb slots of its own
             if (k->padic) {
-                if ((rc = upload_padic(k->mpA, k->p, sh))) return rc;
-                if ((rc = upload_padic(k->mqA, k->q, sh))) return rc;
+                if ((rc = upload_padic(k->mpA, k->p, Kd))) return rc;
+                if ((rc = upload_padic(k->mqA, k->q, Kd))) return rc;
                 for (int side = 0; side < 2; side++) {
                     const Mpz &P = side ? k->q : k->p;
                     Prog a;                                          // P-adic kernel
@@ -791,7 +802,7 @@ static int key_finish(fthe_key *k) {
                     a.storep(SL_SAVED); a.end();
                     fthe_key::PH ha = k->add_prog(a);
                     ha.alg = padic_alg(a, P);
-                    ha.exec = padic_exec(a);
+                    ha.exec = padic_exec(a, Kd);
                     (side ? k->prP_enc_q : k->prP_enc_p) = ha;
                     Prog e;                                          // s74
                     e.loadx(SL_SAVED); e.mul(side ? SL_C2 : SL_C0);  // y^P R
@@ -870,7 +881,7 @@ static int key_finish(fthe_key *k) {
             a.loadp(SL_SAVED); a.pow(Pm1, SL_TAB, SL_SQ, k->w_dec); a.storep(SL_SAVED); a.end();
             fthe_key::PH ha = k->add_prog(a);
             ha.alg = padic_alg(a, side ? k->q : k->p);
-            ha.exec = padic_exec(a);
+            ha.exec = padic_exec(a, k->mpA.kernel_S - 1000);
             (side ? k->prP_dec_q : k->prP_dec_p) = ha;
             Prog t;
             t.loadx(SL_SAVED); t.mul(side ? SL_C2 : SL_C0); t.mul(SL_T5);   // (X R) * 1 R^-1: X mod P^2 < 2 P^2
@@ -1278,18 +1289,43 @@ struct Launch {
 
 // CRT stage B of the encrypt (side 0: p, 1: q; nt: the p program without the CRT tail) and the
 // decrypt's c^(P-1) mod P^2: P-adic exponentiation + s74 programs when the key has them.
-int enc_stage_b(Launch &L, const fthe_key *k, int side, bool nt = false) {
+// The P-adic launch itself: on L's slots, or (padic_own_slots, Paillier-1024) on the region of pa
+// with the input slot copied in and SAVED copied back (k_copy_limbs between the slot shapes).
+static int padic_launch(Launch &L, Launch *pa, const fthe_key *k, const fthe_key::PH &ph, const DevMod &mA, int in) {
+    if (!k->padic_own_slots) return L.prog(ph, mA);
+    Launch &A = *pa;
+    A.live = L.live;
+    hipStream_t st = L.st ? L.st : L.c->stream;
+    hipLaunchKernelGGL(k_copy_limbs, L.grid(), dim3(256), 0, st, L.slot(in), L.S, A.slot(in), A.S, L.L);
+    if (int rc = A.prog(ph, mA)) return rc;
+    L.mm += A.mm; A.mm = 0;
+    hipLaunchKernelGGL(k_copy_limbs, L.grid(), dim3(256), 0, st, A.slot(SL_SAVED), A.S, L.slot(SL_SAVED), L.S, L.L);
+    return FTHE_OK;
+}
+static bool padic_here(const fthe_key *k, const Launch *pa) { return k->padic && (!k->padic_own_slots || pa); }
+int enc_stage_b(Launch &L, const fthe_key *k, int side, bool nt = false, Launch *pa = nullptr) {
     const DevMod &m2 = side ? k->mq2 : k->mp2;
-    if (!k->padic) return L.prog(side ? k->pr_enc_q : (nt ? k->pr_enc_p_nt : k->pr_enc_p), m2);
-    if (int rc = L.prog(side ? k->prP_enc_q : k->prP_enc_p, side ? k->mqA : k->mpA)) return rc;
+    if (!padic_here(k, pa)) return L.prog(side ? k->pr_enc_q : (nt ? k->pr_enc_p_nt : k->pr_enc_p), m2);
+    if (int rc = padic_launch(L, pa, k, side ? k->prP_enc_q : k->prP_enc_p, side ? k->mqA : k->mpA,
+                              side ? SL_T4 : SL_T3)) return rc;
     return L.prog(side ? k->prP_encB_q : (nt ? k->prP_encB_p_nt : k->prP_encB_p), m2);
 }
-int dec_pow(Launch &L, const fthe_key *k, int side) {
+int dec_pow(Launch &L, const fthe_key *k, int side, Launch *pa = nullptr) {
     const DevMod &m2 = side ? k->mq2 : k->mp2;
-    if (!k->padic) return L.prog(side ? k->pr_dec_q : k->pr_dec_p, m2);
+    if (!padic_here(k, pa)) return L.prog(side ? k->pr_dec_q : k->pr_dec_p, m2);
     if (int rc = L.prog(side ? k->prP_dec_pre_q : k->prP_dec_pre_p, m2)) return rc;
-    if (int rc = L.prog(side ? k->prP_dec_q : k->prP_dec_p, side ? k->mqA : k->mpA)) return rc;
+    if (int rc = padic_launch(L, pa, k, side ? k->prP_dec_q : k->prP_dec_p, side ? k->mqA : k->mpA, SL_SAVED))
+        return rc;
     return L.prog(side ? k->prP_dec_post_q : k->prP_dec_post_p, m2);
+}
+// The P-adic region of a call on a key with padic_own_slots (c->slots1, free while stage B runs).
+static int padic_region(fthe_ctx *c, const fthe_key *k, const Launch &Lc, Launch &pa) {
+    pa = Lc;
+    if (!k->padic_own_slots) return FTHE_OK;
+    pa.S = 2 * (k->mpA.kernel_S - 1000);
+    if (int rc = c->slots1.ensure((size_t)nslots_for(k) * pa.S * Lc.L * 4)) return rc;
+    pa.base = c->slots1.p;
+    return FTHE_OK;
 }
 
 int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nslots, Shape sh,
@@ -1550,14 +1586,17 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         Lp4.fill(SL_C0, k->cl_R2p); Lp4.fill(SL_C1, k->cl_nRp);
         Lq4.fill(SL_C2, k->cl_R2q); Lq4.fill(SL_C3, k->cl_nRq);
     }
+    Launch Lpa;                        // the P-adic kernel's own slots (Paillier-1024; else Lc's)
+    if (crt && (rc = padic_region(c, k, Lc, Lpa))) return rc;
     if (direct_y) {
         Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
         Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_nRq);
         Lc.fill(SL_T1, k->c_qinvRp2);
     } else if (crt) {
         L1.S = k->sp1.S; L1.B = k->sp1.B;
-        if ((rc = c->slots1.ensure((size_t)nslots_for(k) * L1.S * L * 4))) return rc;
+        if ((rc = c->slots1.ensure((size_t)nslots_for(k) * std::max(L1.S, Lpa.S) * L * 4))) return rc;
         L1.base = c->slots1.p;
+        if (k->padic_own_slots) Lpa.base = c->slots1.p;
         L1.fill(SL_C0, k->c1_R2p); L1.fill(SL_C1, k->c1_R3p);
         L1.fill(SL_C2, k->c1_R2q); L1.fill(SL_C3, k->c1_R3q);
         L1.fill(SL_T5, k->c1_one);
@@ -1632,10 +1671,10 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                 if (pipe && (rc = pipe->after(off, cnt))) return rc;
                 continue;
             }
-            if ((rc = enc_stage_b(Lc, k, 1))) return rc;
+            if ((rc = enc_stage_b(Lc, k, 1, false, &Lpa))) return rc;
             hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
                                k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = enc_stage_b(Lc, k, 0))) return rc;                 // ends with h = (cp - cq) q^-2 in T2
+            if ((rc = enc_stage_b(Lc, k, 0, false, &Lpa))) return rc;                 // ends with h = (cp - cq) q^-2 in T2
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
                         k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
@@ -1661,10 +1700,10 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                                Lc.slot(SL_T3), S, L);
             hipLaunchKernelGGL(k_copy_limbs, Lc.grid(), dim3(256), 0, c->stream, L1.slot(SL_OUTQ), L1.S,
                                Lc.slot(SL_T4), S, L);
-            if ((rc = enc_stage_b(Lc, k, 1))) return rc;
+            if ((rc = enc_stage_b(Lc, k, 1, false, &Lpa))) return rc;
             hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
                                k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-            if ((rc = enc_stage_b(Lc, k, 0))) return rc;                 // ends with h = (cp - cq) q^-2 in T2
+            if ((rc = enc_stage_b(Lc, k, 0, false, &Lpa))) return rc;                 // ends with h = (cp - cq) q^-2 in T2
             hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
@@ -2597,6 +2636,8 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
         Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_R3q); Lq.fill(SL_T5, k->c_one);
     }
+    Launch Lpa;                            // the P-adic kernel's own slots (Paillier-1024; else Lc's)
+    if (!quad && (rc = padic_region(c, k, Lc, Lpa))) return rc;
     Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p);
     Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_R3q);
     Lc.fill(SL_T5, k->c_one);
@@ -2639,7 +2680,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
                 if ((rc = dec_pow(Lq, k, 1))) return rc;
                 HIPOK(hipEventRecord(c->ev_join, c->side));
             }
-            if ((rc = dec_pow(Lc, k, 0))) return rc;
+            if ((rc = dec_pow(Lc, k, 0, &Lpa))) return rc;
         }
         if (short_pt) {
             // plaintext < p: m = m_p = L_p(c^(p-1) mod p^2) h_p mod p, the q half and the CRT skipped
@@ -2658,7 +2699,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         }
         if (split) {
             HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
-        } else if (!quad && (rc = dec_pow(Lc, k, 1))) {
+        } else if (!quad && (rc = dec_pow(Lc, k, 1, &Lpa))) {
             return rc;
         }
         hipLaunchKernelGGL(k_dec_lfunc, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTP), k->cst(k->c_p2), S,

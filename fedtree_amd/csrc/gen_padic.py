@@ -30,8 +30,9 @@ Ops (uint32 pairs from the program buffer; the host's Prog of bn_host.hpp):
    22 LOADP  slot   digits <- plain X of the slot (2K limbs, X < 50 P^2): one Barrett
    23 STOREP slot   slot <- x0 + x1 P as 2K normalised limbs (< 6 P^2, not reduced mod P^2)
 
-Kernel arguments: those of gen_montprog.py; ctx = [-P limbs (K, int32), 3 zero words, mu limbs (K+1)]
-with mu = floor(2^(56 K) / P).
+Kernel arguments: those of gen_montprog.py; ctx = [-P limbs (K, int32), zero words up to SGPR 20 + K
+rounded up to a multiple of 4, mu limbs (K+1)] with mu = floor(2^(56 K) / P).  K = 37 (Paillier-2048,
+P of 1009..1030 bits) and K = 19 (Paillier-1024, P of 505..516 bits).
 """
 import os
 import sys
@@ -63,7 +64,7 @@ def gen_padic(K: int, B: int, name: str) -> str:
     # s11 slot stride, s[12:13] return address, s[14:15] op/arg, s[16:17] addr, s19 counter,
     # s[2:3] call target (after the prologue); -P limbs from s20, mu limbs from s20 + K + 3
     SNP = 20
-    SMU = SNP + K + 3
+    SMU = (SNP + K + 3) & ~3                    # mu from a 4-aligned SGPR (s_load_dwordx4+ alignment)
     NSGPR = SMU + K + 1
     assert SMU % 4 == 0 and NSGPR <= 102, (SMU, NSGPR)
 

@@ -16,11 +16,11 @@ pytestmark = pytest.mark.gpu
 SEED = 20261016
 
 
-@pytest.fixture(scope="module")
-def keys():
+@pytest.fixture(scope="module", params=[2048, 1024])
+def keys(request):
     from fedtree_amd.paillier import Device, Paillier
     dev = Device(0)
-    pa = Paillier(dev).keygen(2048, seed=SEED)
+    pa = Paillier(dev).keygen(request.param, seed=SEED)
     os.environ["FTHE_NO_PADIC"] = "1"
     try:
         pm = Paillier.from_primes(pa.p, pa.q, dev)
@@ -80,9 +80,12 @@ def test_padic_launches_run(keys):
     vals = [ctypes.c_double() for _ in range(7)]
     assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
     ms, nl = ctypes.c_double(), ctypes.c_double()
-    assert lib.fthe_prof_variant(dev.ctx, 1037, ctypes.byref(ms), ctypes.byref(nl)) == 0
+    big = pa.modulus.bit_length() > 1100
+    assert lib.fthe_prof_variant(dev.ctx, 1037 if big else 1019, ctypes.byref(ms), ctypes.byref(nl)) == 0
     lib.fthe_prof_enable(dev.ctx, 0)
     assert nl.value == 2 and ms.value > 0                 # y_p^p and y_q^q, one launch each
-    # v_mad per lane: 1,024 squarings x 5,108 + ~180 products x 7,143 + LOADP / STOREP, per prime
+    # v_mad per lane and prime: 1,024 squarings x 5,108 + ~180 products x 7,143 + LOADP / STOREP at
+    # K = 37; 512 x 1,427 + ~100 x 1,959 + ... at K = 19
     per_lane = x.value / (2 * 70000)
-    assert 6.0e6 < per_lane < 7.0e6, per_lane
+    lo, hi = (6.0e6, 7.0e6) if big else (0.85e6, 1.05e6)
+    assert lo < per_lane < hi, per_lane

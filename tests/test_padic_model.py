@@ -11,17 +11,20 @@ sys.path.insert(0, os.path.join(ROOT, "fedtree_amd", "csrc"))
 
 import padic_model as pm  # noqa: E402
 
+import pytest  # noqa: E402
+
 K = 37
 
 
-def _key(rng, bits):
-    return pm.PadicKey(rng.getrandbits(bits) | (1 << (bits - 1)) | 1, K)
+def _key(rng, bits, k=K):
+    return pm.PadicKey(rng.getrandbits(bits) | (1 << (bits - 1)) | 1, k)
 
 
 def test_model_products_at_digit_bounds():
     rng = random.Random(11)
-    for bits in (1009, 1024, 1030):
-        key = _key(rng, bits)
+    for k, bits in ((37, 1009), (37, 1024), (37, 1030), (19, 505), (19, 512), (19, 516)):
+        key = _key(rng, bits, k)
+        K = k
         P, P2 = key.P, key.P * key.P
         hi = pm.limbs(5 * P - 1, K)
         for a0, a1, b0, b1 in ((hi, hi, hi, hi),
@@ -38,12 +41,13 @@ def test_model_products_at_digit_bounds():
             pm.check_digit(key, z1)
 
 
-def test_generated_assembly_on_emulator():
+@pytest.mark.parametrize("K,bits", [(37, 1024), (19, 512)])
+def test_generated_assembly_on_emulator(K, bits):
     from asm_emu import Emu, M32
     from gen_padic import gen_padic
-    asm = gen_padic(K, 28, "fthe_padic_k37")
+    asm = gen_padic(K, 28, f"fthe_padic_k{K}")
     rng = random.Random(5)
-    key = _key(rng, 1024)
+    key = _key(rng, bits, K)
     P, P2 = key.P, key.P * key.P
     S, L = 2 * K, 256
     KA, CTX, PROG, SLOTS = 0x100, 0x1000, 0x2000, 0x100000
@@ -53,7 +57,8 @@ def test_generated_assembly_on_emulator():
     em = Emu(asm)
     for i, v in enumerate([SLOTS, 0, PROG, 0, CTX, 0, L * 4, S * L * 4, L, 0]):
         em.mem[KA + 4 * i] = v
-    for i, w in enumerate([(-x) & M32 for x in pm.limbs(P, K)] + [0, 0, 0] + key.mu):
+    pad = ((20 + K + 3) & ~3) - 20 - K                          # zero words before mu (gen_padic.py)
+    for i, w in enumerate([(-x) & M32 for x in pm.limbs(P, K)] + [0] * pad + key.mu):
         em.mem[CTX + 4 * i] = w
     for i, w in enumerate(prog):
         em.mem[PROG + 4 * i] = w
@@ -62,7 +67,7 @@ def test_generated_assembly_on_emulator():
             em.mem[SLOTS + slot * S * L * 4 + k * L * 4] = limb
     em.s[0], em.s[1], em.s[2] = KA, 0, 0
     em.v[0] = 0
-    em.run("fthe_padic_k37")
+    em.run(f"fthe_padic_k{K}")
     rd = lambda slot: [em.mem.get(SLOTS + slot * S * L * 4 + k * L * 4, 0) for k in range(S)]
     x0, x1 = pm.loadp(key, X)
     assert rd(2) == x0 + x1                                    # raw digits of LOADP, as the model's
