@@ -383,6 +383,7 @@ struct fthe_key {
         uint32_t *d_tab[2] = {nullptr, nullptr}, *d_prog = nullptr;
         size_t off[2] = {0, 0};
         double mm = 0;
+        bool padic = false;               // tables in digit form, products on the P-adic kernel
     } xb;
     // ---- public exact fixed-base randomizer (FTHE_ENC_FIXED_BASE_EXACT, public form) ----
     // Bases hs_i = t_i^n mod n^2 published by the key holder, <t_1 .. t_nb> = Z_n^*;
@@ -1814,6 +1815,7 @@ std::function<void(const mpz_t, uint32_t *)> fb_store_limbs(const MontMod &M) {
 // canonical rows itself (STOREW).
 int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32_t *tab8, int nwin16, int ew,
              bool rows_form, uint32_t **out) {
+    const int Kd = mod.kernel_S > 1000 ? mod.kernel_S - 1000 : 0;     // P-adic: digit-form entries
     const size_t W16 = 65536;
     int rc;
     if (hipMalloc((void **)out, (size_t)nwin16 * W16 * ew * 4) != hipSuccess) return FTHE_ERR_NOMEM;
@@ -1838,8 +1840,14 @@ int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32
         const void *rows[3] = {(const uint8_t *)tab8 + (size_t)(2 * j) * 256 * eb, c->hb[0].p, dst};
         if ((rc = launch_dyn(Lc, c->io[3].p, pr.montmuls, mod, rows, rows_form ? 3 : 2))) return rc;
         if (!rows_form)
-            hipLaunchKernelGGL(k_slot_to_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
-                               Lc.slot(SL_OUTP), Lc.S, Lc.L, W16, ew, dst);
+        {
+            if (Kd)
+                hipLaunchKernelGGL(k_slot_to_digit_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
+                                   Lc.slot(SL_OUTP), Kd, ew / 2, Lc.L, W16, dst);
+            else
+                hipLaunchKernelGGL(k_slot_to_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
+                                   Lc.slot(SL_OUTP), Lc.S, Lc.L, W16, ew, dst);
+        }
     }
     HIPOK(hipStreamSynchronize(c->stream));
     return end_call(c, Lc);
@@ -2147,33 +2155,49 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
         seed_gmp_state(st, 0, 0);       // 256 bits of /dev/urandom
     }
     X.nwin = (int)((std::max(k->p.bits(), k->q.bits()) + 15) / 16);
-    X.ew = 4 * ((k->spq.S + 3) / 4);
+    // P-2048: the gathered products on the P-adic kernel, entries in its digit form (2 KB words)
+    X.padic = k->padic && !k->padic_own_slots;
+    const int Kd = X.padic ? k->mpA.kernel_S - 1000 : 0, KB = Kd + (Kd & 1);
+    X.ew = X.padic ? 2 * KB : 4 * ((k->spq.S + 3) / 4);
     X.nb = k->order_known ? 1 : 3;
     std::vector<uint32_t> progs;
     int rc = FTHE_OK;
     for (int side = 0; side < 2 && rc == FTHE_OK; side++) {
         const Mpz &P = side ? k->q : k->p;
         const DevMod &D = side ? k->mq2 : k->mp2;
+        const DevMod &A = side ? k->mqA : k->mpA;
+        // digit form of x < P^2: x mod P at words 0.., x div P at KB..
+        auto store_digits = [&P, Kd, KB](const mpz_t x, uint32_t *dst) {
+            Mpz q, r; mpz_fdiv_qr(q, r, x, P);
+            std::vector<uint32_t> a = to_limbs(r, Kd, 28), b = to_limbs(q, Kd, 28);
+            std::copy(a.begin(), a.end(), dst);
+            std::copy(b.begin(), b.end(), dst + KB);
+        };
         Mpz t[3];
         if (k->order_known) xb_pick_generator(st, P, side ? k->qm1_factors : k->pm1_factors, t[0]);
         else xb_pick_bases(st, P, t);
         std::vector<uint32_t> tab;                        // 8-bit windows, base after base
         for (int b = 0; b < X.nb; b++) {
             mpz_powm(X.gam[side][b], t[b], P, D.m.N);
-            std::vector<uint32_t> tb = fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, fb_store_limbs(D.m));
+            std::vector<uint32_t> tb = X.padic ? fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, store_digits)
+                                               : fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, fb_store_limbs(D.m));
             tab.insert(tab.end(), tb.begin(), tb.end());
         }
         uint32_t *d8 = nullptr;
         if ((rc = fb_upload(tab, &d8))) break;
-        rc = fb_widen(k, c, D, k->spq, d8, X.nb * X.nwin, X.ew, false, &X.d_tab[side]);
+        rc = fb_widen(k, c, X.padic ? A : D, k->spq, d8, X.nb * X.nwin, X.ew, false, &X.d_tab[side]);
         (void)hipFree(d8);
         if (rc) break;
         Prog e;                                           // X = prod_j entry(j, digit j), then (1 + m n) X
         e.loadgd16(0);
         for (int j = 1; j < X.nb * X.nwin; j++) e.mulgd16(j);
-        e.storex(SL_SAVED);
-        e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
-        if (side) e.storex(SL_OUTQ); else crt_tail(e);
+        if (X.padic) {
+            e.storep(SL_SAVED);                           // the rest: k->prP_encB_* on s74
+        } else {
+            e.storex(SL_SAVED);
+            e.loadx(SL_IN1); e.mul(side ? SL_C3 : SL_C1); e.addsmall(1); e.mul(SL_SAVED);
+            if (side) e.storex(SL_OUTQ); else crt_tail(e);
+        }
         e.end();
         X.off[side] = progs.size(); X.mm = std::max(X.mm, e.montmuls);
         progs.insert(progs.end(), e.w.begin(), e.w.end());
@@ -2544,6 +2568,7 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
     if (!y) rk = make_rng_key(rng_seed, 0x6578616374626173ull);
     Lc.fill(SL_C1, k->c_nRp); Lc.fill(SL_C3, k->c_nRq);
     Lc.fill(SL_T1, k->c_qinvRp2);
+    if (X.padic) { Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C2, k->c_R2q); }
     const size_t exp_bytes = (size_t)X.nwin * L * 2;
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
@@ -2568,10 +2593,12 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
         m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         const void *rp[2] = {X.d_tab[0], dig[0]};
         const void *rq[2] = {X.d_tab[1], dig[1]};
-        if ((rc = Lc.prog_raw(X.d_prog + X.off[1], X.mm, k->mq2, rq, 2))) return rc;
+        if ((rc = Lc.prog_raw(X.d_prog + X.off[1], X.mm, X.padic ? k->mqA : k->mq2, rq, 2))) return rc;
+        if (X.padic && (rc = Lc.prog(k->prP_encB_q, k->mq2))) return rc;
         hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_OUTQ), k->cst(k->c_q2),
                            k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
-        if ((rc = Lc.prog_raw(X.d_prog + X.off[0], X.mm, k->mp2, rp, 2))) return rc;
+        if ((rc = Lc.prog_raw(X.d_prog + X.off[0], X.mm, X.padic ? k->mpA : k->mp2, rp, 2))) return rc;
+        if (X.padic && (rc = Lc.prog(k->prP_encB_p, k->mp2))) return rc;
         hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->stream, Lc.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
         mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
                     k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);

@@ -24,6 +24,8 @@ column's multiply-adds so that its dependent steps do not stall the wave.
 Ops (uint32 pairs from the program buffer; the host's Prog of bn_host.hpp):
     0 END
     1 LOADX  slot   digits <- slot (raw: limbs 0..K-1 = x0, K..2K-1 = x1)
+   14 / 16 LOADXGD(16) j   digits <- fixed-base table entry (j << 8 | 16) | digit j of the lane
+   15 / 17 MULGD(16) j     X <- X * that entry (tables in digit form, the register-bank layout)
     2 STOREX slot   slot <- digits (raw)
     3 SQR    count  X <- X^2, count times
     4 MUL    slot   X <- X * (digits of slot)
@@ -262,7 +264,8 @@ def gen_padic(K: int, B: int, name: str) -> str:
     e('  s_add_u32 s6, s6, 8')
     e('  s_addc_u32 s7, s7, 0')
     e('  s_waitcnt lgkmcnt(0)')
-    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (22, '.Lloadp'), (23, '.Lstorep')):
+    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (22, '.Lloadp'), (23, '.Lstorep'),
+                      (14, '.Lloadxgd'), (15, '.Lmulgd'), (16, '.Lloadxgd16'), (17, '.Lmulgd16')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -341,10 +344,48 @@ def gen_padic(K: int, B: int, name: str) -> str:
     # MUL slot: y -> banks 2, 3; W = x0 y1 + x1 y0 (x1, y1 dead), T = x0 y0 into banks 1, 3
     e('.Lmul:')
     load_limbs(Y0 + Y1)
+    e('.Lmul_body:')
     columns(product_cols(X0, Y1, 2 * K, VV, a2=X1, b2=Y0))
     columns(product_cols(X0, Y0, 2 * K, TT))
     call('.Lreduce')
     e('  s_branch .Lprog')
+
+    # Fixed-base tables in digit form (the exact randomizer's gathered products): entry
+    # (j << W) | dig[j][g] of the table at rows[0], EW = 2 KB words laid out like the register banks
+    # (x0 limbs, pad, x1 limbs, pad), so it loads with dwordx4 straight into banks 0, 1 (LOADXGD) or
+    # 2, 3 (MULGD, then the product); rows[1] = the u8 / u16 digit array [window][L].
+    EW = 2 * KB
+    assert EW % 4 == 0 and BANK[1] == BANK[0] + KB and BANK[3] == BANK[2] + KB
+
+    def gather_entry(wide, dst0):
+        e('  s_load_dwordx2 s[16:17], s[0:1], 0x30')        # digit array
+        e('  s_lshr_b32 s14, s10, 2')                        # L
+        e('  s_mul_i32 s14, s14, s15')                       # j * L
+        if wide:
+            e('  s_lshl_b32 s14, s14, 1')                    # u16 digits
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_add_u32 s16, s16, s14')
+        e('  s_addc_u32 s17, s17, 0')
+        e(f'  v_lshrrev_b32_e32 v4, {1 if wide else 2}, v{V_GOFF}')   # g x digit size
+        e(f'  global_load_{"ushort" if wide else "ubyte"} v4, v4, s[16:17]')
+        e('  s_load_dwordx2 s[16:17], s[0:1], 0x28')        # table
+        e(f'  s_lshl_b32 s14, s15, {16 if wide else 8}')     # j << W
+        e(f'  v_mov_b32_e32 v5, {4 * EW}')
+        e('  s_waitcnt vmcnt(0) lgkmcnt(0)')
+        e('  v_or_b32_e32 v4, s14, v4')
+        e('  v_mad_u64_u32 v[2:3], vcc, v4, v5, s[16:17]')  # 64-bit entry address (tables > 4 GiB)
+        for i in range(EW // 4):
+            e(f'  global_load_dwordx4 v[{dst0 + 4 * i}:{dst0 + 4 * i + 3}], v[2:3], off offset:{16 * i}')
+        e('  s_waitcnt vmcnt(0)')
+
+    for wide in (False, True):
+        sfx = "16" if wide else ""
+        e(f'.Lloadxgd{sfx}:')
+        gather_entry(wide, BANK[0])
+        e('  s_branch .Lprog')
+        e(f'.Lmulgd{sfx}:')
+        gather_entry(wide, BANK[2])
+        e('  s_branch .Lmul_body')
 
     # LOADP slot: plain X -> T -> (q3, r) -> x0 = r, x1 = q3
     e('.Lloadp:')

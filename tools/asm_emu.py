@@ -162,12 +162,23 @@ class Emu:
                 self.s['scc'] = int(r != 0)
                 self.write(args[0], r)
                 continue
+            if op == 's_lshr_b32':
+                r = (self.read(args[1]) & M32) >> self.read(args[2])
+                self.s['scc'] = int(r != 0)
+                self.write(args[0], r)
+                continue
             if op == 's_cmp_eq_u32':
                 self.s['scc'] = int((self.read(args[0]) & M32) == (self.read(args[1]) & M32))
                 continue
             # ---- vector ----
             if op == 'v_lshlrev_b32_e32':
                 self.write(args[0], self.read(args[2]) << self.read(args[1]))
+                continue
+            if op == 'v_lshrrev_b32_e32':
+                self.write(args[0], (self.read(args[2]) & M32) >> self.read(args[1]))
+                continue
+            if op == 'v_or_b32_e32':
+                self.write(args[0], self.read(args[1]) | self.read(args[2]))
                 continue
             if op == 'v_add_u32_e32':
                 self.write(args[0], self.read(args[1]) + self.read(args[2]))
@@ -212,6 +223,22 @@ class Emu:
                 if x >> 63:
                     x -= 1 << 64
                 self.write(args[0], (x >> int(args[1])) & M64)
+                continue
+            if op in ('global_load_ubyte', 'global_load_ushort'):
+                dst, voff, sbase = args
+                addr = self.read(sbase) + (self.read(voff) & M32)
+                w = self.mem.get(addr & ~3, 0) >> (8 * (addr & 3))
+                self.write(dst, w & (0xff if op.endswith('ubyte') else 0xffff))
+                continue
+            if op == 'global_load_dwordx4':
+                # global_load_dwordx4 v[a:a+3], v[addr:addr+1], off offset:N
+                dst, vaddr = args[0], args[1]
+                rest_ = args[2].split()
+                off = int(rest_[1].split(':')[1]) if len(rest_) > 1 else 0
+                addr = self.read(vaddr) + off
+                kind, b0, n = self.reg_range(dst)
+                for i in range(n):
+                    self.v[b0 + i] = self.mem.get(addr + 4 * i, 0)
                 continue
             if op == 'global_load_dword':
                 dst, voff, sbase = args
