@@ -417,8 +417,9 @@ def run(a, world):
     lanes = 393216
     roof["algorithmic_bytes_per_launch"] = lanes * 772 // 2
     roof["window_operand_bytes_per_launch_model"] = int(lanes * (190 + 16 + 4) * 296)
-    roof["traffic_note"] = ("HBM bytes are the per-lane window-table operand reads (~190 multiplications x 296 B "
-                            "per lane per exponentiation), 2.2% of HBM bandwidth in a VALU-bound kernel")
+    roof["traffic_note"] = ("HBM bytes are the per-lane window-table traffic (~180 window multiplications reading and "
+                            "32 table stores writing 296 B per lane per exponentiation), ~300 GB/s = ~4% of HBM "
+                            "bandwidth in a VALU-bound kernel")
 
 
     secondary = {}
