@@ -1319,13 +1319,16 @@ int dec_pow(Launch &L, const fthe_key *k, int side, Launch *pa = nullptr) {
         return rc;
     return L.prog(side ? k->prP_dec_post_q : k->prP_dec_post_p, m2);
 }
-// The P-adic region of a call on a key with padic_own_slots (c->slots1, free while stage B runs).
+// The P-adic region of a call on a key with padic_own_slots: c->slots1 after the stage-A region of
+// the small-limb kernel (sp1 slots of the same key, whose constants must survive across chunks).
+static size_t padic_region_offset(const fthe_key *k, int L) { return (size_t)nslots_for(k) * k->sp1.S * L * 4; }
 static int padic_region(fthe_ctx *c, const fthe_key *k, const Launch &Lc, Launch &pa) {
     pa = Lc;
     if (!k->padic_own_slots) return FTHE_OK;
     pa.S = 2 * (k->mpA.kernel_S - 1000);
-    if (int rc = c->slots1.ensure((size_t)nslots_for(k) * pa.S * Lc.L * 4)) return rc;
-    pa.base = c->slots1.p;
+    const size_t off = padic_region_offset(k, Lc.L);
+    if (int rc = c->slots1.ensure(off + (size_t)nslots_for(k) * pa.S * Lc.L * 4)) return rc;
+    pa.base = (uint8_t *)c->slots1.p + off;
     return FTHE_OK;
 }
 
@@ -1595,9 +1598,12 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         Lc.fill(SL_T1, k->c_qinvRp2);
     } else if (crt) {
         L1.S = k->sp1.S; L1.B = k->sp1.B;
-        if ((rc = c->slots1.ensure((size_t)nslots_for(k) * std::max(L1.S, Lpa.S) * L * 4))) return rc;
-        L1.base = c->slots1.p;
-        if (k->padic_own_slots) Lpa.base = c->slots1.p;
+        if ((rc = c->slots1.ensure(std::max((size_t)nslots_for(k) * L1.S * L * 4,
+                                            k->padic_own_slots ? padic_region_offset(k, L) +
+                                                (size_t)nslots_for(k) * Lpa.S * L * 4 : (size_t)0))))
+            return rc;
+        L1.base = c->slots1.p;                 // stage A; the P-adic region (if any) follows it
+        if (k->padic_own_slots) Lpa.base = (uint8_t *)c->slots1.p + padic_region_offset(k, L);
         L1.fill(SL_C0, k->c1_R2p); L1.fill(SL_C1, k->c1_R3p);
         L1.fill(SL_C2, k->c1_R2q); L1.fill(SL_C3, k->c1_R3q);
         L1.fill(SL_T5, k->c1_one);

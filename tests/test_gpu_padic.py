@@ -89,3 +89,25 @@ def test_padic_launches_run(keys):
     per_lane = x.value / (2 * 70000)
     lo, hi = (6.0e6, 7.0e6) if big else (0.85e6, 1.05e6)
     assert lo < per_lane < hi, per_lane
+
+
+def test_multi_chunk_injected_r_paillier1024(coracle):
+    """Paillier-1024 with injected r across a chunk boundary: stage A (small-limb kernel) and the K = 19
+    P-adic kernel share c->slots1 in separate regions, so the stage-A constants of the second chunk are
+    intact; sampled ciphertexts on both sides of the boundary equal the C oracle's encrypt(m, r)."""
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    pl = Paillier(dev).keygen(1024, seed=SEED + 7)
+    rng = np.random.default_rng(SEED + 7)
+    cnt = 393216 + 4096
+    n = pl.modulus
+    raw = rng.integers(0, 2**32, (cnt, pl.n_words + 2), dtype=np.uint32)
+    rs = [int.from_bytes(row.tobytes(), "little") % (n - 1) + 1 for row in raw]     # uniform-ish in [1, n)
+    rw = pyoracle.ints_to_words(rs, pl.n_words)
+    m = rng.integers(0, 2**63, cnt, dtype=np.uint64)
+    c = pl.encrypt_u64(m, r=rw)
+    pw = (max(pl.p.bit_length(), pl.q.bit_length()) + 31) // 32
+    ok = coracle.key(pyoracle.to_words(pl.p, pw), pyoracle.to_words(pl.q, pw))
+    idx = np.r_[0:32, 393216 - 32:393216 + 32, cnt - 32:cnt]
+    assert np.array_equal(c[idx], ok.encrypt_batch(m[idx], rw[idx]))
+    assert np.array_equal(pl.decrypt_u64(c), m)
