@@ -400,6 +400,10 @@ def run(a, world):
         vms, vn = ctypes.c_double(), ctypes.c_double()
         lib.fthe_prof_variant(dev.ctx, 1037, ctypes.byref(vms), ctypes.byref(vn))
         rate = xmacs.value / (vms.value * 1e-3) if vms.value else 0.0
+        roof["unit_note"] = ("achieved/frac count the 32-bit MACs of the executed algorithm: the P-adic products need "
+                             f"{round(alg_macs / enc_rank / 1e6, 2)}e6 per encrypt, 2.1x fewer than the Montgomery CRT's "
+                             "1.98e7 (round 1), so frac falls while encrypts/s rise; padic_frac_executed_mads is the "
+                             "kernel's issue efficiency (its v_mad instructions over its launch time), DESIGN.md 3")
         roof["padic_executed_mads_per_encrypt"] = round(xmacs.value / enc_rank)
         roof["padic_frac_executed_mads"] = round(rate / PEAK_MAC_S, 4)
         roof["padic_frac_of_measured_mad_peak"] = round(rate / MEASURED_MAD_S, 4)
