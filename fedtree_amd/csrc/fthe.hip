@@ -589,7 +589,8 @@ static int upload_mod(DevMod &d, const mpz_t N, Shape sh) {
 // shape (2K limbs: slot strides, roofline units).  The digit size K for the CRT half shape sh:
 //   K = 37 on the s74 slots (Paillier-2048): b^36 <= P and 50 P < b^37 -> P of 1009..1030 bits;
 //   K = 19 on 38-limb slots of its own (Paillier-1024, sh = s37): P of 505..516 bits, which also
-//     keeps its < 6 P^2 results within the 37 limbs of the s37 slots they are copied back to.
+//     keeps its < 6 P^2 results within the 37 limbs of the s37 slots they are copied back to; the
+//     s37 shape itself takes P^2 of <= 1028 bits (kernel_shape_for_bits), so in effect 505..514.
 // 0: no P-adic kernel for this P.
 static int padic_digits(const mpz_t P, Shape sh) {
     if (getenv("FTHE_NO_PADIC") || sh.B != 28 || sh.lanes != 1) return 0;
@@ -1322,13 +1323,16 @@ int dec_pow(Launch &L, const fthe_key *k, int side, Launch *pa = nullptr) {
 // The P-adic region of a call on a key with padic_own_slots: c->slots1 after the stage-A region of
 // the small-limb kernel (sp1 slots of the same key, whose constants must survive across chunks).
 static size_t padic_region_offset(const fthe_key *k, int L) { return (size_t)nslots_for(k) * k->sp1.S * L * 4; }
-static int padic_region(fthe_ctx *c, const fthe_key *k, const Launch &Lc, Launch &pa) {
+// paq (split calls): a second region after it for the q half on the side stream.
+static int padic_region(fthe_ctx *c, const fthe_key *k, const Launch &Lc, Launch &pa, Launch *paq = nullptr) {
     pa = Lc;
+    if (paq) { *paq = Lc; paq->st = c->side; }
     if (!k->padic_own_slots) return FTHE_OK;
     pa.S = 2 * (k->mpA.kernel_S - 1000);
-    const size_t off = padic_region_offset(k, Lc.L);
-    if (int rc = c->slots1.ensure(off + (size_t)nslots_for(k) * pa.S * Lc.L * 4)) return rc;
+    const size_t off = padic_region_offset(k, Lc.L), reg = (size_t)nslots_for(k) * pa.S * Lc.L * 4;
+    if (int rc = c->slots1.ensure(off + (paq ? 2 : 1) * reg)) return rc;
     pa.base = (uint8_t *)c->slots1.p + off;
+    if (paq) { paq->S = pa.S; paq->base = (uint8_t *)pa.base + reg; }
     return FTHE_OK;
 }
 
@@ -1590,8 +1594,8 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         Lp4.fill(SL_C0, k->cl_R2p); Lp4.fill(SL_C1, k->cl_nRp);
         Lq4.fill(SL_C2, k->cl_R2q); Lq4.fill(SL_C3, k->cl_nRq);
     }
-    Launch Lpa;                        // the P-adic kernel's own slots (Paillier-1024; else Lc's)
-    if (crt && (rc = padic_region(c, k, Lc, Lpa))) return rc;
+    Launch Lpa, Lpaq;                  // the P-adic kernel's own slots (Paillier-1024; else Lc's)
+    if (crt && (rc = padic_region(c, k, Lc, Lpa, split ? &Lpaq : nullptr))) return rc;
     if (direct_y) {
         Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_nRp);
         Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_nRq);
@@ -1664,9 +1668,9 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
                 pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lq.slot(SL_T4), S, L, Lc.B);
                 HIPOK(hipEventRecord(c->ev_fork, c->stream));
                 HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-                if ((rc = enc_stage_b(Lq, k, 1))) return rc;
+                if ((rc = enc_stage_b(Lq, k, 1, false, &Lpaq))) return rc;
                 HIPOK(hipEventRecord(c->ev_join, c->side));
-                if ((rc = enc_stage_b(Lc, k, 0, true))) return rc;
+                if ((rc = enc_stage_b(Lc, k, 0, true, &Lpa))) return rc;
                 HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
                 hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->stream, Lq.slot(SL_OUTQ),
                                    k->cst(k->c_q2), k->cst(k->c_2p2), Lc.slot(SL_T0), S, L, Lc.B);
@@ -2669,8 +2673,8 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
         HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
         Lq.fill(SL_C2, k->c_R2q); Lq.fill(SL_C3, k->c_R3q); Lq.fill(SL_T5, k->c_one);
     }
-    Launch Lpa;                            // the P-adic kernel's own slots (Paillier-1024; else Lc's)
-    if (!quad && (rc = padic_region(c, k, Lc, Lpa))) return rc;
+    Launch Lpa, Lpaq;                      // the P-adic kernel's own slots (Paillier-1024; else Lc's)
+    if (!quad && (rc = padic_region(c, k, Lc, Lpa, split ? &Lpaq : nullptr))) return rc;
     Lc.fill(SL_C0, k->c_R2p); Lc.fill(SL_C1, k->c_R3p);
     Lc.fill(SL_C2, k->c_R2q); Lc.fill(SL_C3, k->c_R3q);
     Lc.fill(SL_T5, k->c_one);
@@ -2710,7 +2714,7 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
                 pack_rows(c->stream, src, cw, cnt, Lc.B * S, Lq.slot(SL_IN1), S, L, Lc.B);
                 HIPOK(hipEventRecord(c->ev_fork, c->stream));
                 HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-                if ((rc = dec_pow(Lq, k, 1))) return rc;
+                if ((rc = dec_pow(Lq, k, 1, &Lpaq))) return rc;
                 HIPOK(hipEventRecord(c->ev_join, c->side));
             }
             if ((rc = dec_pow(Lc, k, 0, &Lpa))) return rc;

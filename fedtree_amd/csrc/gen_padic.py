@@ -34,7 +34,8 @@ Ops (uint32 pairs from the program buffer; the host's Prog of bn_host.hpp):
 
 Kernel arguments: those of gen_montprog.py; ctx = [-P limbs (K, int32), zero words up to SGPR 20 + K
 rounded up to a multiple of 4, mu limbs (K+1)] with mu = floor(2^(56 K) / P).  K = 37 (Paillier-2048,
-P of 1009..1030 bits) and K = 19 (Paillier-1024, P of 505..516 bits).
+P of 1009..1030 bits) and K = 19 (Paillier-1024, P of 505..516 bits; the key's
+s37 CRT shape admits 505..514).
 """
 import os
 import sys

@@ -111,3 +111,76 @@ def test_multi_chunk_injected_r_paillier1024(coracle):
     idx = np.r_[0:32, 393216 - 32:393216 + 32, cnt - 32:cnt]
     assert np.array_equal(c[idx], ok.encrypt_batch(m[idx], rw[idx]))
     assert np.array_equal(pl.decrypt_u64(c), m)
+
+
+def _padic_launches(dev, fn):
+    """fn's result and its P-adic launches per variant (profiling counters of the context)."""
+    lib = dev.lib
+    lib.fthe_prof_enable(dev.ctx, 1)
+    try:
+        out = fn()
+        vals = [ctypes.c_double() for _ in range(7)]
+        assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
+        launches = {}
+        for v in (1037, 1019):
+            ms, nl = ctypes.c_double(), ctypes.c_double()
+            assert lib.fthe_prof_variant(dev.ctx, v, ctypes.byref(ms), ctypes.byref(nl)) == 0
+            launches[v] = nl.value
+    finally:
+        lib.fthe_prof_enable(dev.ctx, 0)
+    return out, launches
+
+
+def _prime_of_bits(rng, bits):
+    """A probable prime of exactly `bits` bits (test keys only)."""
+    from test_gpu_parity import _next_prime
+    while True:
+        x = int.from_bytes(rng.bytes((bits + 7) // 8), "little") & ((1 << bits) - 1)
+        x |= (1 << (bits - 1)) | (1 << (bits - 2))
+        p = _next_prime(x)
+        if p.bit_length() == bits:
+            return p
+
+
+# Prime sizes at the edges of the P-adic digit ranges (fthe.hip padic_digits): K = 37 takes P of
+# 1009..1030 bits, K = 19 P of 505..514 bits (P of 515-516 bits puts the key's CRT halves on the s74
+# shape, kernel_shape_for_bits); one bit outside, the key runs the Montgomery programs.
+@pytest.mark.parametrize("pbits,qbits,variant", [
+    (1009, 1030, 1037), (1030, 1030, 1037), (1008, 1030, None), (1030, 1031, None),
+    (505, 514, 1019), (514, 514, 1019), (504, 514, None), (505, 515, None)])
+def test_digit_range_edges_vs_c_oracle(coracle, pbits, qbits, variant):
+    """Keys whose primes sit on (or one bit past) the P-adic kernel's range: the largest P has the
+    tightest digit bounds ([0, 5P) digits, 50 P < b^K).  Injected r at the extremes and random r are
+    bit-exact against the C oracle, decrypts (low and full) match it, device randomness and the exact
+    fixed-base randomizer decrypt back, and the P-adic kernel runs exactly when both primes are in range."""
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    rng = np.random.default_rng(pbits * 7919 + qbits)
+    p, q = _prime_of_bits(rng, pbits), _prime_of_bits(rng, qbits)
+    pl = Paillier.from_primes(p, q, dev)
+    n = pl.modulus
+    hw = (qbits + 31) // 32
+    ok = coracle.key(pyoracle.to_words(p, hw), pyoracle.to_words(q, hw))
+    cnt = 20000                                    # above the small-batch (s80) decrypt threshold
+    m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    m[:3] = [0, 1, 2**64 - 2]
+    rs = [1, 2, n - 1, n - 2] + [int.from_bytes(rng.bytes(pl.n_words * 4), "little") % (n - 1) + 1
+                                 for _ in range(cnt - 4)]
+    r = pyoracle.ints_to_words(rs, pl.n_words)
+    c, launches = _padic_launches(dev, lambda: pl.encrypt_u64(m, r=r))
+    (low, full), dl = _padic_launches(dev, lambda: pl.decrypt_u64(c, full=True))
+    cd, el = _padic_launches(dev, lambda: pl.encrypt_u64(m, seed=11))      # device randomness (direct y)
+    for got in (launches, dl, el):                 # y_p^p and y_q^q, or c^(p-1) and c^(q-1)
+        assert got == ({1037: 0, 1019: 0} if variant is None else {1037: 0, 1019: 0, variant: 2}), got
+    assert np.array_equal(low, m)
+    idx = np.r_[0:48, cnt - 16:cnt]
+    r_or = np.zeros((len(idx), 2 * hw), np.uint32)
+    r_or[:, :pl.n_words] = r[idx]
+    want_or = ok.encrypt_batch(m[idx], r_or)
+    assert not want_or[:, 2 * pl.n_words:].any()
+    assert np.array_equal(c[idx], want_or[:, :2 * pl.n_words])
+    assert np.array_equal(full[idx], ok.decrypt_batch(want_or)[:, :pl.n_words])
+    ld, fd = pl.decrypt_u64(cd, full=True)
+    assert np.array_equal(ld, m) and not fd[:, 2:].any()
+    if pbits > 1000:                               # exact fixed-base tables (digit form when P-adic)
+        assert np.array_equal(pl.decrypt_u64(pl.encrypt_u64(m, seed=12, fixed_base_exact=True)), m)
