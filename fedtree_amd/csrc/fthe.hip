@@ -40,14 +40,15 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 6;
+constexpr int MAX_VARIANTS = 7;
 // s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency);
 // 1000 + K: the P-adic exponentiation kernels mod P^2 (gen_padic.py, digits of K limbs, slots of 2K
 // limbs; the "S" here only names the variant): K = 37 runs on the s74 slots of Paillier-2048,
-// K = 19 on slots of its own (38 limbs) for Paillier-1024
-constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19;
+// K = 19 on slots of its own (38 limbs) for Paillier-1024;
+// 2000 + 76: the n-adic four-lane kernel (gen_nadic.py, base-n digits of 76 limbs) on the s152 slots
+constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19, kNadicS = 2076;
 const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4},
-                                       {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}};
+                                       {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}, {kNadicS, 27, 4}};
 constexpr Shape kLatShape{80, 27, 4};
 
 int variant_index(int S) {
@@ -293,6 +294,10 @@ struct fthe_key {
     bool padic = false;
     bool padic_own_slots = false;   // the P-adic kernel's slots are not the CRT region's (K = 19)
     DevMod mpA, mqA;
+    // n-adic four-lane kernel (gen_nadic.py): the public-key encrypt's r^n mod n^2 on base-n digits
+    bool nadic = false;
+    DevMod mnA;                     // m: n^2 on the s152 slot shape; ctx: n on 76 limbs of 27 bits
+    int c_n76 = -1;                 // n in 76 limbs (the output c = x0 + x1 n)
     int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1, cl_nRp = -1, cl_nRq = -1;
     int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
     int kp = 0, kq = 0;             // limbs of p, q
@@ -309,7 +314,7 @@ struct fthe_key {
     int pq_w = 0;
     ~fthe_key() {
         co.reset();
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA})
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA})
             if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
@@ -353,6 +358,7 @@ struct fthe_key {
     // P-adic form of stage B: the exponentiation (P-adic kernel), then the rest on s74
     PH prP_enc_p, prP_enc_q, prP_encB_p, prP_encB_q, prP_encB_p_nt;
     PH prP_dec_pre_p, prP_dec_pre_q, prP_dec_p, prP_dec_q, prP_dec_post_p, prP_dec_post_q;
+    PH prN_enc_pub;                  // n-adic form of the public-key encrypt
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
     // r^n = hs^alpha with hs = h^n mod n^2 for one random h per key: 8-bit-window
@@ -469,7 +475,8 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         if (!blob) return FTHE_ERR_HIP;
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
-        if (kVariants[i].S > 1000) snprintf(name, sizeof name, "fthe_padic_k%d", kVariants[i].S - 1000);
+        if (kVariants[i].S > 2000) snprintf(name, sizeof name, "fthe_nadic_q%d", kVariants[i].S - 2000);
+        else if (kVariants[i].S > 1000) snprintf(name, sizeof name, "fthe_padic_k%d", kVariants[i].S - 1000);
         else snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
         HIPOK(hipFuncGetAttribute(&c->static_lds[i], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, c->fn[i]));
@@ -633,6 +640,35 @@ static double padic_exec(const Prog &p, int Kd) {
     return p.squarings * sq + (p.montmuls - p.squarings) * mul + bar + K * K + K;
 }
 
+// n-adic kernel (gen_nadic.py) for the public-key encrypt: n of 2042..2050 bits on the s152 slots.
+// ctx = MontMod(n, 76 limbs of 27 bits, four lanes).ctx (n limbs, nprime, quotient-estimate doubles).
+constexpr Shape kNadicDigit{76, 27, 4};
+static bool nadic_ok(const fthe_key *k) {
+    const size_t b = mpz_sizeinbase(k->n, 2);
+    return !getenv("FTHE_NO_NADIC") && k->sn2.S == 152 && k->sn2.B == 27 && k->sn2.lanes == 4 &&
+           b >= 2042 && b <= 2050;
+}
+static int upload_nadic(DevMod &d, const mpz_t n, const mpz_t n2, Shape slots) {
+    d.m.init(n2, slots);
+    MontMod dm;
+    dm.init(n, kNadicDigit);
+    if (!dm.classical_ok()) return FTHE_ERR_UNSUPPORTED;
+    if (hipMalloc(&d.d_ctx, dm.ctx.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
+    HIPOK(hipMemcpy(d.d_ctx, dm.ctx.data(), dm.ctx.size() * 4, hipMemcpyHostToDevice));
+    d.kernel_S = kNadicS;
+    return FTHE_OK;
+}
+// Algorithmic 32-bit MACs of an n-adic program (s = words of n): a squaring is two classical products
+// mod n, 2 (s^2 + s^2) (product + quotient-digit reduction), a general product 2 s^2 + 3 s^2.
+static double nadic_alg(const Prog &p, const mpz_t n) {
+    const double s = (double)((mpz_sizeinbase(n, 2) + 31) / 32);
+    return p.squarings * 4 * s * s + (p.montmuls - p.squarings) * 5 * s * s;
+}
+// v_mad per lane of the same program in the kernel (76 steps of 4 x 19 / 5 x 19 MADs, quads of lanes)
+static double nadic_exec(const Prog &p) {
+    return p.squarings * 76.0 * 76 + (p.montmuls - p.squarings) * 76.0 * 95;
+}
+
 static int key_finish(fthe_key *k) {
     // choose kernel variants: CRT moduli (p^2, q^2, p, q) and n^2
     if (k->priv) {
@@ -665,6 +701,21 @@ static int key_finish(fthe_key *k) {
         e.storex(SL_OUTP); e.end();
         k->pr_enc_pub = k->add_prog(e);
         k->tabn_max = std::max(k->tabn_max, 1 << (k->w_pub - 1));
+        // n-adic form (n of 2048 bits): X = r as base-n digits (r, 0); X^n; X (1 + m n) with the digits
+        // (1, m) of slot C1; canonical digits -> c = x0 + x1 n by the output kernel (mul_add_out)
+        k->nadic = nadic_ok(k);
+        if (k->nadic) {
+            if ((rc = upload_nadic(k->mnA, k->n, k->n2, k->sn2))) return rc;
+            k->c_n76 = k->add_const(to_limbs(k->n, kNadicDigit.S, kNadicDigit.B));
+            Prog x;
+            x.loadx(SL_IN0); x.canon();
+            x.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
+            x.mul(SL_C1); x.canon(); x.storex(SL_OUTP); x.end();
+            fthe_key::PH h = k->add_prog(x);
+            h.alg = nadic_alg(x, k->n);
+            h.exec = nadic_exec(x);
+            k->prN_enc_pub = h;
+        }
         // add: a b R^-1 -> * R2 -> a b mod n^2 (paillier.cpp:103)
         Prog a;
         a.loadx(SL_IN0); a.mul(SL_IN1); a.mul(SL_C0); a.storex(SL_OUTP); a.end();
@@ -1719,6 +1770,15 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
                         k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+        } else if (k->nadic) {
+            // n-adic kernel: digits (r, 0) in IN0, (1, m) in C1; out = x0 + x1 n (x0, x1 < n: c < n^2)
+            const int D = kNadicDigit.S;
+            pack_rows(c->stream, rw, rwn, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+            Lc.fill(SL_C1, k->c_one_n2);
+            m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_C1) + (size_t)D * L, D, L, Lc.B);
+            if ((rc = Lc.prog(k->prN_enc_pub, k->mnA))) return rc;
+            mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTP), D, k->cst(k->c_n76), D,
+                        Lc.slot(SL_OUTP) + (size_t)D * L, D, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else {
             pack_rows(c->stream, rw, rwn, cnt, 0,
                                Lc.slot(SL_IN0), S, L, Lc.B);

@@ -26,7 +26,7 @@ def trace_csv(csvfile, out):
         lines.append(f"{name[:90]},{len(v)},{sum(v) / 1e6:.3f},{sum(v) / len(v) / 1e6:.4f}")
     lines.append("")
     for name, v in sorted(per.items()):
-        if name.startswith("fthe_montprog"):
+        if name.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic")):
             heavy = [d for d in v if d > 5e6]
             if heavy:
                 lines.append(f"{name} exponentiation launches (>5 ms): n={len(heavy)} "
@@ -67,7 +67,7 @@ def pmc(dirs, out):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 kn = r.get("Kernel_Name", "")
-                if not kn.startswith(("fthe_montprog", "fthe_padic")):
+                if not kn.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic")):
                     continue
                 key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                 agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
@@ -101,21 +101,21 @@ def pmc(dirs, out):
 
 
 def pmc_round(tag, out):
-    """Summary of tools/pmc_round.sh TAG: per workload (enc, add, kway) and montprog
+    """Summary of tools/pmc_round.sh TAG: per workload (enc, add, kway, pub) and montprog
     kernel, the mean counters of its dominant dispatches (>= 90% of the largest value: the
     full-chunk launches), HBM bytes per launch = 2*FETCH_SIZE + WRITE_SIZE
     (KiB; gfx950 FETCH_SIZE counts half of a 16-B/lane streaming read,
     MI355X_MICROARCH.md HBM section) and the launch duration from the ops kernel
     trace (add, kway) or the bench trace (enc) for the achieved GB/s."""
     res = {}
-    for w in ("enc", "add", "kway"):
+    for w in ("enc", "add", "kway", "pub"):
         per = {}
         for t in ("fetch", "write", "vb", "occ", "sq"):
             for f in glob.glob(f"gpurun_out/{tag}_pmc_{w}_{t}/**/*counter_collection.csv", recursive=True):
                 acc = {}
                 for r in csv.DictReader(open(f)):
                     kn = r["Kernel_Name"]
-                    if not kn.startswith(("fthe_montprog", "fthe_padic")):
+                    if not kn.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic")):
                         continue
                     key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                     acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
