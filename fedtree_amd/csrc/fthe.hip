@@ -298,6 +298,9 @@ struct fthe_key {
     bool nadic = false;
     DevMod mnA;                     // m: n^2 on the s152 slot shape; ctx: n on 76 limbs of 27 bits
     int c_n76 = -1;                 // n in 76 limbs (the output c = x0 + x1 n)
+    // Paillier-1024 public-key encrypt (n of 1009..1030 bits) on the P-adic kernel with P = n
+    bool padic_pub = false;
+    DevMod mnP;
     int cl_R2p = -1, cl_R3p = -1, cl_R2q = -1, cl_R3q = -1, cl_one = -1, cl_p2 = -1, cl_q2 = -1, cl_nRp = -1, cl_nRq = -1;
     int c1_R2p = -1, c1_R3p = -1, c1_R2q = -1, c1_R3q = -1, c1_one = -1;
     int kp = 0, kq = 0;             // limbs of p, q
@@ -314,7 +317,7 @@ struct fthe_key {
     int pq_w = 0;
     ~fthe_key() {
         co.reset();
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA})
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA, &mnP})
             if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
@@ -359,6 +362,7 @@ struct fthe_key {
     PH prP_enc_p, prP_enc_q, prP_encB_p, prP_encB_q, prP_encB_p_nt;
     PH prP_dec_pre_p, prP_dec_pre_q, prP_dec_p, prP_dec_q, prP_dec_post_p, prP_dec_post_q;
     PH prN_enc_pub;                  // n-adic form of the public-key encrypt
+    PH prP_enc_pub;                  // P-adic form (P = n) of the Paillier-1024 public-key encrypt
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
     // r^n = hs^alpha with hs = h^n mod n^2 for one random h per key: 8-bit-window
@@ -715,6 +719,21 @@ static int key_finish(fthe_key *k) {
             h.alg = nadic_alg(x, k->n);
             h.exec = nadic_exec(x);
             k->prN_enc_pub = h;
+        }
+        // Paillier-1024 (n of 1009..1030 bits, n^2 on the s74 slots): the P-adic kernel with P = n -- the
+        // base-n digit arithmetic needs no factorisation.  X = r -> digits (LOADP), X^n, X (1 + m n) with the
+        // raw digits (1, m) of slot C1, STOREP (< 6 n^2; the output kernel reduces it)
+        k->padic_pub = padic_digits(k->n, k->sn2) == kPadicK;
+        if (k->padic_pub) {
+            if ((rc = upload_padic(k->mnP, k->n, kPadicK))) return rc;
+            Prog x;
+            x.loadp(SL_IN0);
+            x.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
+            x.mul(SL_C1); x.storep(SL_OUTP); x.end();
+            fthe_key::PH h = k->add_prog(x);
+            h.alg = padic_alg(x, k->n);
+            h.exec = padic_exec(x, kPadicK);
+            k->prP_enc_pub = h;
         }
         // add: a b R^-1 -> * R2 -> a b mod n^2 (paillier.cpp:103)
         Prog a;
@@ -1779,6 +1798,14 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             if ((rc = Lc.prog(k->prN_enc_pub, k->mnA))) return rc;
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTP), D, k->cst(k->c_n76), D,
                         Lc.slot(SL_OUTP) + (size_t)D * L, D, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+        } else if (k->padic_pub) {
+            // P-adic kernel, P = n: plain r in IN0, raw digits (1, m) in C1; out = STOREP's < 6 n^2 mod n^2
+            const int D = kPadicK;
+            pack_rows(c->stream, rw, rwn, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
+            Lc.fill(SL_C1, k->c_one_n2);
+            m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_C1) + (size_t)D * L, D, L, Lc.B);
+            if ((rc = Lc.prog(k->prP_enc_pub, k->mnP))) return rc;
+            unpack_rows(c->stream, Lc.slot(SL_OUTP), k->cst(k->c_n2), S, L, cnt, out + off * cw, cw, Lc.B);
         } else {
             pack_rows(c->stream, rw, rwn, cnt, 0,
                                Lc.slot(SL_IN0), S, L, Lc.B);

@@ -184,3 +184,31 @@ def test_digit_range_edges_vs_c_oracle(coracle, pbits, qbits, variant):
     assert np.array_equal(ld, m) and not fd[:, 2:].any()
     if pbits > 1000:                               # exact fixed-base tables (digit form when P-adic)
         assert np.array_equal(pl.decrypt_u64(pl.encrypt_u64(m, seed=12, fixed_base_exact=True)), m)
+
+
+def test_public_encrypt_padic_paillier1024(keys):
+    """Paillier-1024 public-key encrypt (n of 1009..1030 bits) runs on the K = 37 P-adic kernel with P = n:
+    the same ciphertexts as the Montgomery s74 program for injected r at the extremes and random r, and
+    decrypts back; at Paillier-2048 the n-adic kernel serves it (tests/test_gpu_nadic.py)."""
+    dev, pa, pm = keys
+    if pa.modulus.bit_length() > 1100:
+        pytest.skip("Paillier-2048: n-adic kernel")
+    rng = np.random.default_rng(SEED + 3)
+    n = pa.modulus
+    cnt = 3000
+    rs = [1, 2, n - 1, n - 2, n + 7, 2**1024 - 1] + \
+        [int.from_bytes(rng.bytes(128), "little") % (n - 1) + 1 for _ in range(cnt - 6)]
+    m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    m[:3] = [0, 1, 2**64 - 2]
+    rw = pyoracle.ints_to_words(rs, pa.n_words)
+    ca, launches = _padic_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True))
+    assert launches == {1037: 1, 1019: 0}
+    assert np.array_equal(ca, pm.encrypt_u64(m, r=rw, public=True))
+    n2 = n * n
+    for i in (0, 1, 2, 3, 4, 5, cnt - 1):             # paillier.cpp:134-137 with g = n + 1
+        assert pyoracle.from_words(ca[i]) == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
+    assert np.array_equal(pa.decrypt_u64(ca), m)
+    ms = [0, n - 1, 2**64, 2**1000 + 3]
+    assert np.array_equal(pa.encrypt_words(ms, r=rs[:4], public=True), pm.encrypt_words(ms, r=rs[:4], public=True))
+    c = pa.encrypt_u64(m, seed=SEED, public=True)
+    assert np.array_equal(pa.decrypt_u64(c), m)
