@@ -658,10 +658,15 @@ def run(a, world):
         na = min(2 * P, 1 << 20)
         o = torch.empty((na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
         pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
-        pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
         dev.sync()
-        add_s = lib.fthe_last_kernel_ms(dev.ctx) * 1e-3
+        add_ts = []
+        for _ in range(5):                               # the median of 5 timed calls (one call: +-5%)
+            pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
+            dev.sync()
+            add_ts.append(lib.fthe_last_kernel_ms(dev.ctx) * 1e-3)
+        add_s = sorted(add_ts)[2]
         secondary["p2048_add_per_s"] = round(na / add_s)
+        secondary["p2048_add_per_s_range"] = [round(na / max(add_ts)), round(na / min(add_ts))]
         prods = lib.fthe_last_montmuls(dev.ctx) / na          # 4096-bit products per add (1: classical MULWC)
         # the add kernel's HBM side (north star): algorithmic bytes (2 rows in, 1 out, 512 B each)
         # over the live launch time, and the PMC-measured bytes of a full-chunk launch
