@@ -644,7 +644,8 @@ static double padic_exec(const Prog &p, int Kd) {
     return p.squarings * sq + (p.montmuls - p.squarings) * mul + bar + K * K + K;
 }
 
-// n-adic kernel (gen_nadic.py) for the public-key encrypt: n of 2042..2050 bits on the s152 slots.
+// n-adic kernel (gen_nadic.py) for the public-key encrypt: n of 2042..2050 bits on the s152 slots (which
+// hold n^2 of <= 4096 bits: in effect 2042..2048).
 // ctx = MontMod(n, 76 limbs of 27 bits, four lanes).ctx (n limbs, nprime, quotient-estimate doubles).
 constexpr Shape kNadicDigit{76, 27, 4};
 static bool nadic_ok(const fthe_key *k) {

@@ -32,7 +32,7 @@ a LOADX of a raw r < 2n).
 
 Kernel arguments: those of gen_montprog.py; ctx = MontMod(n, 76 x 27-bit, four lanes).ctx: n limbs,
 nprime (unused), the quotient-estimate doubles -k1, -k2, -k3, bias at words 77..84 (bn_host.hpp).
-n of 2042..2050 bits (the estimate's ignored columns; 2n below 2^2052).
+n of 2042..2050 bits (the estimate's ignored columns; 2n below 2^2052); the s152 slots of n^2 stop at 2048.
 """
 import os
 import sys

@@ -96,3 +96,40 @@ def test_chunk_boundary_and_public_only_key(keys):
     idx = np.r_[0:64, 98304 - 64:98304 + 64, cnt - 64:cnt]
     assert np.array_equal(cp[idx], pm.encrypt_u64(m[idx], r=raw[idx], public=True))
     assert np.array_equal(pa.decrypt_u64(cp), m)
+
+
+def _prime_of_bits(rng, bits):
+    from test_gpu_parity import _next_prime
+    while True:
+        x = int.from_bytes(rng.bytes((bits + 7) // 8), "little") & ((1 << bits) - 1)
+        x |= (1 << (bits - 1)) | (1 << (bits - 2))
+        p = _next_prime(x)
+        if p.bit_length() == bits:
+            return p
+
+
+# n of 2042..2048 bits runs on the n-adic kernel (the quotient estimate needs n >= 2^(27*76 - 10); n^2 of
+# more than 4096 bits has no kernel shape at all); one bit below, on the Montgomery s152 program
+@pytest.mark.parametrize("nbits,nadic", [(2042, True), (2045, True), (2041, False), (2030, False)])
+def test_modulus_range_edges(nbits, nadic):
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    rng = np.random.default_rng(nbits)
+    while True:
+        p = _prime_of_bits(rng, nbits // 2)
+        q = _prime_of_bits(rng, nbits - nbits // 2)
+        n = p * q
+        if n.bit_length() == nbits:
+            break
+    pl = Paillier.from_public(n, dev)
+    cnt = 600
+    rs = [1, n - 1] + [int.from_bytes(rng.bytes(260), "little") % (n - 1) + 1 for _ in range(cnt - 2)]
+    m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    rw = pyoracle.ints_to_words(rs, pl.n_words)
+    c, launches = _nadic_launches(dev, lambda: pl.encrypt_u64(m, r=rw))
+    assert launches == (1 if nadic else 0)
+    n2 = n * n
+    for i in (0, 1, 2, cnt - 1):                         # paillier.cpp:134-137 with g = n + 1
+        assert pyoracle.from_words(c[i]) == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
+    full = Paillier.from_primes(p, q, dev)
+    assert np.array_equal(full.decrypt_u64(c), m)
