@@ -35,6 +35,10 @@ def main():
     res = {"lib": os.environ.get("FTHE_LIB", "default")}
     res["encrypt"] = best(lambda: pl.encrypt_u64_dev(m, c, seed=1), a.n)
     res["add"] = best(lambda: pl.add_dev(c, c, o), a.n)
+    if os.environ.get("FTHE_AB_ADD2") == "1":          # distinct operand rows (the bench's add)
+        c2 = torch.empty_like(c)
+        pl.encrypt_u64_dev(m, c2, seed=2)
+        res["add_distinct"] = best(lambda: pl.add_dev(c, c2, o), a.n)
     if os.environ.get("FTHE_AB_FB", "1") == "1":
         pl.set_fixed_base(None)
         res["encrypt_fixed_base"] = best(lambda: pl.encrypt_u64_dev(m, c, seed=1, fixed_base=True), a.n)
