@@ -406,6 +406,7 @@ struct fthe_key {
     };
     struct PublicBase {
         bool ready = false, rows = false;
+        bool nadic = false;               // digit-form entries, products on the n-adic kernel (P-2048)
         int nb = 0, ew = 0;               // bases, words per table entry
         int nwin[3] = {0, 0, 0};          // 16-bit windows of each base's exponent
         int wtot = 0;                     // windows of all bases
@@ -1913,7 +1914,7 @@ std::function<void(const mpz_t, uint32_t *)> fb_store_limbs(const MontMod &M) {
 // canonical rows itself (STOREW).
 int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32_t *tab8, int nwin16, int ew,
              bool rows_form, uint32_t **out) {
-    const int Kd = mod.kernel_S > 1000 ? mod.kernel_S - 1000 : 0;     // P-adic: digit-form entries
+    const int Kd = mod.kernel_S > 1000 && mod.kernel_S < 2000 ? mod.kernel_S - 1000 : 0;   // P-adic: digit-form entries
     const size_t W16 = 65536;
     int rc;
     if (hipMalloc((void **)out, (size_t)nwin16 * W16 * ew * 4) != hipSuccess) return FTHE_ERR_NOMEM;
@@ -1928,6 +1929,7 @@ int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32
     HIPOK(hipMemcpy(c->hb[0].p, dg.data(), dg.size(), hipMemcpyHostToDevice));
     Prog pr;
     if (rows_form) { pr.loadgd(0); pr.mulgd(1); pr.storew(2); }
+    else if (mod.kernel_S == kNadicS) { pr.loadgd(0); pr.mulgd(1); pr.canon(); pr.storex(SL_OUTP); }   // digits
     else { pr.loadgd(0); pr.mulgd(1); pr.storex(SL_OUTP); }
     pr.end();
     fthe_key::PH ph;
@@ -1941,7 +1943,10 @@ int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32
         {
             if (Kd)
                 hipLaunchKernelGGL(k_slot_to_digit_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
-                                   Lc.slot(SL_OUTP), Kd, ew / 2, Lc.L, W16, dst);
+                                   Lc.slot(SL_OUTP), Kd, ew / 2, 2, Lc.L, W16, dst);
+            else if (mod.kernel_S == kNadicS)          // n-adic: lane quarters of 19 limbs + a pad word
+                hipLaunchKernelGGL(k_slot_to_digit_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
+                                   Lc.slot(SL_OUTP), kNadicDigit.S / 4, ew / 8, 8, Lc.L, W16, dst);
             else
                 hipLaunchKernelGGL(k_slot_to_entries, dim3((unsigned)(W16 / 256)), dim3(256), 0, c->stream,
                                    Lc.slot(SL_OUTP), Lc.S, Lc.L, W16, ew, dst);
@@ -1955,15 +1960,26 @@ int fb_widen(fthe_key *k, fthe_ctx *c, const DevMod &mod, Shape sh, const uint32
 // base after base: one-lane n^2 kernels store radix-2^B limb entries, the four-lane kernel
 // canonical 2 n_words-word rows (k->sn2.lanes == 4).  wide = false keeps 8-bit windows.
 int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *nwin16, bool wide, uint32_t **d_tab,
-               int *ew) {
+               int *ew, bool nadic = false) {
     const MontMod &M = k->mn2.m;
-    const bool rows = k->sn2.lanes == 4;
+    const bool rows = k->sn2.lanes == 4 && !nadic;
     const int cw = 2 * k->n_words;
-    *ew = rows ? cw : 4 * ((M.S + 3) / 4);
+    const int D = kNadicDigit.S;
+    const int Qd = D / 4, QP = Qd + 1;                   // gen_nadic.py: lane quarters of 19 limbs + a pad word
+    *ew = nadic ? 8 * QP : rows ? cw : 4 * ((M.S + 3) / 4);
     std::vector<uint32_t> tab;
     for (int b = 0; b < nb; b++) {
         std::vector<uint32_t> tb;
-        if (rows)
+        if (nadic)                                        // plain x as base-n digits (x mod n, x div n)
+            tb = fb_table(hs[b], k->n2, 2 * nwin16[b], *ew, [k, D, Qd, QP](const mpz_t x, uint32_t *dst) {
+                Mpz q, r; mpz_tdiv_qr(q, r, x, k->n);
+                for (int h = 0; h < 2; h++) {
+                    std::vector<uint32_t> l = to_limbs(h ? q : r, D, kNadicDigit.B);
+                    for (int kq = 0; kq < 4; kq++)
+                        std::copy(l.begin() + kq * Qd, l.begin() + (kq + 1) * Qd, dst + (h * 4 + kq) * QP);
+                }
+            });
+        else if (rows)
             tb = fb_table(hs[b], k->n2, 2 * nwin16[b], cw, [&M, cw](const mpz_t x, uint32_t *dst) {
                 Mpz t; mpz_mul(t, x, M.R); mpz_mod(t, t, M.N);
                 mpz_to_words(t, dst, cw);
@@ -1979,7 +1995,7 @@ int pub_tables(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *nwin1
     if (!wide) { *d_tab = d8; return FTHE_OK; }
     int total = 0;
     for (int b = 0; b < nb; b++) total += nwin16[b];
-    rc = fb_widen(k, c, k->mn2, k->sn2, d8, total, *ew, rows, d_tab);
+    rc = fb_widen(k, c, nadic ? k->mnA : k->mn2, k->sn2, d8, total, *ew, rows, d_tab);
     (void)hipFree(d8);
     return rc;
 }
@@ -2447,7 +2463,8 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *ebits) 
         B.nwin[i] = ebits ? ebits[i] / 16 : (k->n_bits + 64 + 15) / 16;
         B.wtot += B.nwin[i];
     }
-    B.rows = k->sn2.lanes == 4;
+    B.nadic = k->nadic && !getenv("FTHE_PB_MONT");     // FTHE_PB_MONT=1: Montgomery rows on s152 (A/B)
+    B.rows = k->sn2.lanes == 4 && !B.nadic;
     for (int i = 0; i < nb; i++) mpz_set(B.hs[i], hs[i]);
     // process-wide cache: (device, n, hs_1 .. hs_nb) -> tables
     static std::mutex cache_mu;
@@ -2460,6 +2477,7 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *ebits) 
         for (int i = 0; i < nb; i++) mpz_to_words(B.hs[i], w.data() + (size_t)(i + 1) * cw, cw);
         id.append((const char *)w.data(), w.size() * 4);
         id.append((const char *)B.nwin, sizeof(B.nwin));
+        id.append(B.nadic ? "N" : "M");
     }
     int rc;
     {
@@ -2467,10 +2485,10 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *ebits) 
         auto it = cache.find(id);
         if (it != cache.end()) B.tab = it->second.lock();
         if (B.tab) {
-            B.ew = B.rows ? 2 * k->n_words : 4 * ((k->mn2.m.S + 3) / 4);
+            B.ew = B.nadic ? 8 * (kNadicDigit.S / 4 + 1) : B.rows ? 2 * k->n_words : 4 * ((k->mn2.m.S + 3) / 4);
         } else {
             auto t = std::make_shared<fthe_key::SharedTab>();
-            if ((rc = pub_tables(k, c, B.hs, nb, B.nwin, true, &t->d, &B.ew))) return rc;
+            if ((rc = pub_tables(k, c, B.hs, nb, B.nwin, true, &t->d, &B.ew, B.nadic))) return rc;
             B.tab = t;
             cache[id] = t;
             for (auto i = cache.begin(); i != cache.end();)      // drop entries whose tables are gone
@@ -2481,9 +2499,13 @@ int pb_build(fthe_key *k, fthe_ctx *c, const Mpz *hs, int nb, const int *ebits) 
     Prog e;                                              // X = prod_j entry(j, digit j), then (1 + m n) X
     e.loadgd16(0);
     for (int j = 1; j < B.wtot; j++) e.mulgd16(j);
-    e.storex(SL_SAVED);
-    e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);
-    if (B.rows) e.storew(2); else e.storex(SL_OUTP);
+    if (B.nadic) {                                       // digits: X (1, m) in C1, canonical digits out
+        e.mul(SL_C1); e.canon(); e.storex(SL_OUTP);
+    } else {
+        e.storex(SL_SAVED);
+        e.loadx(SL_IN1); e.mul(SL_C1); e.addsmall(1); e.mul(SL_SAVED);
+        if (B.rows) e.storew(2); else e.storex(SL_OUTP);
+    }
     e.end();
     B.mm = e.montmuls;
     if ((rc = fb_upload(e.w, &B.d_prog))) return rc;
@@ -2632,6 +2654,17 @@ static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
                 hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, kb, (uint64_t)off, cnt, B.nwin[b],
                                    L, 2, 0, dst);
             }
+        }
+        if (B.nadic) {
+            const int D = kNadicDigit.S;
+            Lc.fill(SL_C1, k->c_one_n2);
+            m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_C1) + (size_t)D * L, D, L, Lc.B);
+            const void *rows[2] = {B.d_tab, dig};
+            if ((rc = Lc.prog_raw(B.d_prog, B.mm, k->mnA, rows, 2))) return rc;
+            mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTP), D, k->cst(k->c_n76), D,
+                        Lc.slot(SL_OUTP) + (size_t)D * L, D, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+            if (pipe && (rc = pipe->after(off, cnt))) return rc;
+            continue;
         }
         m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
         if (B.rows) {

@@ -31,7 +31,10 @@ __global__ void k_rng_digits(RngKey key, uint64_t index0, size_t count, int nwin
 __global__ void k_alpha_digits(const uint32_t *alpha, int stride, int aw, size_t count, int nwin, int L, int bpd,
                                uint8_t *dig);
 __global__ void k_slot_to_entries(const uint32_t *slot, int S, int L, size_t count, int ew, uint32_t *out);
-__global__ void k_slot_to_digit_entries(const uint32_t *slot, int K, int KB, int L, size_t count, uint32_t *out);
+// entries of nblk blocks of KB words, block h holding limbs [h K, h K + K) of the slot and KB - K zero pads
+// (P-adic: 2 blocks, the digits; n-adic: 8 blocks, the four lane quarters of each digit)
+__global__ void k_slot_to_digit_entries(const uint32_t *slot, int K, int KB, int nblk, int L, size_t count,
+                                        uint32_t *out);
 // fthe_hist.hip: histogram CSR and the segmented-product planner
 __global__ void k_hist_count(const uint8_t *bin, int n_col, const int32_t *cut, int max_bin, const int32_t *inst,
                              size_t n_sel, int planes, int64_t n_bins, unsigned long long *cnt);

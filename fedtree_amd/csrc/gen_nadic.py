@@ -27,6 +27,9 @@ Ops (uint32 pairs, bn_host.hpp Prog):
     3 SQR    count  X <- X^2, count times
     4 MUL    slot   X <- X * (digits of slot)   (y0, y1 any limbs < 2^27: only X must be reduced)
    20 CANON  -      x0 (< 2n) -> x0 mod n with its carry into x1, then x1 -> x1 mod n (x1 <= n + 1)
+   14 / 16 LOADGD(16) j   digits <- fixed-base table entry (j << W) | digit j of the ciphertext (W = 8 / 16)
+   15 / 17 MULGD(16) j    X <- X * that entry  (tables in digit form: y0 then y1, each as four lane quarters
+                          of 19 limbs + 1 pad word: 160 words per entry)
 Products leave x0 in [0, n) and x1 in [0, n]; CANON makes both canonical (before the output and after
 a LOADX of a raw r < 2n).
 
@@ -130,7 +133,8 @@ def gen_nadic(S: int, B: int, name: str) -> str:
     e('  s_add_u32 s6, s6, 8')
     e('  s_addc_u32 s7, s7, 0')
     e('  s_waitcnt lgkmcnt(0)')
-    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (20, '.Lcanon')):
+    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (20, '.Lcanon'),
+                      (14, '.Lloadgd'), (15, '.Lmulgd'), (16, '.Lloadgd16'), (17, '.Lmulgd16')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
     e('  s_branch .Lend')
@@ -278,6 +282,61 @@ def gen_nadic(S: int, B: int, name: str) -> str:
     write_rows(lambda j: f"v{TB1 + Q + j}", S)
     e('  s_mov_b32 s19, 0')
     e('  s_branch .Lprod_mul')
+
+    # ---- gathered fixed-base table entries (digit form) ------------------------------------
+    # entry (j << W) | dig[j][g] of the table at rows[0]: EW = 8 QP words, y0 then y1, each as four lane
+    # quarters of QP = Q + 1 words (Q limbs and a pad word: 16-byte aligned, so lane k reads its quarters
+    # with dwordx4 loads); the digit array (u8, or u16 when W = 16) [window][L] at rows[1]
+    QP = Q + 1
+    assert QP % 4 == 0
+    EW = 8 * QP
+
+    def gather_entry(wide):
+        """the entry's quarters of y0, y1 -> v[TB1 .. TB1 + QP), v[TB1 + QP .. TB1 + 2 QP)"""
+        vt, vt2, vk = f"v{V_Q}", f"v{V_Q2}", f"v{V_A2}"
+        addr = f"v[{V_TMP}:{V_TMP + 1}]"
+        e('  s_load_dwordx2 s[16:17], s[0:1], 0x30')        # digit array
+        e('  s_lshr_b32 s14, s10, 2')                        # L
+        e('  s_mul_i32 s14, s14, s15')                       # j * L
+        if wide:
+            e('  s_lshl_b32 s14, s14, 1')                    # u16 digits
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_add_u32 s16, s16, s14')
+        e('  s_addc_u32 s17, s17, 0')
+        e(f'  v_lshrrev_b32_e32 {vt}, 9, v{V_ROW}')          # g
+        if wide:
+            e(f'  v_lshlrev_b32_e32 {vt}, 1, {vt}')
+        e(f'  global_load_{"ushort" if wide else "ubyte"} {vt}, {vt}, s[16:17]')
+        e('  s_load_dwordx2 s[16:17], s[0:1], 0x28')        # table
+        e(f'  s_lshl_b32 s14, s15, {16 if wide else 8}')     # j << W
+        e(f'  v_mov_b32_e32 {vt2}, {4 * EW}')
+        e(f'  v_bfe_u32 {vk}, v{V_ROW}, 7, 2')               # k
+        e(f'  v_mul_u32_u24_e32 {vk}, {4 * QP}, {vk}')       # this lane's quarter
+        e('  s_waitcnt vmcnt(0) lgkmcnt(0)')
+        e(f'  v_or_b32_e32 {vt}, s14, {vt}')
+        e(f'  v_mad_u64_u32 {addr}, vcc, {vt}, {vt2}, s[16:17]')     # 64-bit entry address (tables > 4 GiB)
+        e(f'  v_add_co_u32_e32 v{V_TMP}, vcc, v{V_TMP}, {vk}')
+        e(f'  v_addc_co_u32_e32 v{V_TMP + 1}, vcc, 0, v{V_TMP + 1}, vcc')
+        for dig in range(2):
+            for i in range(QP // 4):
+                r0 = TB1 + dig * QP + 4 * i
+                e(f'  global_load_dwordx4 v[{r0}:{r0 + 3}], {addr}, off offset:{4 * (dig * 4 * QP + 4 * i)}')
+        e('  s_waitcnt vmcnt(0)')
+
+    for wide in (False, True):
+        sfx = "16" if wide else ""
+        e(f'.Lloadgd{sfx}:')
+        gather_entry(wide)
+        for j in range(Q):
+            e(f'  v_mov_b32_e32 {X0(j)}, v{TB1 + j}')
+            e(f'  v_mov_b32_e32 {X1(j)}, v{TB1 + QP + j}')
+        e('  s_branch .Lprog')
+        e(f'.Lmulgd{sfx}:')
+        gather_entry(wide)
+        write_rows(lambda j: f"v{TB1 + j}", 0)
+        write_rows(lambda j: f"v{TB1 + QP + j}", S)
+        e('  s_mov_b32 s19, 0')
+        e('  s_branch .Lprod_mul')
 
     e('.Lsqr:')
     e('  s_mov_b32 s19, s15')

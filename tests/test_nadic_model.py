@@ -50,3 +50,16 @@ def test_generated_assembly_on_quad_emulator():
         quad_emu.selftest(trials=1, ebits=6)
     finally:
         os.chdir(cwd)
+
+
+def test_gathered_digit_entries_on_quad_emulator():
+    """LOADGD / MULGD (8-bit windows) and LOADGD16 / MULGD16 from digit-form table entries (the
+    published-bases public encrypt's gathered products) on the emulated quad"""
+    import quad_emu
+    cwd = os.getcwd()
+    os.chdir(ROOT)
+    try:
+        quad_emu.selftest_gather(False)
+        quad_emu.selftest_gather(True)
+    finally:
+        os.chdir(cwd)

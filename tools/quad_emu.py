@@ -197,6 +197,38 @@ class QuadEmu:
                 self.scc = int(r != 0)
                 self.swrite(args[0], r)
                 continue
+            if op == 's_lshr_b32':
+                r = (self.sread(args[1]) & M32) >> (self.sread(args[2]) & 31)
+                self.scc = int(r != 0)
+                self.swrite(args[0], r)
+                continue
+            if op in ('global_load_ubyte', 'global_load_ushort'):
+                dst, voff, sbase = args
+                for ln in self.active():
+                    addr = self.sread(sbase) + (self.vread(ln, voff) & M32)
+                    w = self.mem.get(addr & ~3, 0) >> (8 * (addr & 3))
+                    self.vwrite(ln, dst, w & (0xff if op.endswith('ubyte') else 0xffff))
+                continue
+            if op == 'global_load_dwordx4':
+                dst, vaddr = args[0], args[1]
+                m = re.search(r'offset:(\d+)', ins)
+                off = int(m.group(1)) if m else 0
+                _, b0, n = self.rr(dst)
+                for ln in self.active():
+                    addr = self.vread(ln, vaddr, 2) + off
+                    assert addr % 16 == 0, addr
+                    for i in range(n):
+                        self.v[ln][b0 + i] = self.mem.get(addr + 4 * i, 0)
+                continue
+            if op == 'global_load_dword' and args[2].split()[0] == 'off':
+                dst, vaddr = args[0], args[1]
+                m = re.search(r'offset:(\d+)', ins)
+                off = int(m.group(1)) if m else 0
+                for ln in self.active():
+                    addr = self.vread(ln, vaddr, 2) + off
+                    assert addr % 4 == 0
+                    self.vwrite(ln, dst, self.mem.get(addr, 0))
+                continue
             if op == 's_cmp_eq_u32':
                 self.scc = int((self.sread(args[0]) & M32) == (self.sread(args[1]) & M32))
                 continue
@@ -289,6 +321,14 @@ class QuadEmu:
                 W(args[0], R(args[1], 2))
             elif op == 'v_mul_u32_u24_e32':
                 W(args[0], ((R(args[1]) & 0xffffff) * (R(args[2]) & 0xffffff)) & M32)
+            elif op == 'v_add_co_u32_e32':
+                r = (R(args[2]) & M32) + (R(args[3]) & M32)
+                W(args[0], r & M32)
+                newvcc = (newvcc & ~(1 << ln)) | ((r >> 32) << ln)
+            elif op == 'v_addc_co_u32_e32':
+                r = (R(args[2]) & M32) + (R(args[3]) & M32) + (self.vcc >> ln & 1)
+                W(args[0], r & M32)
+                newvcc = (newvcc & ~(1 << ln)) | ((r >> 32) << ln)
             elif op == 'v_mul_lo_u32':
                 W(args[0], (R(args[1]) * R(args[2])) & M32)
             elif op == 'v_lshl_add_u32':
@@ -446,5 +486,87 @@ def selftest(trials=2, ebits=24):
     print('quad_emu selftest ok')
 
 
+def nadic_entry(v, n, S=76, B=27):
+    """digit-form table entry of v (gen_nadic.py): y0 = v mod n, y1 = v div n, each as four lane quarters
+    of S/4 limbs and a pad word"""
+    import nadic_model as nm
+    Q = S // 4
+    out = []
+    for y in (v % n, v // n):
+        lim = nm.limbs(y)
+        for k in range(4):
+            out += lim[k * Q:(k + 1) * Q] + [0]
+    return out
+
+
+def selftest_gather(wide=False):
+    """LOADGD(16) / MULGD(16) from a digit-form table: X = e0 e1 (1 + m n) mod n^2 for entries e0, e1 at
+    windows 0 and 1 selected by per-ciphertext digits, against Python integers"""
+    sys.path.insert(0, 'fedtree_amd/csrc')
+    sys.path.insert(0, 'tools')
+    from gen_nadic import gen_nadic
+    import nadic_model as nm
+    S, B, SS = 76, 27, 152
+    asm = gen_nadic(S, B, 'fthe_nadic_q76')
+    rng = random.Random(13)
+    n = rng.getrandbits(2048) | (1 << 2047) | 1
+    n2 = n * n
+    em = QuadEmu(asm, 4 * 2 * S * 68)
+    L = 256
+    KA, CTX, PROG, SLOTS, TAB, DIG = 0x100, 0x1000, 0x2000, 0x100000, 0x10000000, 0x8000000
+    W = 16 if wide else 8
+    kargs = [SLOTS & M32, SLOTS >> 32, PROG, 0, CTX, 0, L * 4, SS * L * 4, L, 0]
+    kargs += [TAB & M32, TAB >> 32, DIG & M32, DIG >> 32]            # rows[0] (offset 40), rows[1] (48)
+    for i, v in enumerate(kargs):
+        em.mem[KA + 4 * i] = v
+    k1, k2, k3, bias = nm.consts(n)
+    ctxw = nm.limbs(n) + [0]
+    for d in (k1, k2, k3, bias):
+        b_ = f2b(d)
+        ctxw += [b_ & M32, b_ >> 32]
+    for i, w in enumerate(ctxw):
+        em.mem[CTX + 4 * i] = w
+    dg = [rng.randrange(1 << W), rng.randrange(1 << W)]
+    vals = {}
+    for j, d in enumerate(dg):
+        v = rng.randrange(n2) if j == 0 else n2 - 1 - rng.randrange(1 << 64)
+        vals[j] = v
+        ent = (j << W) | d
+        words = nadic_entry(v, n)
+        for i_, w_ in enumerate(words):
+            em.mem[TAB + ent * 4 * len(words) + 4 * i_] = w_
+        # digit of ciphertext 0 in window j (u8 / u16 array [window][L])
+        a = DIG + (j * L) * (2 if wide else 1)
+        w0 = em.mem.get(a & ~3, 0)
+        sh = 8 * (a & 3)
+        w0 |= d << sh
+        em.mem[a & ~3] = w0
+    m = rng.getrandbits(64)
+    prog = []
+    op = lambda o, a_: prog.extend([o, a_])
+    op(16 if wide else 14, 0)
+    op(17 if wide else 15, 1)
+    op(4, 3)
+    op(20, 0)
+    op(2, 6)
+    op(0, 0)
+    for i, w_ in enumerate(prog):
+        em.mem[PROG + 4 * i] = w_
+    for k_, limb in enumerate(nm.limbs(1) + nm.limbs(m)):
+        em.mem[SLOTS + 3 * SS * L * 4 + k_ * L * 4] = limb
+    em.s[0], em.s[1], em.s[2] = KA, 0, 0
+    for ln in range(NL):
+        em.v[ln][0] = ln
+    em.run('fthe_nadic_q76')
+    out = [em.mem.get(SLOTS + 6 * SS * L * 4 + k_ * L * 4, 0) for k_ in range(SS)]
+    x0 = sum(out[k_] << (B * k_) for k_ in range(S))
+    x1 = sum(out[S + k_] << (B * k_) for k_ in range(S))
+    assert x0 < n and x1 < n
+    assert x0 + x1 * n == vals[0] * vals[1] * (1 + m * n) % n2
+    print(f'gather ({W}-bit windows): ok')
+
+
 if __name__ == '__main__':
     selftest(int(sys.argv[1]) if len(sys.argv) > 1 else 2, int(sys.argv[2]) if len(sys.argv) > 2 else 24)
+    selftest_gather(False)
+    selftest_gather(True)
