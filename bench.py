@@ -388,13 +388,13 @@ def run(a, world):
             "kernel_share_of_step": round(k_s / elapsed_rank, 4)}
     # exponentiation kernels: the Montgomery program kernels and the P-adic one (pseudo-variant 1037)
     for S, kname in ((37, "fthe_montprog_s37"), (74, "fthe_montprog_s74"), (152, "fthe_montprog_s152"),
-                     (1037, "fthe_padic_k37")):
+                     (1037, "fthe_padic_k37"), (1137, "fthe_padic_m37")):
         vms, vn = ctypes.c_double(), ctypes.c_double()
         lib.fthe_prof_variant(dev.ctx, S, ctypes.byref(vms), ctypes.byref(vn))
         if vn.value:
             roof["avg_expo_launch_ms_by_kernel"][kname] = round(vms.value / vn.value, 3)
     roof["kernel"] = " + ".join(roof["avg_expo_launch_ms_by_kernel"]) or "fthe_montprog"
-    if xmacs.value:
+    if xmacs.value and "fthe_padic_k37" in roof["avg_expo_launch_ms_by_kernel"]:
         # the P-adic kernel in issue terms: its v_mad instructions (radix 2^28, counted per program by the
         # engine) over its own launch time, against the same 39.3 T/s issue peak
         vms, vn = ctypes.c_double(), ctypes.c_double()
@@ -407,7 +407,8 @@ def run(a, world):
         roof["padic_executed_mads_per_encrypt"] = round(xmacs.value / enc_rank)
         roof["padic_frac_executed_mads"] = round(rate / PEAK_MAC_S, 4)
         roof["padic_frac_of_measured_mad_peak"] = round(rate / MEASURED_MAD_S, 4)
-    expo_kernel = "fthe_padic_k37" if "fthe_padic_k37" in roof["avg_expo_launch_ms_by_kernel"] else "fthe_montprog_s74"
+    expo_kernel = next((kn for kn in ("fthe_padic_m37", "fthe_padic_k37") if kn in roof["avg_expo_launch_ms_by_kernel"]),
+                       "fthe_montprog_s74")
     # HBM traffic per full-chunk exponentiation launch from the committed PMC passes
     # (tools/pmc_round.sh; 2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section)
     pmc = {}

@@ -31,6 +31,7 @@
 
 #include "../../include/fthe.h"
 #include "bn_host.hpp"
+#include "padic_tiles.hpp"
 #include "fthe_glue.h"
 #include "gen/montprog_blobs.h"
 
@@ -40,15 +41,18 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 7;
+constexpr int MAX_VARIANTS = 8;
 // s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency);
 // 1000 + K: the P-adic exponentiation kernels mod P^2 (gen_padic.py, digits of K limbs, slots of 2K
 // limbs; the "S" here only names the variant): K = 37 runs on the s74 slots of Paillier-2048,
 // K = 19 on slots of its own (38 limbs) for Paillier-1024;
+// 1137: the K = 37 P-adic kernel with matrix-core (MFMA) Barrett reductions (gen_padic_mfma.py), same
+// slots and programs, no fixed-base table ops;
 // 2000 + 76: the n-adic four-lane kernel (gen_nadic.py, base-n digits of 76 limbs) on the s152 slots
-constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19, kNadicS = 2076;
+constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19, kNadicS = 2076, kPadicMfmaS = 1137;
 const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4},
-                                       {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}, {kNadicS, 27, 4}};
+                                       {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}, {kNadicS, 27, 4},
+                                       {kPadicMfmaS, 28, 1}};
 constexpr Shape kLatShape{80, 27, 4};
 
 int variant_index(int S) {
@@ -237,6 +241,7 @@ struct DevMod {
     MontMod m;
     uint32_t *d_ctx = nullptr;     // N limbs (S) + nprime; P-adic: -P limbs, mu limbs
     int kernel_S = 0;              // kPadicS: the P-adic kernel on m's slot shape (m.N = P^2)
+    int kernel_S_mfma = 0;         // kPadicMfmaS: the same programs on the MFMA-Barrett kernel (no table ops)
     // SURVEY 8(d) work unit: W(s) = 2 s^2 + s 32x32 MACs per Montgomery
     // product on s = ceil(bits/32) u32 limbs (algorithmic, kernel-independent)
     double w_alg() const {
@@ -481,6 +486,7 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
         if (kVariants[i].S > 2000) snprintf(name, sizeof name, "fthe_nadic_q%d", kVariants[i].S - 2000);
+        else if (kVariants[i].S > 1100) snprintf(name, sizeof name, "fthe_padic_m%d", kVariants[i].S - 1100);
         else if (kVariants[i].S > 1000) snprintf(name, sizeof name, "fthe_padic_k%d", kVariants[i].S - 1000);
         else snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
@@ -611,11 +617,17 @@ static int padic_digits(const mpz_t P, Shape sh) {
     if (sh.S == 37 && b >= 505 && b <= 516) return kPadicSmallK;
     return 0;
 }
+// K = 37 also carries the LDS tile image of fthe_padic_m37 (padic_tiles.hpp) at byte 512 of the context
+// when FTHE_PADIC_MFMA is set (opt-in while it is being tuned); the MFMA kernel then runs the key's
+// exponentiation programs.
 static int upload_padic(DevMod &d, const mpz_t P, int K) {
     Mpz P2; mpz_mul(P2, P, P);
     d.m.init(P2, Shape{2 * K, 28, 1});
     const int pad = ((20 + K + 3) & ~3) - 20 - K;          // gen_padic.py: mu from an aligned SGPR
-    std::vector<uint32_t> w((size_t)2 * K + 1 + pad, 0u), l = to_limbs(P, K, 28);
+    std::vector<uint8_t> tiles;
+    if (K == kPadicK && getenv("FTHE_PADIC_MFMA")) tiles = padic_tiles::build(P);
+    std::vector<uint32_t> w(tiles.empty() ? (size_t)2 * K + 1 + pad : 128 + tiles.size() / 4, 0u), l = to_limbs(P, K, 28);
+    if (!tiles.empty()) std::memcpy(w.data() + 128, tiles.data(), tiles.size());
     for (int j = 0; j < K; j++) w[j] = (uint32_t)(-(int32_t)l[j]);
     Mpz mu; mpz_set_ui(mu, 1); mpz_mul_2exp(mu, mu, 56 * K); mpz_fdiv_q(mu, mu, P);
     std::vector<uint32_t> ml = to_limbs(mu, K + 1, 28);
@@ -623,6 +635,7 @@ static int upload_padic(DevMod &d, const mpz_t P, int K) {
     if (hipMalloc(&d.d_ctx, w.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(d.d_ctx, w.data(), w.size() * 4, hipMemcpyHostToDevice));
     d.kernel_S = 1000 + K;
+    d.kernel_S_mfma = tiles.empty() ? 0 : kPadicMfmaS;
     return FTHE_OK;
 }
 // Algorithmic 32-bit MACs of a P-adic program (SURVEY 8(d) units, the executed algorithm): s = words
@@ -1273,7 +1286,7 @@ constexpr int kSpreadLds = 84 * 1024;   // > 80 KB: one workgroup per CU (gfx950
 
 int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, const DevMod &mod, double lane_mm,
                     size_t live, const void *const *rows = nullptr, int nrows = 0, hipStream_t st = nullptr,
-                    bool spread = false, double lane_alg = -1, double lane_exec = -1) {
+                    bool spread = false, double lane_alg = -1, double lane_exec = -1, bool table_free = false) {
     if (!st) st = c->stream;
     struct {
         void *s; const void *p; const void *cx; uint32_t ls, ss; uint32_t live, pad; const void *rows[16];
@@ -1283,7 +1296,8 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     for (int i = 0; i < nrows; i++) args.rows[i] = rows[i];
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    int vi = variant_index(mod.kernel_S ? mod.kernel_S : S);
+    // programs without fixed-base table ops (the key's own) may take the MFMA-Barrett P-adic kernel
+    int vi = variant_index(table_free && mod.kernel_S_mfma ? mod.kernel_S_mfma : mod.kernel_S ? mod.kernel_S : S);
     if (vi < 0) return FTHE_ERR_UNSUPPORTED;
     // only the workgroups that hold live elements (slot strides stay those of L)
     if (live > (size_t)L) return FTHE_ERR_ARG;
@@ -1344,7 +1358,7 @@ struct Launch {
     int prog(const fthe_key::PH &ph, const DevMod &mod, const void *const *rows = nullptr, int nrows = 0) {
         if (mod.m.S != S) return FTHE_ERR_ARG;
         int rc = launch_montprog(c, base, S, L, k->prog(ph), mod, ph.mm, live, rows, nrows, st, spread, ph.alg,
-                                 ph.exec);
+                                 ph.exec, true);
         if (rc) return rc;
         mm += ph.mm * (double)live;
         return FTHE_OK;

@@ -1,0 +1,547 @@
+#!/usr/bin/env python3
+"""Generator of the P-adic exponentiation kernel with matrix-core Barrett reductions (gfx950 assembly):
+fthe_padic_m37, X^e mod P^2 with X = x0 + x1 P kept as two base-P digits of K = 37 radix-2^28 limbs,
+one ciphertext half per lane -- the arithmetic of gen_padic.py (see its docstring), except where the
+work goes.
+
+The products of a squaring (2 x0 x1, x0^2) are variable x variable and stay on the VALU (product
+scanning, v_mad_u64_u32).  The two Barrett reductions that follow every product are 60% of the
+multiply-adds of fthe_padic_k37, and both of their products have a constant operand (mu, P): over the
+64 lanes of a wave they are matrix products, so they run on v_mfma_i32_32x32x32_i8:
+
+  * each lane packs its operand (q1 = T >> 28 (K-1), or q3) into base-256 digits fed as b ^ 0x80 = b - 128
+    (40 dwords, region XB), and v_permlane32_swap turns them into the B operands of two 32-lane groups
+    (lanes 0-31 / 32-63 of the wave);
+  * the A operand is a 32 x 32 tile of the constant's Toeplitz matrix in balanced base-256 digits, read
+    from LDS (19 tiles, 19 KB, filled once per workgroup from the key's context; the correction for the
+    -128 offset and the truncation bias ride in one extra digit column, tools/padic_mfma_model.py);
+  * each M-tile (32 output columns) accumulates its K-tiles in int32 (16 VGPRs per group), the two groups'
+    accumulators are exchanged with 16 v_permlane32_swap so that every lane holds its own 32 column sums,
+    and the lane folds them into 28-bit limbs: one v_mad_i64_i32 per column (x 2^sh), one mask and one
+    arithmetic shift per limb.
+
+Product 1 forms columns 112..271 of q1 mu and yields q3 = Barrett's quotient estimate or one less (q3 is
+clamped to 0 when q1 = 0); product 2 forms columns 0..129 of q3 P (as matrix columns 1..130, the constant
+digit leading) and r = (T - q3 P) mod b^K exactly.
+The digits stay within [0, 5P) as in fthe_padic_k37 (the bounds are asserted by the model).
+
+Ops: those of gen_padic.py except the fixed-base table ops (LOADXGD / MULGD), which the host keeps on
+fthe_padic_k37:  0 END, 1 LOADX, 2 STOREX, 3 SQR, 4 MUL, 22 LOADP, 23 STOREP.
+ctx: [-P limbs (K, int32) ...] as for fthe_padic_k37, and the LDS tile image at byte 512 (20 KB).
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gen_montprog import _descriptor  # noqa: E402
+
+AB = os.environ.get("FTHE_GEN_M37_AB", "")     # timing-only A/B variants (wrong results): noswap, nonop, nomfma
+TILE_OFF = 512                  # byte offset of the tile image in ctx
+LDS_BYTES = 20 * 1024           # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
+S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
+QBIT = 28 * 38                  # q3 = floor(N / 2^1064)
+TILE_D1 = (-3, -2, -1, 0, 1)    # product-1 Toeplitz tiles (k <= 3) by m - k; then k = 4 for m = 0..4
+TILE_D2 = (0, 1, 2, 3)          # product-2: k = 0 for m = 0..4 (tiles 10..14), then Toeplitz (k >= 1) by m - k
+
+
+def tile_index(prod, m, k):
+    if prod == 1:
+        return TILE_D1.index(m - k) if k <= 3 else 5 + m
+    return 10 + m if k == 0 else 15 + TILE_D2.index(m - k)
+
+
+def gen_padic_mfma(name: str) -> str:
+    K, B = 37, 28
+    MASK = (1 << B) - 1
+    # ---- VGPR plan ---------------------------------------------------------
+    V_TID, V_GOFF = 0, 1
+    VA = (2, 6, 10)                              # A-tile buffers v[2:5], v[6:9], v[10:13] (ACC is free)
+    ACC0 = 10                                    # product columns: 2 column sets x 2 chains x 64-bit
+    CARRY = 18
+    XA = 20                                      # x0 digit (v20..v56); Barrett: accumulators v20..v51
+    G0, G1 = XA, XA + 16
+    # Barrett scratch in XA above the accumulators: chunk sums v[52:55], clamp mask v56, chunk carry v[58:59]
+    XB = 60                                      # x1 digit (v60..v96); Barrett: operand dwords D0..D39
+    TT = 100                                     # T limbs v100..v173
+    VV = 174                                     # V limbs v174..v247
+    V_LDS = 248                                  # (lane & 63) * 16
+    NVGPR = 249
+    X0 = [f"v{XA + i}" for i in range(K)]
+    X1 = [f"v{XB + i}" for i in range(K)]
+    T = [f"v{TT + i}" for i in range(2 * K)]
+    V = [f"v{VV + i}" for i in range(2 * K)]
+    D = [f"v{XB + i}" for i in range(40)]
+    # ---- SGPR plan ---------------------------------------------------------
+    # s[0:1] kernarg, s2 wg id, s[2:3] call target, s[4:5] slots, s[6:7] prog, s[8:9] ctx, s10 limb
+    # stride, s11 slot stride, s[12:13] return address, s[14:15] op/arg, s[16:17] addr, s19 counter;
+    # s20..s27 = 2^0, 2^4, .., 2^28; s28..s34 = -2^0, .., -2^24; -P limbs from s36
+    SPOW, SNEG, SNP = 20, 28, 36                   # s35 = 0x0fffffff
+    NSGPR = SNP + K
+    POW = lambda sh: f"s{SPOW + sh // 4}"
+    NEG = lambda sh: f"s{SNEG + sh // 4}"
+    NP = lambda j: f"s{SNP + j}"
+
+    def pair(n):
+        return f"v[{n}:{n + 1}]"
+
+    def acc(s, ch):
+        n = ACC0 + 2 * (2 * s + ch)
+        return f"v[{n}:{n + 1}]"
+
+    def acclo(s, ch):
+        return f"v{ACC0 + 2 * (2 * s + ch)}"
+
+    carry = pair(CARRY)
+    o = []
+    e = o.append
+
+    # ---- column engine (product scanning, two adjacent columns side by side) --------------------
+    def columns(cols, signed=False):
+        mad = 'v_mad_i64_i32' if signed else 'v_mad_u64_u32'
+        shr = 'v_ashrrev_i64' if signed else 'v_lshrrev_b64'
+        pending = []
+
+        def flush(n):
+            for _ in range(min(n, len(pending))):
+                e(pending.pop(0))
+
+        def tail_of(ci, col, a0, lo0, used):
+            t = []
+            first = ci == 0
+            if not used:
+                t.append(f'  v_mov_b64_e32 {a0}, {"0" if first else carry}')
+            elif col.get('dbl'):
+                t.append(f'  v_lshl_add_u64 {a0}, {a0}, 1, {"0" if first else carry}')
+            elif not first:
+                t.append(f'  v_lshl_add_u64 {a0}, {a0}, 0, {carry}')
+            if col.get('sq'):
+                x = col['sq']
+                t.append(f'  {mad} {a0}, vcc, {x}, {x}, {a0}')
+            if col.get('out') is not None:
+                if col.get('last'):
+                    t.append(f'  v_mov_b32_e32 {col["out"]}, {lo0}')
+                else:
+                    t.append(f'  v_and_b32_e32 {col["out"]}, {hex(MASK)}, {lo0}')
+            if not col.get('last') and not col.get('nocarry'):
+                t.append(f'  {shr} {carry}, {B}, {a0}')
+            return t
+
+        for gi in range(0, len(cols), 2):
+            s = (gi // 2) % 2
+            members = list(range(gi, min(gi + 2, len(cols))))
+            seqs = [(acc(s, m), cols[ci]['terms']) for m, ci in enumerate(members)]
+            used = [False] * len(seqs)
+            n = 0
+            for t in range(max(len(q[1]) for q in seqs)):
+                for k, (ac, terms) in enumerate(seqs):
+                    if t < len(terms):
+                        a_, b_ = terms[t]
+                        e(f'  {mad} {ac}, vcc, {a_}, {b_}, {ac if used[k] else "0"}')
+                        used[k] = True
+                        n += 1
+                        if n % 2 == 0:
+                            flush(1)
+            flush(len(pending))
+            tail = []
+            for m, ci in enumerate(members):
+                tail += tail_of(ci, cols[ci], acc(s, m), acclo(s, m), used[m])
+            pending = tail
+        flush(len(pending))
+
+    def product_cols(a, b, n_out, outs, a2=None, b2=None):
+        cols = []
+        for c in range(n_out):
+            terms = []
+            for i in range(len(a)):
+                j = c - i
+                if 0 <= j < len(b):
+                    terms.append((a[i], b[j]))
+                    if a2 is not None:
+                        terms.append((a2[i], b2[j]))
+            cols.append({'terms': terms, 'out': outs[c], 'last': c == n_out - 1})
+        return cols
+
+    def move(dst, src):
+        n = len(src)
+        for i in range(0, n - 1, 2):
+            if int(dst[i][1:]) % 2 == 0 and int(src[i][1:]) % 2 == 0:
+                e(f'  v_pk_mov_b32 {pair(int(dst[i][1:]))}, {pair(int(src[i][1:]))}, {pair(int(src[i][1:]))} op_sel:[0,1]')
+            else:
+                e(f'  v_mov_b32_e32 {dst[i]}, {src[i]}')
+                e(f'  v_mov_b32_e32 {dst[i + 1]}, {src[i + 1]}')
+        if n % 2:
+            e(f'  v_mov_b32_e32 {dst[n - 1]}, {src[n - 1]}')
+
+    # ---- matrix-core Barrett -------------------------------------------------
+    CACC2 = (pair(XA + 32), pair(XA + 34))      # chunk sums, alternating by chunk parity: v[52:53], v[54:55]
+    CCARRY = pair(XA + 38)                      # chunk carry v[58:59]
+    SMASK = "s35"                               # 0x0fffffff (v_bfi_b32 operand)
+
+    def orpack(limbs, shift_bits, ndw, xor_masks, lead_one=False, norm0=False):
+        """normalised 28-bit limbs (limb t at bit 28 t + shift_bits) -> dwords D[0..ndw-1] XOR xor_masks[w],
+        each dword from the (at most two) limbs it overlaps: no carry chain.  lead_one: byte 0 is the
+        constant digit 1 (shift_bits = 8).  norm0: limb 0 may hold a bit 28 (masked off here)."""
+        n = len(limbs)
+        for w in range(ndw):
+            d = D[w]
+            if lead_one and w == 0:
+                e(f'  v_lshl_or_b32 {d}, {limbs[0]}, 8, 1')
+            else:
+                lo = (32 * w - shift_bits) // B
+                off = 32 * w - shift_bits - B * lo
+                hi_ok = lo + 1 < n
+                if norm0 and lo == 0:
+                    assert off == 0 and hi_ok
+                    e(f'  v_lshlrev_b32_e32 {d}, 28, {limbs[1]}')
+                    e(f'  v_bfi_b32 {d}, {SMASK}, {limbs[0]}, {d}')
+                elif not hi_ok:
+                    e(f'  v_lshrrev_b32_e32 {d}, {off}, {limbs[lo]}')
+                elif off == 0:
+                    e(f'  v_lshl_or_b32 {d}, {limbs[lo + 1]}, 28, {limbs[lo]}')
+                else:
+                    e(f'  v_lshrrev_b32_e32 {d}, {off}, {limbs[lo]}')
+                    e(f'  v_lshl_or_b32 {d}, {limbs[lo + 1]}, {B - off}, {d}')
+            if xor_masks[w]:
+                e(f'  v_xor_b32_e32 {d}, {hex(xor_masks[w])}, {d}')
+
+    def swap_operands():
+        e('  s_nop 1')
+        for k in range(5):
+            for j in range(4):
+                e(f'  v_permlane32_swap_b32_e32 {D[8 * k + j]}, {D[8 * k + 4 + j]}')
+        e('  s_nop 4')
+
+    def rd(prod, m, k, n):
+        b_ = VA[n % 3]
+        e(f'  ds_read_b128 v[{b_}:{b_ + 3}], v{V_LDS} offset:{1024 * tile_index(prod, m, k)}')
+
+    def prefetch(prod, m, ks):
+        """the first two A-tile reads of M-tile m (issued while the lane still has VALU work)"""
+        for n in range(min(2, len(ks))):
+            rd(prod, m, ks[n], n)
+
+    def mtile_mfmas(prod, m, ks, nxt=None):
+        """the MFMAs of M-tile m over K-tiles ks (both lane groups); its first two A tiles are already in
+        flight (prefetch), the rest rotate through three buffers one step ahead.  nxt = (prod, m, ks) of
+        the next M-tile: its first reads go out as soon as this tile's MFMAs have read their operands."""
+        L = len(ks)
+        for n, k in enumerate(ks):
+            if n + 2 < L:
+                rd(prod, m, ks[n + 2], n + 2)
+            e(f'  s_waitcnt lgkmcnt({min(L, n + 3) - n - 1})')
+            buf = VA[n % 3]
+            for g, G in ((0, G0), (1, G1)):
+                src_c = "0" if n == 0 else f"v[{G}:{G + 15}]"
+                bo = 8 * k + 4 * g
+                if "nomfma" not in AB:
+                    e(f'  v_mfma_i32_32x32x32_i8 v[{G}:{G + 15}], v[{buf}:{buf + 3}], v[{XB + bo}:{XB + bo + 3}], {src_c}')
+        # results -> VALU: wait out the last MFMA (8-pass XDL), then exchange the halves
+        if "nonop" not in AB:
+            e('  s_nop 7')
+            e('  s_nop 7')
+            e('  s_nop 7')
+        if nxt is not None:
+            prefetch(*nxt)
+        for r in range(16 if "noswap" not in AB else 0):
+            e(f'  v_permlane32_swap_b32_e32 v{G0 + r}, v{G1 + r}')
+        e('  s_nop 1')
+
+    def col_reg(rho):
+        """register of column rho (0..31) of the M-tile after the exchange"""
+        rr = (rho & 3) + 4 * (rho >> 3)
+        return f"v{(G1 if (rho >> 2) & 1 else G0) + rr}"
+
+    class Chunks:
+        """column sums -> 28-bit limbs.  Chunk t (bits [base + 28 t, +28)) sums its columns (x 2^sh) into its
+        own accumulator (two, alternating), independent of the carry; its tail (+ carry, mask, carry out)
+        is deferred into the next chunk's multiply-adds, so the carry chain never stalls the wave."""
+
+        def __init__(self, base_bits, t0, t_last, outs, neg, inits=None, nocarry_last=False):
+            self.base, self.t, self.t0, self.t_last, self.outs, self.neg = base_bits, t0, t0, t_last, outs, neg
+            self.inits, self.nocarry_last = inits, nocarry_last
+            self.pending = []
+            self.fresh = True
+            self.begun = False
+
+        def acc(self):
+            return CACC2[(self.t - self.t0) & 1]
+
+        def emit(self, ins):
+            e(ins)
+            if self.pending:
+                e(self.pending.pop(0))
+
+        def start(self):
+            if self.inits is not None and 0 <= self.t < len(self.inits):
+                self.emit(f'  v_mad_u64_u32 {self.acc()}, vcc, {self.inits[self.t]}, 1, 0')
+                self.fresh = False
+
+        def close(self):
+            for ins in self.pending:
+                e(ins)
+            a = self.acc()
+            tail = []
+            if self.t != self.t0:
+                tail.append(f'  v_lshl_add_u64 {a}, {a}, 0, {CCARRY}')
+            if 0 <= self.t < len(self.outs):
+                tail.append(f'  v_and_b32_e32 {self.outs[self.t]}, {hex(MASK)}, v{a[2:a.index(":")]}')
+            if not (self.nocarry_last and self.t == self.t_last):
+                tail.append(f'  v_ashrrev_i64 {CCARRY}, {B}, {a}')
+            self.pending = tail
+            self.t += 1
+            self.fresh = True
+            if self.t <= self.t_last:
+                self.start()
+
+        def column(self, s, reg):
+            t = (8 * s - self.base) // B
+            while t > self.t:
+                self.close()
+            if not self.begun:
+                self.begun = True
+                self.start()
+            sh = 8 * s - self.base - B * t
+            mul = NEG(sh) if self.neg else POW(sh)
+            a = self.acc()
+            self.emit(f'  v_mad_i64_i32 {a}, vcc, {reg}, {mul}, {"0" if self.fresh else a}')
+            self.fresh = False
+
+        def finish(self):
+            while self.t <= self.t_last:
+                self.close()
+            for ins in self.pending:
+                e(ins)
+            self.pending = []
+
+    P1_TILES = [(1, m, [k for k in range(5) if m - k <= 1]) for m in range(5)]
+    P2_TILES = [(2, m, [k for k in range(5) if m >= k]) for m in range(5)]
+
+    def mfma_barrett(Tl, q3out, clamp, prefetched=False):
+        """product 1: q3 = Barrett's quotient of T (Tl: 2K limbs, Tl[K-1] < 2^29 allowed) -> q3out (K regs,
+        may be Tl[K:]); clamp: q3 = -1 (q1 = 0) -> 0; prefetched: its first A-tile reads are in flight"""
+        if not prefetched:
+            prefetch(*P1_TILES[0])
+        orpack(Tl[K - 1:2 * K], 0, 34, [0x80808080] * 34, norm0=True)
+        e(f'  v_bfe_u32 {D[34]}, {Tl[K - 1]}, 28, 1')              # c = bit 28 of q1[0] -> digit 16 c at byte 137
+        e(f'  v_lshl_or_b32 {D[34]}, {D[34]}, 12, 1')               # and the constant digit 1 at byte 136
+        for w in range(35, 40):
+            e(f'  v_mov_b32_e32 {D[w]}, 0')
+        swap_operands()
+        ch = Chunks(QBIT, (8 * S1_LO - QBIT) // B, 39, q3out, neg=False)
+        for m in range(5):
+            mtile_mfmas(*P1_TILES[m], nxt=P1_TILES[m + 1] if m < 4 else P2_TILES[0])
+            for rho in range(32):
+                ch.column(S1_LO + 32 * m + rho, col_reg(rho))
+        ch.finish()
+        if clamp:                                  # final carry = 0, or -1 when q1 = 0 (q3 = -1 -> 0)
+            e(f'  v_not_b32_e32 v{XA + 36}, v{XA + 38}')
+            for r in q3out:
+                e(f'  v_and_b32_e32 {r}, {r}, v{XA + 36}')
+        return q3out
+
+    def mfma_remainder(Tl, q3, rout, nxt_p1):
+        """product 2: r = (T - q3 P) mod b^K -> rout (may be Tl[:K]); the product-2 tile-0 reads are already
+        in flight; nxt_p1: prefetch product 1's first tiles at the end (the next Barrett)"""
+        orpack(q3, 8, 33, [0x80808000] + [0x80808080] * 32, lead_one=True)
+        e(f'  v_mov_b32_e32 {D[33]}, 0x80')          # q3 byte 131 (zero, offset) at byte 132; pads 0
+        for w in range(34, 40):
+            e(f'  v_mov_b32_e32 {D[w]}, 0')
+        swap_operands()
+        # matrix column s holds column s - 1 of q3 P (bits 8 s - 8): P'[s - i] is a plain Toeplitz band
+        ch = Chunks(8, 0, K - 1, rout, neg=True, inits=Tl[:K], nocarry_last=True)
+        for m in range(5):
+            nxt = P2_TILES[m + 1] if m < 4 else (P1_TILES[0] if nxt_p1 else None)
+            mtile_mfmas(*P2_TILES[m], nxt=nxt)
+            for rho in range(32):
+                s = 32 * m + rho
+                if 1 <= s <= 130:
+                    ch.column(s, col_reg(rho))
+        ch.finish()
+
+    # ---- prologue ------------------------------------------------------------
+    e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
+    e('.amdhsa_code_object_version 5')
+    e('.text')
+    e(f'.globl {name}')
+    e('.p2align 8')
+    e(f'.type {name},@function')
+    e(f'{name}:')
+    e('  s_load_dwordx2 s[4:5], s[0:1], 0x0')
+    e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
+    e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
+    e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
+    e('  s_waitcnt lgkmcnt(0)')
+    off, sreg, rem = 0, SNP, K
+    for width in (16, 8, 4, 2, 1):
+        while rem >= width:
+            suffix = f"x{width}" if width > 1 else ""
+            dst = f"s[{sreg}:{sreg + width - 1}]" if width > 1 else f"s{sreg}"
+            e(f'  s_load_dword{suffix} {dst}, s[8:9], {hex(off)}')
+            off += 4 * width
+            sreg += width
+            rem -= width
+    for i in range(8):
+        e(f'  s_mov_b32 s{SPOW + i}, {hex(1 << (4 * i))}')
+    for i in range(7):
+        e(f'  s_mov_b32 s{SNEG + i}, {hex((-(1 << (4 * i))) & 0xFFFFFFFF)}')
+    e(f'  s_mov_b32 s35, {hex(MASK)}')
+    e('  s_lshl_b32 s14, s2, 10')
+    e(f'  v_lshlrev_b32_e32 v{V_GOFF}, 2, v{V_TID}')
+    e(f'  v_add_u32_e32 v{V_GOFF}, s14, v{V_GOFF}')
+    # LDS tile image: 5 x 4 KB, each thread one dwordx4 per 4 KB
+    e(f'  v_lshlrev_b32_e32 v10, 4, v{V_TID}')
+    for it in range(LDS_BYTES // 4096):
+        e(f'  global_load_dwordx4 v[2:5], v10, s[8:9] offset:{TILE_OFF}')
+        e('  s_waitcnt vmcnt(0)')
+        e('  ds_write_b128 v10, v[2:5]')
+        if it != LDS_BYTES // 4096 - 1:
+            e('  v_add_u32_e32 v10, 0x1000, v10')
+    e(f'  v_and_b32_e32 v{V_LDS}, 63, v{V_TID}')
+    e(f'  v_lshlrev_b32_e32 v{V_LDS}, 4, v{V_LDS}')
+    e('  s_waitcnt lgkmcnt(0)')
+    e('  s_barrier')
+
+    e('.Lprog:')
+    e('  s_load_dwordx2 s[14:15], s[6:7], 0x0')
+    e('  s_add_u32 s6, s6, 8')
+    e('  s_addc_u32 s7, s7, 0')
+    e('  s_waitcnt lgkmcnt(0)')
+    for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (22, '.Lloadp'), (23, '.Lstorep')):
+        e(f'  s_cmp_eq_u32 s14, {code}')
+        e(f'  s_cbranch_scc1 {lab}')
+    e('  s_branch .Lend')
+
+    def slot_addr():
+        e('  s_mul_i32 s16, s15, s11')
+        e('  s_mul_hi_u32 s17, s15, s11')
+        e('  s_add_u32 s16, s4, s16')
+        e('  s_addc_u32 s17, s5, s17')
+
+    def load_limbs(regs):
+        slot_addr()
+        for k, r in enumerate(regs):
+            e(f'  global_load_dword {r}, v{V_GOFF}, s[16:17]')
+            if k != len(regs) - 1:
+                e('  s_add_u32 s16, s16, s10')
+                e('  s_addc_u32 s17, s17, 0')
+        e('  s_waitcnt vmcnt(0)')
+
+    def store_limbs(regs):
+        slot_addr()
+        for k, r in enumerate(regs):
+            e(f'  global_store_dword v{V_GOFF}, {r}, s[16:17]')
+            if k != len(regs) - 1:
+                e('  s_add_u32 s16, s16, s10')
+                e('  s_addc_u32 s17, s17, 0')
+        e('  s_waitcnt vmcnt(0)')
+
+    ncall = [0]
+
+    def call(label):
+        n = ncall[0]
+        ncall[0] += 1
+        e('  s_getpc_b64 s[2:3]')
+        e(f'.Lpc{n}:')
+        e(f'  s_add_u32 s2, s2, {label}-.Lpc{n}')
+        e('  s_addc_u32 s3, s3, 0')
+        e('  s_swappc_b64 s[12:13], s[2:3]')
+
+    e('.Lloadx:')
+    load_limbs(X0 + X1)
+    e('  s_branch .Lprog')
+    e('.Lstorex:')
+    store_limbs(X0 + X1)
+    e('  s_branch .Lprog')
+
+    # SQR: V = 2 x0 x1, T = x0^2, reduce
+    e('.Lsqr:')
+    e('  s_mov_b32 s19, s15')
+    e('.Lsqr_loop:')
+    e('  s_cmp_eq_u32 s19, 0')
+    e('  s_cbranch_scc1 .Lprog')
+    cols = []
+    for c in range(2 * K):
+        terms = [(X0[i], X1[c - i]) for i in range(K) if 0 <= c - i < K]
+        cols.append({'terms': terms, 'dbl': True, 'out': V[c], 'last': c == 2 * K - 1})
+    columns(cols)
+    cols = []
+    for c in range(2 * K):
+        terms = [(X0[i], X0[c - i]) for i in range(K) if i < c - i < K]
+        sq = X0[c // 2] if c % 2 == 0 and c // 2 < K else None
+        col = {'terms': terms, 'out': T[c], 'last': c == 2 * K - 1}
+        if terms:
+            col['dbl'] = True
+            if sq:
+                col['sq'] = sq
+        elif sq:
+            col['terms'] = [(sq, sq)]
+        cols.append(col)
+    columns(cols)
+    call('.Lreduce')
+    e('  s_sub_u32 s19, s19, 1')
+    e('  s_branch .Lsqr_loop')
+
+    # MUL slot: y0 -> T[0..K-1], y1 -> T[K..]; W = x0 y1 + x1 y0 -> V; T = x0 y0 -> (XB, T[K..]); move
+    e('.Lmul:')
+    Y0, Y1 = T[:K], T[K:]
+    load_limbs(Y0 + Y1)
+    columns(product_cols(X0, Y1, 2 * K, V, a2=X1, b2=Y0))
+    TM = X1 + T[K:]                              # x1, y1 dead
+    columns(product_cols(X0, Y0, 2 * K, TM))
+    move(T[:K], X1)
+    call('.Lreduce')
+    e('  s_branch .Lprog')
+
+    # LOADP slot: plain X -> T -> (q3 = x1, r = x0)
+    e('.Lloadp:')
+    load_limbs(T)
+    q3 = mfma_barrett(T, T[K:], clamp=True)
+    mfma_remainder(T, q3, T[:K], nxt_p1=False)
+    move(X0, T[:K])
+    move(X1, T[K:2 * K])
+    e('  s_branch .Lprog')
+
+    # STOREP slot: x0 + x1 P with -P in SGPRs (scratch -x1 in T[0..K-1]; out V)
+    e('.Lstorep:')
+    NX1 = T[:K]
+    for i in range(K):
+        e(f'  v_sub_u32_e32 {NX1[i]}, 0, {X1[i]}')
+    cols = []
+    for c in range(2 * K):
+        terms = [(X0[c], '1')] if c < K else []
+        terms += [(NX1[i], NP(c - i)) for i in range(K) if 0 <= c - i < K]
+        cols.append({'terms': terms, 'out': V[c], 'last': c == 2 * K - 1})
+    columns(cols, signed=True)
+    store_limbs(V)
+    e('  s_branch .Lprog')
+
+    e('.Lend:')
+    e('  s_endpgm')
+
+    # reduce (SQR, MUL): T (x0^2 or x0 y0), V (cross terms) -> x0 = T mod P, x1 = (V + T div P) mod P
+    e('.Lreduce:')
+    q3 = mfma_barrett(T, T[K:], clamp=True)             # u1 -> T[K..2K-1]
+    mfma_remainder(T, q3, T[:K], nxt_p1=True)           # u0 -> T[0..K-1]
+    for i in range(K):
+        e(f'  v_add_u32_e32 {V[i]}, {V[i]}, {q3[i]}')     # V += u1 (limbs < 2^29)
+    q3b = mfma_barrett(V, V[K:], clamp=False, prefetched=True)
+    mfma_remainder(V, q3b, V[:K], nxt_p1=False)
+    move(X0, T[:K])
+    move(X1, V[:K])
+    e('  s_setpc_b64 s[12:13]')
+
+    e(f'.Lfunc_end_{name}:')
+    e(f'  .size {name}, .Lfunc_end_{name}-{name}')
+    e('')
+    o.extend(_descriptor(name, LDS_BYTES, NVGPR, NSGPR).splitlines())
+    return "\n".join(o) + "\n"
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--name', default='fthe_padic_m37')
+    ap.add_argument('-o', '--out', required=True)
+    a = ap.parse_args()
+    with open(a.out, 'w') as f:
+        f.write(gen_padic_mfma(a.name))

@@ -1,6 +1,8 @@
 // Standalone bring-up test + timing of the P-adic exponentiation kernel (fedtree_amd/csrc/gen_padic.py).
 // Build: hipcc --offload-arch=gfx950 -O2 -idirafter /opt/conda/include tools/test_padic.cpp -l:libgmp.so.10 -o tools/bin/test_padic
-// Run:   tools/bin/test_padic <hsaco> [lanes] [mode]     mode 0: y^P, y < P (encrypt); 1: c^(P-1), c < P^2
+// Run:   tools/bin/test_padic <hsaco> [lanes] [mode] [kernel]   mode 0: y^P, y < P (encrypt); 1: c^(P-1), c < P^2;
+//        bring-up programs: 2: LOADP; STOREP (c < P^2), 3: LOADP; SQR 1; STOREP, 4: LOADP; SQR 1; MUL IN; STOREP
+//        kernel: fthe_padic_k37 (default) or fthe_padic_m37 (gen_padic_mfma.py: ctx carries the LDS tile image)
 // Checks sampled lanes against GMP's mpz_powm and prints the launch time and products per second.
 #include <hip/hip_runtime.h>
 #include <gmp.h>
@@ -9,6 +11,9 @@
 #include <cstdlib>
 #include <fstream>
 #include <vector>
+#include <cstring>
+#include <string>
+#include "../fedtree_amd/csrc/padic_tiles.hpp"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     printf("HIP error %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -66,13 +71,14 @@ int main(int argc, char **argv) {
     const char *path = argc > 1 ? argv[1] : "padic.hsaco";
     int L = argc > 2 ? atoi(argv[2]) : 65536;
     int mode = argc > 3 ? atoi(argv[3]) : 0;
+    std::string kname = argc > 4 ? argv[4] : "fthe_padic_k37";
     if (L % 256) { printf("lanes must be a multiple of 256\n"); return 2; }
     std::ifstream f(path, std::ios::binary);
     std::vector<char> blob((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
     if (blob.empty()) { printf("no code object at %s\n", path); return 2; }
     hipModule_t mod; hipFunction_t fn;
     CHECK(hipModuleLoadData(&mod, blob.data()));
-    CHECK(hipModuleGetFunction(&fn, mod, "fthe_padic_k37"));
+    CHECK(hipModuleGetFunction(&fn, mod, kname.c_str()));
 
     gmp_randstate_t rs; gmp_randinit_mt(rs); gmp_randseed_ui(rs, 20261016 + mode);
     mpz_t P, P2, mu, t, x, e, got, want;
@@ -80,27 +86,41 @@ int main(int argc, char **argv) {
     mpz_urandomb(P, rs, 1024); mpz_setbit(P, 1023); mpz_setbit(P, 1022); mpz_setbit(P, 0);
     mpz_mul(P2, P, P);
     mpz_set_ui(t, 1); mpz_mul_2exp(t, t, 2 * B * K); mpz_fdiv_q(mu, t, P);
-    std::vector<uint32_t> ctx(2 * K + 4, 0), pl(K);
+    std::vector<uint32_t> ctx(128 + padic_tiles::kImageBytes / 4, 0), pl(K);
     to_limbs(P, pl.data(), K);
     for (int j = 0; j < K; j++) ctx[j] = (uint32_t)(-(int32_t)pl[j]);
     to_limbs(mu, ctx.data() + K + 3, K + 1);
-    if (mode == 0) mpz_set(e, P); else mpz_sub_ui(e, P, 1);
+    {
+        std::vector<uint8_t> img = padic_tiles::build(P);
+        if (img.empty()) { printf("tile image failed\n"); return 2; }
+        memcpy(ctx.data() + 128, img.data(), img.size());
+    }
+    if (mode == 0) mpz_set(e, P); else if (mode == 1) mpz_sub_ui(e, P, 1);
+    else mpz_set_ui(e, mode == 2 ? 1 : mode == 3 ? 2 : 3);
 
     const int W = 6, TAB = 2, SQ = 1, IN = 0, OUT = TAB + (1 << (W - 1));
     const int NSLOTS = OUT + 1;
     Prog p;
-    p.op(22, IN); p.pow(e, TAB, SQ, W); p.op(23, OUT); p.op(0, 0);
+    if (mode == 2) { p.op(22, IN); p.op(23, OUT); }
+    else if (mode == 5) { p.op(22, IN); p.op(2, OUT); }          // raw digits x0 | x1 (dumped)
+    else if (mode == 3) { p.op(22, IN); p.op(3, 1); p.op(23, OUT); }
+    else if (mode == 4) { p.op(22, IN); p.op(2, TAB); p.op(3, 1); p.op(4, TAB); p.op(23, OUT); }
+    else { p.op(22, IN); p.pow(e, TAB, SQ, W); p.op(23, OUT); }
+    p.op(0, 0);
 
     size_t slot_words = (size_t)S * L;
     std::vector<uint32_t> in(slot_words), out(slot_words);
     std::vector<uint32_t> lb(S);
     std::vector<int> sample;
-    for (int g = 0; g < L; g += L / 256) sample.push_back(g);
+    for (int g = 0; g < 8; g++) sample.push_back(g);
+    for (int g = 8; g < L; g += L / 256) sample.push_back(g);
     sample.push_back(L - 1);
     std::vector<std::vector<uint32_t>> xs(L);
     for (int g = 0; g < L; g++) {
         if (g == 0) mpz_set_ui(x, 1);
         else if (g == 1) { if (mode == 0) mpz_sub_ui(x, P, 1); else mpz_sub_ui(x, P2, 1); }
+        else if (g == 2) mpz_set_ui(x, 2);
+        else if (g == 3 && mode >= 2) mpz_sub_ui(x, P2, 1);
         else if (mode == 0) mpz_urandomm(x, rs, P);
         else mpz_urandomm(x, rs, P2);
         to_limbs(x, lb.data(), S);
@@ -131,6 +151,19 @@ int main(int argc, char **argv) {
         if (ms < best) best = ms;
     }
     CHECK(hipMemcpy(out.data(), d_slots + OUT * slot_words, slot_words * 4, hipMemcpyDeviceToHost));
+    if (mode == 5) {                                            // lanes 0..7: P, input, raw output limbs
+        FILE *fo = fopen("gpurun_out/padic_dump.txt", "w");
+        gmp_fprintf(fo, "P %Zx\n", P);
+        for (int g = 0; g < 8; g++) {
+            fprintf(fo, "in %d", g);
+            for (int k = 0; k < S; k++) fprintf(fo, " %x", in[(size_t)k * L + g]);
+            fprintf(fo, "\nout %d", g);
+            for (int k = 0; k < S; k++) fprintf(fo, " %x", out[(size_t)k * L + g]);
+            fprintf(fo, "\n");
+        }
+        fclose(fo);
+        return 0;
+    }
     int bad = 0;
     for (int g : sample) {
         for (int k = 0; k < S; k++) lb[k] = out[(size_t)k * L + g];
