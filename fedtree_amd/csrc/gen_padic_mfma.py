@@ -400,6 +400,15 @@ def gen_padic_mfma(name: str) -> str:
     e(f'  v_lshlrev_b32_e32 v{V_LDS}, 4, v{V_LDS}')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
+    if "desync" in AB:
+        # odd workgroups start ~16K cycles late: the two waves of a SIMD then reach their matrix-core
+        # phases at different times (s_sleep spends no issue slots)
+        e('  s_bitcmp1_b32 s2, 0')
+        e('  s_cbranch_scc0 .Ldesync_done')
+        nsl = int(os.environ.get("FTHE_GEN_M37_SLEEPS", "2"))
+        for _ in range(nsl):
+            e('  s_sleep 127')
+        e('.Ldesync_done:')
 
     e('.Lprog:')
     e('  s_load_dwordx2 s[14:15], s[6:7], 0x0')
