@@ -400,12 +400,12 @@ def gen_padic_mfma(name: str) -> str:
     e(f'  v_lshlrev_b32_e32 v{V_LDS}, 4, v{V_LDS}')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
-    if "desync" in AB:
-        # odd workgroups start ~16K cycles late: the two waves of a SIMD then reach their matrix-core
-        # phases at different times (s_sleep spends no issue slots)
+    if "nodesync" not in AB:
+        # odd workgroups start ~8K cycles late: the two waves of a SIMD then reach their matrix-core
+        # phases at different times (s_sleep spends no issue slots); 1.5% (profiles/r02zt_desync_ab.jsonl)
         e('  s_bitcmp1_b32 s2, 0')
         e('  s_cbranch_scc0 .Ldesync_done')
-        nsl = int(os.environ.get("FTHE_GEN_M37_SLEEPS", "2"))
+        nsl = int(os.environ.get("FTHE_GEN_M37_SLEEPS", "1"))
         for _ in range(nsl):
             e('  s_sleep 127')
         e('.Ldesync_done:')
