@@ -617,15 +617,15 @@ static int padic_digits(const mpz_t P, Shape sh) {
     if (sh.S == 37 && b >= 505 && b <= 516) return kPadicSmallK;
     return 0;
 }
-// K = 37 also carries the LDS tile image of fthe_padic_m37 (padic_tiles.hpp) at byte 512 of the context
-// when FTHE_PADIC_MFMA is set (opt-in while it is being tuned); the MFMA kernel then runs the key's
-// exponentiation programs.
+// K = 37 also carries the LDS tile image of fthe_padic_m37 (padic_tiles.hpp) at byte 512 of the context,
+// and the MFMA-Barrett kernel then runs the key's exponentiation programs; FTHE_NO_PADIC_MFMA=1 keeps
+// them on fthe_padic_k37 (bit-identical results).
 static int upload_padic(DevMod &d, const mpz_t P, int K) {
     Mpz P2; mpz_mul(P2, P, P);
     d.m.init(P2, Shape{2 * K, 28, 1});
     const int pad = ((20 + K + 3) & ~3) - 20 - K;          // gen_padic.py: mu from an aligned SGPR
     std::vector<uint8_t> tiles;
-    if (K == kPadicK && getenv("FTHE_PADIC_MFMA")) tiles = padic_tiles::build(P);
+    if (K == kPadicK && !getenv("FTHE_NO_PADIC_MFMA")) tiles = padic_tiles::build(P);
     std::vector<uint32_t> w(tiles.empty() ? (size_t)2 * K + 1 + pad : 128 + tiles.size() / 4, 0u), l = to_limbs(P, K, 28);
     if (!tiles.empty()) std::memcpy(w.data() + 128, tiles.data(), tiles.size());
     for (int j = 0; j < K; j++) w[j] = (uint32_t)(-(int32_t)l[j]);
@@ -1297,8 +1297,10 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     // programs without fixed-base table ops (the key's own) may take the MFMA-Barrett P-adic kernel
-    int vi = variant_index(table_free && mod.kernel_S_mfma ? mod.kernel_S_mfma : mod.kernel_S ? mod.kernel_S : S);
+    const bool mfma = table_free && mod.kernel_S_mfma;
+    int vi = variant_index(mfma ? mod.kernel_S_mfma : mod.kernel_S ? mod.kernel_S : S);
     if (vi < 0) return FTHE_ERR_UNSUPPORTED;
+    if (mfma) lane_exec = -1;             // the v_mad counts of padic_exec are fthe_padic_k37's
     // only the workgroups that hold live elements (slot strides stay those of L)
     if (live > (size_t)L) return FTHE_ERR_ARG;
     if (live == 0) return FTHE_OK;

@@ -1,4 +1,5 @@
-"""The P-adic exponentiation kernel (fthe_padic_k37) behind the key holder's CRT encrypt
+"""The VALU P-adic exponentiation kernel (fthe_padic_k37; the key holder's default is its
+MFMA-Barrett variant fthe_padic_m37, tests/test_gpu_padic_mfma.py, so these keys set FTHE_NO_PADIC_MFMA) behind the key holder's CRT encrypt
 and decrypt at Paillier-2048: the same ciphertexts and plaintexts as the Montgomery s74 programs it
 replaces (FTHE_NO_PADIC=1 at key set-up restores those), for injected r at the extremes and random r,
 and its launches really run (profiling counters of the variant).  Integer work: exact equality.
@@ -20,7 +21,11 @@ SEED = 20261016
 def keys(request):
     from fedtree_amd.paillier import Device, Paillier
     dev = Device(0)
-    pa = Paillier(dev).keygen(request.param, seed=SEED)
+    os.environ["FTHE_NO_PADIC_MFMA"] = "1"
+    try:
+        pa = Paillier(dev).keygen(request.param, seed=SEED)
+    finally:
+        del os.environ["FTHE_NO_PADIC_MFMA"]
     os.environ["FTHE_NO_PADIC"] = "1"
     try:
         pm = Paillier.from_primes(pa.p, pa.q, dev)
@@ -122,7 +127,7 @@ def _padic_launches(dev, fn):
         vals = [ctypes.c_double() for _ in range(7)]
         assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
         launches = {}
-        for v in (1037, 1019):
+        for v in (1037, 1019, 1137):
             ms, nl = ctypes.c_double(), ctypes.c_double()
             assert lib.fthe_prof_variant(dev.ctx, v, ctypes.byref(ms), ctypes.byref(nl)) == 0
             launches[v] = nl.value
@@ -145,8 +150,9 @@ def _prime_of_bits(rng, bits):
 # Prime sizes at the edges of the P-adic digit ranges (fthe.hip padic_digits): K = 37 takes P of
 # 1009..1030 bits, K = 19 P of 505..514 bits (P of 515-516 bits puts the key's CRT halves on the s74
 # shape, kernel_shape_for_bits); one bit outside, the key runs the Montgomery programs.
+# (K = 37 keys run the MFMA-Barrett variant fthe_padic_m37 = 1137 by default: the edges hold for it too)
 @pytest.mark.parametrize("pbits,qbits,variant", [
-    (1009, 1030, 1037), (1030, 1030, 1037), (1008, 1030, None), (1030, 1031, None),
+    (1009, 1030, 1137), (1030, 1030, 1137), (1008, 1030, None), (1030, 1031, None),
     (505, 514, 1019), (514, 514, 1019), (504, 514, None), (505, 515, None)])
 def test_digit_range_edges_vs_c_oracle(coracle, pbits, qbits, variant):
     """Keys whose primes sit on (or one bit past) the P-adic kernel's range: the largest P has the
@@ -171,7 +177,10 @@ def test_digit_range_edges_vs_c_oracle(coracle, pbits, qbits, variant):
     (low, full), dl = _padic_launches(dev, lambda: pl.decrypt_u64(c, full=True))
     cd, el = _padic_launches(dev, lambda: pl.encrypt_u64(m, seed=11))      # device randomness (direct y)
     for got in (launches, dl, el):                 # y_p^p and y_q^q, or c^(p-1) and c^(q-1)
-        assert got == ({1037: 0, 1019: 0} if variant is None else {1037: 0, 1019: 0, variant: 2}), got
+        want = {1037: 0, 1019: 0, 1137: 0}
+        if variant is not None:
+            want[variant] = 2
+        assert got == want, got
     assert np.array_equal(low, m)
     idx = np.r_[0:48, cnt - 16:cnt]
     r_or = np.zeros((len(idx), 2 * hw), np.uint32)
@@ -202,7 +211,7 @@ def test_public_encrypt_padic_paillier1024(keys):
     m[:3] = [0, 1, 2**64 - 2]
     rw = pyoracle.ints_to_words(rs, pa.n_words)
     ca, launches = _padic_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True))
-    assert launches == {1037: 1, 1019: 0}
+    assert launches == {1037: 1, 1019: 0, 1137: 0}
     assert np.array_equal(ca, pm.encrypt_u64(m, r=rw, public=True))
     n2 = n * n
     for i in (0, 1, 2, 3, 4, 5, cnt - 1):             # paillier.cpp:134-137 with g = n + 1

@@ -1,4 +1,4 @@
-"""The opt-in matrix-core Barrett P-adic kernel (fthe_padic_m37, FTHE_PADIC_MFMA=1 at key set-up)
+"""The matrix-core Barrett P-adic kernel (fthe_padic_m37, the key holder's default at Paillier-2048)
 through the engine: the same Paillier-2048 ciphertexts and plaintexts as the Montgomery s74 programs
 (FTHE_NO_PADIC=1) for injected r at the extremes and random r, device randomness that decrypts, the
 Paillier-1024 public form with P = n, and its launches really run on the variant (profiling counters).
@@ -33,7 +33,7 @@ def _key_with(env, fn):
 def keys():
     from fedtree_amd.paillier import Device, Paillier
     dev = Device(0)
-    pa = _key_with({"FTHE_PADIC_MFMA": "1"}, lambda: Paillier(dev).keygen(2048, seed=SEED))
+    pa = _key_with({}, lambda: Paillier(dev).keygen(2048, seed=SEED))
     pm = _key_with({"FTHE_NO_PADIC": "1"}, lambda: Paillier.from_primes(pa.p, pa.q, dev))
     return dev, pa, pm
 
@@ -87,7 +87,7 @@ def test_mfma_public_paillier1024_p_equals_n():
     kernel too, with the same ciphertexts as the Montgomery program and the formula of paillier.cpp:134-137"""
     from fedtree_amd.paillier import Device, Paillier
     dev = Device(0)
-    pa = _key_with({"FTHE_PADIC_MFMA": "1"}, lambda: Paillier(dev).keygen(1024, seed=SEED + 2))
+    pa = _key_with({}, lambda: Paillier(dev).keygen(1024, seed=SEED + 2))
     pm = _key_with({"FTHE_NO_PADIC": "1"}, lambda: Paillier.from_primes(pa.p, pa.q, dev))
     rng = np.random.default_rng(SEED + 3)
     n = pa.modulus
