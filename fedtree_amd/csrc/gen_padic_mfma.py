@@ -220,36 +220,67 @@ def gen_padic_mfma(name: str) -> str:
         for n in range(min(2, len(ks))):
             rd(prod, m, ks[n], n)
 
-    def mtile_mfmas(prod, m, ks, nxt=None):
-        """the MFMAs of M-tile m over K-tiles ks (both lane groups); its first two A tiles are already in
-        flight (prefetch), the rest rotate through three buffers one step ahead.  nxt = (prod, m, ks) of
-        the next M-tile: its first reads go out as soon as this tile's MFMAs have read their operands."""
+    GB0, GB1 = TT + 38, TT + 54                  # second accumulator set v[138:153], v[154:169] (T[38..69])
+
+    def issue_tile(prod, m, ks, G0x, G1x, prefetched=True):
+        """the MFMAs of M-tile m over K-tiles ks (both lane groups) into accumulators G0x, G1x; with
+        prefetched its first two A-tile reads are already in flight, the rest rotate through three
+        buffers one step ahead"""
         L = len(ks)
+        if not prefetched:
+            prefetch(prod, m, ks)
         for n, k in enumerate(ks):
             if n + 2 < L:
                 rd(prod, m, ks[n + 2], n + 2)
             e(f'  s_waitcnt lgkmcnt({min(L, n + 3) - n - 1})')
             buf = VA[n % 3]
-            for g, G in ((0, G0), (1, G1)):
+            for g, G in ((0, G0x), (1, G1x)):
                 src_c = "0" if n == 0 else f"v[{G}:{G + 15}]"
                 bo = 8 * k + 4 * g
                 if "nomfma" not in AB:
                     e(f'  v_mfma_i32_32x32x32_i8 v[{G}:{G + 15}], v[{buf}:{buf + 3}], v[{XB + bo}:{XB + bo + 3}], {src_c}')
-        # results -> VALU: wait out the last MFMA (8-pass XDL), then exchange the halves
+
+    def exchange(G0x, G1x):
+        """results -> VALU: wait out the last MFMA writing them (8-pass XDL), then exchange the halves"""
         if "nonop" not in AB:
             e('  s_nop 7')
             e('  s_nop 7')
             e('  s_nop 7')
-        if nxt is not None:
-            prefetch(*nxt)
         for r in range(16 if "noswap" not in AB else 0):
-            e(f'  v_permlane32_swap_b32_e32 v{G0 + r}, v{G1 + r}')
+            e(f'  v_permlane32_swap_b32_e32 v{G0x + r}, v{G1x + r}')
         e('  s_nop 1')
 
-    def col_reg(rho):
+    def mtile_mfmas(prod, m, ks, nxt=None):
+        """one M-tile, issued and then waited for (single accumulator set)"""
+        issue_tile(prod, m, ks, G0, G1)
+        if nxt is not None:
+            prefetch(*nxt)
+        exchange(G0, G1)
+
+    def col_reg(rho, G0x=G0, G1x=G1):
         """register of column rho (0..31) of the M-tile after the exchange"""
         rr = (rho & 3) + 4 * (rho >> 3)
-        return f"v{(G1 if (rho >> 2) & 1 else G0) + rr}"
+        return f"v{(G1x if (rho >> 2) & 1 else G0x) + rr}"
+
+    def run_tiles(tiles, consume, nxt, dbuf):
+        """all M-tiles of a product: consume(m, col_reg_of_the_tile) after each; dbuf: two accumulator sets,
+        tile m+1's MFMAs issued before tile m's results are folded, so the matrix core works while the
+        lane does (needs T[38..69] free); tile 0's first A tiles are prefetched by the caller"""
+        if not dbuf:
+            for m in range(5):
+                mtile_mfmas(*tiles[m], nxt=tiles[m + 1] if m < 4 else nxt)
+                consume(m, col_reg)
+            return
+        sets = ((G0, G1), (GB0, GB1))
+        issue_tile(*tiles[0], *sets[0])
+        for m in range(5):
+            if m < 4:
+                issue_tile(*tiles[m + 1], *sets[(m + 1) % 2], prefetched=False)
+            elif nxt is not None:
+                prefetch(*nxt)
+            ga, gb = sets[m % 2]
+            exchange(ga, gb)
+            consume(m, lambda rho, ga=ga, gb=gb: col_reg(rho, ga, gb))
 
     class Chunks:
         """column sums -> 28-bit limbs.  Chunk t (bits [base + 28 t, +28)) sums its columns (x 2^sh) into its
@@ -316,9 +347,10 @@ def gen_padic_mfma(name: str) -> str:
     P1_TILES = [(1, m, [k for k in range(5) if m - k <= 1]) for m in range(5)]
     P2_TILES = [(2, m, [k for k in range(5) if m >= k]) for m in range(5)]
 
-    def mfma_barrett(Tl, q3out, clamp, prefetched=False):
+    def mfma_barrett(Tl, q3out, clamp, prefetched=False, dbuf=False):
         """product 1: q3 = Barrett's quotient of T (Tl: 2K limbs, Tl[K-1] < 2^29 allowed) -> q3out (K regs,
-        may be Tl[K:]); clamp: q3 = -1 (q1 = 0) -> 0; prefetched: its first A-tile reads are in flight"""
+        may be Tl[K:]); clamp: q3 = -1 (q1 = 0) -> 0; prefetched: its first A-tile reads are in flight;
+        dbuf: double-buffered accumulators (T[38..69] free)"""
         if not prefetched:
             prefetch(*P1_TILES[0])
         orpack(Tl[K - 1:2 * K], 0, 34, [0x80808080] * 34, norm0=True)
@@ -328,10 +360,11 @@ def gen_padic_mfma(name: str) -> str:
             e(f'  v_mov_b32_e32 {D[w]}, 0')
         swap_operands()
         ch = Chunks(QBIT, (8 * S1_LO - QBIT) // B, 39, q3out, neg=False)
-        for m in range(5):
-            mtile_mfmas(*P1_TILES[m], nxt=P1_TILES[m + 1] if m < 4 else P2_TILES[0])
+
+        def consume(m, creg):
             for rho in range(32):
-                ch.column(S1_LO + 32 * m + rho, col_reg(rho))
+                ch.column(S1_LO + 32 * m + rho, creg(rho))
+        run_tiles(P1_TILES, consume, P2_TILES[0], dbuf)
         ch.finish()
         if clamp:                                  # final carry = 0, or -1 when q1 = 0 (q3 = -1 -> 0)
             e(f'  v_not_b32_e32 v{XA + 36}, v{XA + 38}')
@@ -339,23 +372,26 @@ def gen_padic_mfma(name: str) -> str:
                 e(f'  v_and_b32_e32 {r}, {r}, v{XA + 36}')
         return q3out
 
-    def mfma_remainder(Tl, q3, rout, nxt_p1):
+    def mfma_remainder(Tl, q3, rout, nxt_p1, dbuf=False, after_pack=None):
         """product 2: r = (T - q3 P) mod b^K -> rout (may be Tl[:K]); the product-2 tile-0 reads are already
-        in flight; nxt_p1: prefetch product 1's first tiles at the end (the next Barrett)"""
+        in flight; nxt_p1: prefetch product 1's first tiles at the end (the next Barrett); after_pack: the
+        caller's last use of the q3 limbs (dbuf may then take their registers)"""
         orpack(q3, 8, 33, [0x80808000] + [0x80808080] * 32, lead_one=True)
+        if after_pack:
+            after_pack()
         e(f'  v_mov_b32_e32 {D[33]}, 0x80')          # q3 byte 131 (zero, offset) at byte 132; pads 0
         for w in range(34, 40):
             e(f'  v_mov_b32_e32 {D[w]}, 0')
         swap_operands()
         # matrix column s holds column s - 1 of q3 P (bits 8 s - 8): P'[s - i] is a plain Toeplitz band
         ch = Chunks(8, 0, K - 1, rout, neg=True, inits=Tl[:K], nocarry_last=True)
-        for m in range(5):
-            nxt = P2_TILES[m + 1] if m < 4 else (P1_TILES[0] if nxt_p1 else None)
-            mtile_mfmas(*P2_TILES[m], nxt=nxt)
+
+        def consume(m, creg):
             for rho in range(32):
                 s = 32 * m + rho
                 if 1 <= s <= 130:
-                    ch.column(s, col_reg(rho))
+                    ch.column(s, creg(rho))
+        run_tiles(P2_TILES, consume, P1_TILES[0] if nxt_p1 else None, dbuf)
         ch.finish()
 
     # ---- prologue ------------------------------------------------------------
@@ -530,11 +566,14 @@ def gen_padic_mfma(name: str) -> str:
     # reduce (SQR, MUL): T (x0^2 or x0 y0), V (cross terms) -> x0 = T mod P, x1 = (V + T div P) mod P
     e('.Lreduce:')
     q3 = mfma_barrett(T, T[K:], clamp=True)             # u1 -> T[K..2K-1]
-    mfma_remainder(T, q3, T[:K], nxt_p1=True)           # u0 -> T[0..K-1]
-    for i in range(K):
-        e(f'  v_add_u32_e32 {V[i]}, {V[i]}, {q3[i]}')     # V += u1 (limbs < 2^29)
-    q3b = mfma_barrett(V, V[K:], clamp=False, prefetched=True)
-    mfma_remainder(V, q3b, V[:K], nxt_p1=False)
+
+    def add_u1():
+        for i in range(K):
+            e(f'  v_add_u32_e32 {V[i]}, {V[i]}, {q3[i]}')  # V += u1 (limbs < 2^29); u1 dies here
+    dbuf = "nodbuf" not in AB
+    mfma_remainder(T, q3, T[:K], nxt_p1=True, dbuf=dbuf, after_pack=add_u1)      # u0 -> T[0..K-1]
+    q3b = mfma_barrett(V, V[K:], clamp=False, prefetched=True, dbuf=dbuf)        # T[K..] is free
+    mfma_remainder(V, q3b, V[:K], nxt_p1=False, dbuf=dbuf)
     move(X0, T[:K])
     move(X1, V[:K])
     e('  s_setpc_b64 s[12:13]')
