@@ -93,7 +93,18 @@ def gen_padic_mfma(name: str) -> str:
 
     carry = pair(CARRY)
     o = []
-    e = o.append
+    sink = [o]                                   # capture() redirects the emitter into a side list
+
+    def e(line):
+        sink[-1].append(line)
+
+    def capture(fn):
+        sink.append([])
+        try:
+            fn()
+        finally:
+            out = sink.pop()
+        return out
 
     # ---- column engine (product scanning, two adjacent columns side by side) --------------------
     def columns(cols, signed=False):
@@ -275,12 +286,37 @@ def gen_padic_mfma(name: str) -> str:
         issue_tile(*tiles[0], *sets[0])
         for m in range(5):
             if m < 4:
-                issue_tile(*tiles[m + 1], *sets[(m + 1) % 2], prefetched=False)
-            elif nxt is not None:
-                prefetch(*nxt)
+                nxt_issue = capture(lambda: issue_tile(*tiles[m + 1], *sets[(m + 1) % 2], prefetched=False))
+            else:
+                nxt_issue = capture(lambda: prefetch(*nxt)) if nxt is not None else []
             ga, gb = sets[m % 2]
             exchange(ga, gb)
-            consume(m, lambda rho, ga=ga, gb=gb: col_reg(rho, ga, gb))
+            fold = capture(lambda: consume(m, lambda rho, ga=ga, gb=gb: col_reg(rho, ga, gb)))
+            if "nointerleave" in AB:
+                for ins in nxt_issue + fold:
+                    e(ins)
+                continue
+            # the next tile's reads and MFMAs spread through this tile's fold: an in-order wave waiting to
+            # issue its next MFMA issues nothing else, so the MFMAs go out between VALU instructions
+            items, grp = [], []
+            for ins in nxt_issue:
+                grp.append(ins)
+                if "v_mfma" in ins or "ds_read" in ins:
+                    items.append(grp)
+                    grp = []
+            if grp:
+                items.append(grp)
+            gap = max(1, len(fold) // (len(items) + 1)) if items else 0
+            k = 0
+            for i, ins in enumerate(fold):
+                if items and k < len(items) and i % gap == 0:
+                    for x in items[k]:
+                        e(x)
+                    k += 1
+                e(ins)
+            for grp in items[k:]:
+                for x in grp:
+                    e(x)
 
     class Chunks:
         """column sums -> 28-bit limbs.  Chunk t (bits [base + 28 t, +28)) sums its columns (x 2^sh) into its
