@@ -46,7 +46,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
-PMC_FILE = "r02zv_pmc.json"
+PMC_FILE = "r02zy_pmc.json"
 
 
 def parse():
@@ -394,6 +394,11 @@ def run(a, world):
         if vn.value:
             roof["avg_expo_launch_ms_by_kernel"][kname] = round(vms.value / vn.value, 3)
     roof["kernel"] = " + ".join(roof["avg_expo_launch_ms_by_kernel"]) or "fthe_montprog"
+    if "fthe_padic_m37" in roof["avg_expo_launch_ms_by_kernel"]:
+        roof["kernel_note"] = ("fthe_padic_m37: the P-adic products on the VALU (v_mad_u64_u32, radix 2^28) and both "
+                               "Barrett reductions of every product on the matrix cores (v_mfma_i32_32x32x32_i8, "
+                               "136 per squaring per wave); still VALU-bound (VALUBusy in the PMC profile), so "
+                               "achieved/frac stay in VALU MAC units; DESIGN.md 3 'Matrix-core Barrett'")
     if xmacs.value and "fthe_padic_k37" in roof["avg_expo_launch_ms_by_kernel"]:
         # the P-adic kernel in issue terms: its v_mad instructions (radix 2^28, counted per program by the
         # engine) over its own launch time, against the same 39.3 T/s issue peak
