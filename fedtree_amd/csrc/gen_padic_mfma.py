@@ -251,9 +251,10 @@ def gen_padic_mfma(name: str) -> str:
                 if "nomfma" not in AB:
                     e(f'  v_mfma_i32_32x32x32_i8 v[{G}:{G + 15}], v[{buf}:{buf + 3}], v[{XB + bo}:{XB + bo + 3}], {src_c}')
 
-    def exchange(G0x, G1x):
-        """results -> VALU: wait out the last MFMA writing them (8-pass XDL), then exchange the halves"""
-        if "nonop" not in AB:
+    def exchange(G0x, G1x, waited=False):
+        """results -> VALU: wait out the last MFMA writing them (8-pass XDL: 11 wait states on gfx950), then
+        exchange the halves; waited: at least 30 VALU instructions already separate that MFMA from here"""
+        if "nonop" not in AB and not waited:
             e('  s_nop 7')
             e('  s_nop 7')
             e('  s_nop 7')
@@ -290,7 +291,8 @@ def gen_padic_mfma(name: str) -> str:
             else:
                 nxt_issue = capture(lambda: prefetch(*nxt)) if nxt is not None else []
             ga, gb = sets[m % 2]
-            exchange(ga, gb)
+            # tiles after the first were issued inside the previous fold, whose last 40% has no MFMA
+            exchange(ga, gb, waited=m > 0 and "nointerleave" not in AB)
             fold = capture(lambda: consume(m, lambda rho, ga=ga, gb=gb: col_reg(rho, ga, gb)))
             if "nointerleave" in AB:
                 for ins in nxt_issue + fold:
@@ -306,7 +308,9 @@ def gen_padic_mfma(name: str) -> str:
                     grp = []
             if grp:
                 items.append(grp)
-            gap = max(1, len(fold) // (len(items) + 1)) if items else 0
+            gap = max(1, (6 * len(fold) // 10) // (len(items) + 1)) if items else 0
+            has_mfma = any("v_mfma" in x for g_ in items for x in g_)
+            assert not has_mfma or len(fold) - gap * len(items) >= 30, "MFMA too close to the next exchange"
             k = 0
             for i, ins in enumerate(fold):
                 if items and k < len(items) and i % gap == 0:
