@@ -274,7 +274,7 @@ def gen_padic_mfma(name: str) -> str:
         rr = (rho & 3) + 4 * (rho >> 3)
         return f"v{(G1x if (rho >> 2) & 1 else G0x) + rr}"
 
-    def run_tiles(tiles, consume, nxt, dbuf):
+    def run_tiles(tiles, consume, nxt, dbuf, after_issue0=None):
         """all M-tiles of a product: consume(m, col_reg_of_the_tile) after each; dbuf: two accumulator sets,
         tile m+1's MFMAs issued before tile m's results are folded, so the matrix core works while the
         lane does (needs T[38..69] free); tile 0's first A tiles are prefetched by the caller"""
@@ -286,6 +286,11 @@ def gen_padic_mfma(name: str) -> str:
         sets = ((G0, G1), (GB0, GB1))
         issue_tile(*tiles[0], *sets[0])
         separated = False                        # >= 30 VALU instructions after this tile's last MFMA
+        if after_issue0 is not None:             # independent VALU work while tile 0 runs
+            work = capture(after_issue0)
+            for ins in work:
+                e(ins)
+            separated = len(work) >= 30
         for m in range(5):
             if m < 4:
                 nxt_issue = capture(lambda: issue_tile(*tiles[m + 1], *sets[(m + 1) % 2], prefetched=False))
@@ -437,7 +442,7 @@ def gen_padic_mfma(name: str) -> str:
         in flight; nxt_p1: prefetch product 1's first tiles at the end (the next Barrett); after_pack: the
         caller's last use of the q3 limbs (dbuf may then take their registers)"""
         orpack(q3, 8, 33, [0x80808000] + [0x80808080] * 32, lead_one=True)
-        if after_pack:
+        if after_pack and not dbuf:
             after_pack()
         e(f'  v_mov_b32_e32 {D[33]}, 0x80')          # q3 byte 131 (zero, offset) at byte 132; pads 0
         for w in range(34, 40):
@@ -448,7 +453,10 @@ def gen_padic_mfma(name: str) -> str:
 
         def consume(m, creg):
             fold_columns(ch, [(32 * m + rho, creg(rho)) for rho in range(32) if 1 <= 32 * m + rho <= 130])
-        run_tiles(P2_TILES, consume, P1_TILES[0] if nxt_p1 else None, dbuf)
+        # dbuf: the caller's last use of q3 runs while tile 0 (first accumulator set) is in the matrix core;
+        # the second set (q3's registers) is first written by tile 1
+        run_tiles(P2_TILES, consume, P1_TILES[0] if nxt_p1 else None, dbuf,
+                  after_issue0=after_pack if dbuf else None)
         ch.finish()
 
     # ---- prologue ------------------------------------------------------------
