@@ -100,3 +100,18 @@ def test_mfma_public_paillier1024_p_equals_n():
     for i in (0, 1, 2, 3, 999):
         assert pyoracle.from_words(c[i]) == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
     assert np.array_equal(pa.decrypt_u64(c), m)
+
+
+def test_mfma_million_ciphertexts_identical_to_valu_kernel(keys):
+    """2^20 device-randomness encrypts (same seed, so the same y_p, y_q per ciphertext) on the MFMA kernel and
+    on fthe_padic_k37 with the same primes: every ciphertext bit-identical (the intermediate digits differ --
+    the matrix-core quotient may be one lower -- the canonical results may not), and the decrypts agree."""
+    from fedtree_amd.paillier import Paillier
+    dev, pa, pm = keys
+    pk = _key_with({"FTHE_NO_PADIC_MFMA": "1"}, lambda: Paillier.from_primes(pa.p, pa.q, dev))
+    rng = np.random.default_rng(SEED + 9)
+    m = rng.integers(0, 2**64 - 1, 1 << 20, dtype=np.uint64)
+    ca = pa.encrypt_u64(m, seed=SEED + 11)
+    ck = pk.encrypt_u64(m, seed=SEED + 11)
+    assert np.array_equal(ca, ck)
+    assert np.array_equal(pa.decrypt_u64(ck), m)
