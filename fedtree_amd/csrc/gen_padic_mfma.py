@@ -35,7 +35,9 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gen_montprog import _descriptor  # noqa: E402
 
-AB = os.environ.get("FTHE_GEN_M37_AB", "")     # timing-only A/B variants (wrong results): noswap, nonop, nomfma
+# A/B variants for tools/build_m37_ab.sh only (fedtree_amd/build.py clears the switch): the timing-only ones
+# give wrong results (noswap, nonop, nomfma); nodbuf / nointerleave / nopair / nodesync are correct schedules
+AB = os.environ.get("FTHE_GEN_M37_AB", "")
 TILE_OFF = 512                  # byte offset of the tile image in ctx
 LDS_BYTES = 20 * 1024           # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
