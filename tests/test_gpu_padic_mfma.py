@@ -115,3 +115,39 @@ def test_mfma_million_ciphertexts_identical_to_valu_kernel(keys):
     ck = pk.encrypt_u64(m, seed=SEED + 11)
     assert np.array_equal(ca, ck)
     assert np.array_equal(pa.decrypt_u64(ck), m)
+
+
+@pytest.mark.parametrize("pq", [
+    (int("80" * 128, 16), int("7f" * 128, 16) | (1 << 1023)),           # balanced-digit carries in every byte
+    ((1 << 1030) - (1 << 600), (1 << 1008) + (1 << 500)),              # the largest and smallest P of the range
+], ids=["x80-x7f", "max-min"])
+def test_mfma_structured_primes_vs_valu_kernel_and_oracle(pq, coracle):
+    """Primes next to byte-structured values (0x80 / 0x7f runs: the balanced-digit tiles carry everywhere) and
+    at both ends of the 1009..1030-bit range: injected r bit-exact against the C oracle and identical to
+    fthe_padic_k37, device randomness identical to it, decrypts back."""
+    from test_gpu_parity import _next_prime
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    p, q = (_next_prime(x) for x in pq)
+    pa = _key_with({}, lambda: Paillier.from_primes(p, q, dev))
+    pk = _key_with({"FTHE_NO_PADIC_MFMA": "1"}, lambda: Paillier.from_primes(p, q, dev))
+    n = pa.modulus
+    rng = np.random.default_rng(SEED + 13)
+    cnt = 20000
+    rs = [1, 2, n - 1, n - 2] + [int.from_bytes(rng.bytes(pa.n_words * 4), "little") % (n - 1) + 1
+                                 for _ in range(cnt - 4)]
+    m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    rw = pyoracle.ints_to_words(rs, pa.n_words)
+    ca = pa.encrypt_u64(m, r=rw)
+    assert np.array_equal(ca, pk.encrypt_u64(m, r=rw))
+    hw = (max(p.bit_length(), q.bit_length()) + 31) // 32
+    ok = coracle.key(pyoracle.to_words(p, hw), pyoracle.to_words(q, hw))
+    idx = np.r_[0:16, cnt - 16:cnt]
+    r_or = np.zeros((len(idx), 2 * hw), np.uint32)
+    r_or[:, :pa.n_words] = rw[idx]
+    want = ok.encrypt_batch(m[idx], r_or)
+    assert np.array_equal(ca[idx], want[:, :2 * pa.n_words])
+    cd = pa.encrypt_u64(m, seed=SEED + 17)
+    assert np.array_equal(cd, pk.encrypt_u64(m, seed=SEED + 17))
+    assert np.array_equal(pa.decrypt_u64(cd), m)
+    assert np.array_equal(pa.decrypt_u64(ca), m)

@@ -62,3 +62,40 @@ def test_host_tile_image_matches_model(tmp_path):
         out = tmp_path / f"img{bits}.bin"
         subprocess.run([str(exe), format(P, "x"), str(out)], check=True)
         assert out.read_bytes() == mm.MfmaKey(P).tile_image() + bytes(1024)
+
+
+# moduli whose bytes make the balanced-digit conversion carry everywhere (0x80 / 0x7f / 0xff runs) or sit at
+# the ends of the 1009..1030-bit range; Barrett needs no primality, so these need not be prime
+STRUCTURED = [
+    int("80" * 128, 16) | 1,                                  # 1024 bits, every byte 0x80
+    int("7f" * 128, 16) | (1 << 1023) | 1,
+    (1 << 1030) - 1,                                          # all ones, the largest P
+    (1 << 1008) + 1,                                          # the smallest P (1009 bits)
+    (1 << 1029) | int("ff" * 64, 16) << 300 | 1,
+]
+
+
+@pytest.mark.parametrize("P", STRUCTURED, ids=["x80", "x7f", "max", "min", "ffrun"])
+def test_mfma_barrett_structured_moduli(P, tmp_path):
+    key = mm.MfmaKey(P)
+    key.check_skipped_tiles()
+    K = mm.K
+    P2 = P * P
+    for x0v, x1v in ((5 * P - 1, 5 * P - 1), (1, 0), (P - 1, 1), (int("80" * 128, 16) % (5 * P), P // 3)):
+        z0, z1 = pm.sqr(key, pm.limbs(x0v, K), pm.limbs(x1v, K))
+        X = x0v + x1v * P
+        assert (pm.value(z0) + pm.value(z1) * P) % P2 == X * X % P2
+        pm.check_digit(key, z0)
+        pm.check_digit(key, z1)
+    for X in (0, 1, P2 - 1, 50 * P2 - 1, int("80" * 256, 16) % (50 * P2)):
+        q3, r, _ = mm.barrett(key, pm.limbs(X, 2 * K))
+        assert pm.value(r) < 5 * P and pm.value(q3) * P + pm.value(r) == X
+    exe = tmp_path / "padic_tiles_dump"
+    rc = subprocess.run(["g++", "-O1", "-idirafter", "/opt/conda/include", "-o", str(exe),
+                         os.path.join(ROOT, "tools", "padic_tiles_dump.cpp"), "-l:libgmp.so.10"],
+                        capture_output=True, text=True).returncode
+    if rc:
+        pytest.skip("no g++/GMP to build the host tile builder")
+    out = tmp_path / "img.bin"
+    subprocess.run([str(exe), format(P, "x"), str(out)], check=True)
+    assert out.read_bytes() == key.tile_image() + bytes(1024)
