@@ -39,7 +39,10 @@ from gen_montprog import _descriptor  # noqa: E402
 # give wrong results (noswap, nonop, nomfma); nodbuf / nointerleave / nopair / nodesync are correct schedules
 AB = os.environ.get("FTHE_GEN_M37_AB", "")
 TILE_OFF = 512                  # byte offset of the tile image in ctx
-LDS_BYTES = 20 * 1024           # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
+TILE_BYTES = 20 * 1024          # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
+SPILL_BYTES = 10 * 1024         # per wave: V[37..73] while Barrett 1 runs (9 x dwordx4 + 1 dword per lane)
+SPILL = "spill" in AB           # measured: no gain (profiles/r02zzi_spill_ab.jsonl), so off
+LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
 QBIT = 28 * 38                  # q3 = floor(N / 2^1064)
 TILE_D1 = (-3, -2, -1, 0, 1)    # product-1 Toeplitz tiles (k <= 3) by m - k; then k = 4 for m = 0..4
@@ -67,7 +70,8 @@ def gen_padic_mfma(name: str) -> str:
     TT = 100                                     # T limbs v100..v173
     VV = 174                                     # V limbs v174..v247
     V_LDS = 248                                  # (lane & 63) * 16
-    NVGPR = 249
+    V_SPILL = 249                                # this wave's spill area + (lane & 63) * 16 (SPILL only)
+    NVGPR = 250 if SPILL else 249
     X0 = [f"v{XA + i}" for i in range(K)]
     X1 = [f"v{XB + i}" for i in range(K)]
     T = [f"v{TT + i}" for i in range(2 * K)]
@@ -234,6 +238,7 @@ def gen_padic_mfma(name: str) -> str:
             rd(prod, m, ks[n], n)
 
     GB0, GB1 = TT + 38, TT + 54                  # second accumulator set v[138:153], v[154:169] (T[38..69])
+    GV0, GV1 = VV + 38, VV + 54                  # or v[212:227], v[228:243] (V[38..69], spilled to LDS)
 
     def issue_tile(prod, m, ks, G0x, G1x, prefetched=True):
         """the MFMAs of M-tile m over K-tiles ks (both lane groups) into accumulators G0x, G1x; with
@@ -276,7 +281,7 @@ def gen_padic_mfma(name: str) -> str:
         rr = (rho & 3) + 4 * (rho >> 3)
         return f"v{(G1x if (rho >> 2) & 1 else G0x) + rr}"
 
-    def run_tiles(tiles, consume, nxt, dbuf, after_issue0=None):
+    def run_tiles(tiles, consume, nxt, dbuf, after_issue0=None, setb=None):
         """all M-tiles of a product: consume(m, col_reg_of_the_tile) after each; dbuf: two accumulator sets,
         tile m+1's MFMAs issued before tile m's results are folded, so the matrix core works while the
         lane does (needs T[38..69] free); tile 0's first A tiles are prefetched by the caller"""
@@ -285,7 +290,7 @@ def gen_padic_mfma(name: str) -> str:
                 mtile_mfmas(*tiles[m], nxt=tiles[m + 1] if m < 4 else nxt)
                 consume(m, col_reg)
             return
-        sets = ((G0, G1), (GB0, GB1))
+        sets = ((G0, G1), setb or (GB0, GB1))
         issue_tile(*tiles[0], *sets[0])
         separated = False                        # >= 30 VALU instructions after this tile's last MFMA
         if after_issue0 is not None:             # independent VALU work while tile 0 runs
@@ -415,7 +420,7 @@ def gen_padic_mfma(name: str) -> str:
     P1_TILES = [(1, m, [k for k in range(5) if m - k <= 1]) for m in range(5)]
     P2_TILES = [(2, m, [k for k in range(5) if m >= k]) for m in range(5)]
 
-    def mfma_barrett(Tl, q3out, clamp, prefetched=False, dbuf=False):
+    def mfma_barrett(Tl, q3out, clamp, prefetched=False, dbuf=False, setb=None):
         """product 1: q3 = Barrett's quotient of T (Tl: 2K limbs, Tl[K-1] < 2^29 allowed) -> q3out (K regs,
         may be Tl[K:]); clamp: q3 = -1 (q1 = 0) -> 0; prefetched: its first A-tile reads are in flight;
         dbuf: double-buffered accumulators (T[38..69] free)"""
@@ -431,7 +436,7 @@ def gen_padic_mfma(name: str) -> str:
 
         def consume(m, creg):
             fold_columns(ch, [(S1_LO + 32 * m + rho, creg(rho)) for rho in range(32)])
-        run_tiles(P1_TILES, consume, P2_TILES[0], dbuf)
+        run_tiles(P1_TILES, consume, P2_TILES[0], dbuf, setb=setb)
         ch.finish()
         if clamp:                                  # final carry = 0, or -1 when q1 = 0 (q3 = -1 -> 0)
             e(f'  v_not_b32_e32 v{XA + 36}, v{XA + 38}')
@@ -493,14 +498,19 @@ def gen_padic_mfma(name: str) -> str:
     e(f'  v_add_u32_e32 v{V_GOFF}, s14, v{V_GOFF}')
     # LDS tile image: 5 x 4 KB, each thread one dwordx4 per 4 KB
     e(f'  v_lshlrev_b32_e32 v10, 4, v{V_TID}')
-    for it in range(LDS_BYTES // 4096):
+    for it in range(TILE_BYTES // 4096):
         e(f'  global_load_dwordx4 v[2:5], v10, s[8:9] offset:{TILE_OFF}')
         e('  s_waitcnt vmcnt(0)')
         e('  ds_write_b128 v10, v[2:5]')
-        if it != LDS_BYTES // 4096 - 1:
+        if it != TILE_BYTES // 4096 - 1:
             e('  v_add_u32_e32 v10, 0x1000, v10')
     e(f'  v_and_b32_e32 v{V_LDS}, 63, v{V_TID}')
     e(f'  v_lshlrev_b32_e32 v{V_LDS}, 4, v{V_LDS}')
+    if SPILL:
+        e(f'  v_lshrrev_b32_e32 v{V_SPILL}, 6, v{V_TID}')             # wave in the workgroup
+        e(f'  v_mul_u32_u24_e32 v{V_SPILL}, {hex(SPILL_BYTES)}, v{V_SPILL}')
+        e(f'  v_add_u32_e32 v{V_SPILL}, {hex(TILE_BYTES)}, v{V_SPILL}')
+        e(f'  v_add_u32_e32 v{V_SPILL}, v{V_SPILL}, v{V_LDS}')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
     if "nodesync" not in AB:
@@ -632,12 +642,22 @@ def gen_padic_mfma(name: str) -> str:
 
     # reduce (SQR, MUL): T (x0^2 or x0 y0), V (cross terms) -> x0 = T mod P, x1 = (V + T div P) mod P
     e('.Lreduce:')
-    q3 = mfma_barrett(T, T[K:], clamp=True)             # u1 -> T[K..2K-1]
+    dbuf = "nodbuf" not in AB
+    spill = dbuf and SPILL
+    if spill:
+        # V[37..73] waits in LDS while Barrett 1 runs, so its product 1 gets a second accumulator set too
+        for j in range(9):
+            e(f'  ds_write_b128 v{V_SPILL}, v[{VV + 38 + 4 * j}:{VV + 41 + 4 * j}] offset:{1024 * j}')
+        e(f'  ds_write_b32 v{V_SPILL}, {V[K]} offset:{9 * 1024}')
+    q3 = mfma_barrett(T, T[K:], clamp=True, dbuf=spill, setb=(GV0, GV1))    # u1 -> T[K..2K-1]
 
     def add_u1():
         for i in range(K):
             e(f'  v_add_u32_e32 {V[i]}, {V[i]}, {q3[i]}')  # V += u1 (limbs < 2^29); u1 dies here
-    dbuf = "nodbuf" not in AB
+        if spill:                                           # V[37..73] back (older than every tile read)
+            for j in range(9):
+                e(f'  ds_read_b128 v[{VV + 38 + 4 * j}:{VV + 41 + 4 * j}], v{V_SPILL} offset:{1024 * j}')
+            e(f'  ds_read_b32 {V[K]}, v{V_SPILL} offset:{9 * 1024}')
     mfma_remainder(T, q3, T[:K], nxt_p1=True, dbuf=dbuf, after_pack=add_u1)      # u0 -> T[0..K-1]
     q3b = mfma_barrett(V, V[K:], clamp=False, prefetched=True, dbuf=dbuf)        # T[K..] is free
     mfma_remainder(V, q3b, V[:K], nxt_p1=False, dbuf=dbuf)
