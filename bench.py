@@ -422,6 +422,14 @@ def run(a, world):
         pmc = json.load(open(prof_hbm))
         roof["traffic"] = pmc.get("enc", {}).get(expo_kernel, {}).get("hbm_bytes_per_launch")
         roof["traffic_source"] = f"profiles/{PMC_FILE} ({expo_kernel} full-chunk launch)"
+        ek = pmc.get("enc", {}).get(expo_kernel, {})
+        if ek.get("SQ_INSTS_MFMA") and roof["avg_expo_launch_ms"]:
+            # matrix-core share of the launch: SQ_VALU_MFMA_BUSY_CYCLES counts 32 cycles per i8 32x32x32
+            # MFMA, over every SIMD's cycles of the launch (1,024 SIMDs x 2.4 GHz x the HIP-event duration)
+            simd_cycles = 1024 * 2.4e9 * roof["avg_expo_launch_ms"] * 1e-3
+            roof["matrix_core"] = {"mfma_per_launch": ek["SQ_INSTS_MFMA"],
+                                   "mfma_busy_frac": round(ek.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / simd_cycles, 4),
+                                   "valu_busy_pct": ek.get("VALUBusy"), "source": f"profiles/{PMC_FILE}"}
     # what the traffic is: SURVEY 8(d) algorithmic bytes (772 B per encrypt, half per prime launch) vs the
     # operand reads of the one-lane design (each window multiplication reads a 296-B table entry per lane)
     lanes = 393216
