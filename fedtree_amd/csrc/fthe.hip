@@ -131,12 +131,15 @@ size_t chunk_lanes() {
     return v;
 }
 
-// Decrypts of at most this many lanes run their p and q halves on two streams (half the chip's
-// 2-waves/SIMD capacity at s74); FTHE_DEC_SPLIT overrides, 0 turns it off (A/B).
+// CRT decrypts and device-randomness encrypts of at most this many lanes run their p and q halves on
+// two streams, so the two launches share the chip: the waves of a batch that is not a whole number of
+// rounds per half (200,000 Paillier-1024 ciphertexts: 3,125 waves per half, 3,072 resident) fill one
+// tail instead of two -- 16.4 ms instead of 19.4 ms, and 91.7 ms instead of 106.7 ms at Paillier-2048
+// (profiles/r02zzn_split_*.jsonl).  Default: one chunk; FTHE_DEC_SPLIT overrides, 0 turns it off (A/B).
 size_t dec_split_lanes() {
     static size_t v = [] {
         const char *e = getenv("FTHE_DEC_SPLIT");
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)65536;
+        return e ? (size_t)strtoull(e, nullptr, 10) : chunk_lanes();
     }();
     return v;
 }

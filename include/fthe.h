@@ -56,7 +56,7 @@ const char *fthe_strerror(int status);
 
 /* ---- device context (one HIP stream + workspace) ------------------------ */
 /* Every call is ordered on the context stream.  Small decrypts and device-
- * randomness encrypts (<= 65,536 lanes; <= 16,384 ciphertexts of a
+ * randomness encrypts (<= one chunk, 393,216 lanes; <= 16,384 ciphertexts of a
  * Paillier-2048 key also switch to the four-lane s80 kernel) fork their mod-q
  * half onto a private side stream and join it back before any output is
  * written, so callers see one stream: fthe_ctx_sync / an event on

@@ -2,9 +2,9 @@
 m = L(c^lambda mod n^2) mu mod n (paillier.cpp:141-156, Paillier_GMP::decrypt paillier_gmp.cpp:75-85, whose
 mpz_powm reduces c mod n^2 first): uniform rows over the whole 2 n_words-word range (so also c >= n^2,
 unreduced), the edges 1, 2, n^2 - 1, n^2 + 1, 1 + n, 2^(64 n_words) - 1, on the three decrypt paths (the
-four-lane s80 one for small batches, the split p/q one, the chunked one) and on every exponentiation kernel
-of a key: the matrix-core P-adic kernel (default), the VALU P-adic kernel (FTHE_NO_PADIC_MFMA) and the
-Montgomery programs (FTHE_NO_PADIC).  The short form is m mod p.  Integer work: exact equality."""
+four-lane s80 one for small batches, the split p/q one for one chunk, the chunked one beyond) and on every
+exponentiation kernel of a key: the matrix-core P-adic kernel (default), the VALU P-adic kernel
+(FTHE_NO_PADIC_MFMA) and the Montgomery programs (FTHE_NO_PADIC).  The short form is m mod p.  Integer work: exact equality."""
 import math
 import os
 
@@ -16,7 +16,7 @@ import pyoracle
 pytestmark = pytest.mark.gpu
 
 SEED = 20261016
-PATH_COUNTS = (48, 40000, 70000)        # s80 quad path (<= 16,384), split p/q, chunked
+PATH_COUNTS = (48, 40000, 397312)       # s80 quad path (<= 16,384), split p/q (one chunk), chunked
 KERNEL_ENV = [{}, {"FTHE_NO_PADIC_MFMA": "1"}, {"FTHE_NO_PADIC": "1"}]
 
 
@@ -57,13 +57,14 @@ def test_decrypt_arbitrary_rows_vs_reference_formula(dev, bits):
     assert top >= n * n
     rng = np.random.default_rng(SEED + bits + 1)
     edges = [1, 2, n * n - 1, n * n + 1, 1 + n, top]
-    rows = edges + [int.from_bytes(rng.bytes(4 * cw), "little") for _ in range(max(PATH_COUNTS) - len(edges))]
+    cts = rng.integers(0, 2**32, (max(PATH_COUNTS), cw), dtype=np.uint32)
+    cts[:len(edges)] = pyoracle.ints_to_words(edges, cw)
     sample = list(range(48)) + list(range(max(PATH_COUNTS) - 16, max(PATH_COUNTS)))
+    rows = {i: pyoracle.from_words(cts[i]) for i in sample}
     for i in sample:
         assert math.gcd(rows[i], n) == 1, i                 # valid ciphertexts (fails with prob. ~2^-1000)
     want = {i: _ref_decrypt(rows[i], n, lam, mu) for i in sample}
     assert want[0] == want[2] == want[3] == 0 and want[4] == 1
-    cts = pyoracle.ints_to_words(rows, cw)
     for env, k in zip(KERNEL_ENV, keys):
         full_by_count = {}
         for cnt in PATH_COUNTS:

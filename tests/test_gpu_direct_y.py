@@ -11,7 +11,7 @@ sampled ciphertext is compared with the C oracle's encrypt(m, r) -- the full
 PowerMod formula, no CRT, no 1 + mn shortcut (oracle/paillier_oracle.c).
 
 Covered: the four-lane small-batch path (<= 16,384 ciphertexts), the two-stream
-split path (<= 65,536), and the chunked large-batch path across the 393,216-lane
+split path (one chunk, <= 393,216), and the chunked large-batch path across the 393,216-lane
 chunk boundary.  Integer work: exact equality.
 """
 import numpy as np

@@ -61,7 +61,7 @@ def test_injected_r_same_ciphertexts_as_montgomery(keys, coracle):
 def test_device_randomness_same_as_montgomery_and_decrypts(keys):
     dev, pa, pm = keys
     rng = np.random.default_rng(SEED + 1)
-    for cnt in (40000, 70000):                   # the split path (<= 65,536 lanes) and the chunked one
+    for cnt in (40000, 397312):                  # the split path (one chunk) and the chunked one
         m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
         ca = pa.encrypt_u64(m, seed=SEED + cnt)
         cm = pm.encrypt_u64(m, seed=SEED + cnt)

@@ -59,7 +59,7 @@ def test_mfma_injected_r_same_ciphertexts_as_montgomery(keys, coracle):
 def test_mfma_device_randomness_decrypts(keys):
     dev, pa, pm = keys
     rng = np.random.default_rng(SEED + 1)
-    for cnt in (40000, 70000):                   # the split path and the chunked one
+    for cnt in (40000, 397312):                  # the split path (one chunk) and the chunked one
         m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
         c = pa.encrypt_u64(m, seed=SEED + cnt)
         assert np.array_equal(pm.decrypt_u64(c), m)

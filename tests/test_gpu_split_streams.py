@@ -1,5 +1,5 @@
 """Small-batch latency paths: decrypts (paillier.cpp:141-157) and device-randomness
-CRT encrypts (paillier.cpp:122-139) of at most 65,536 lanes run the mod-q half on
+CRT encrypts (paillier.cpp:122-139) of at most one chunk (393,216 lanes) run the mod-q half on
 the context's side stream, in a second slot region, beside the mod-p half; decrypts
 of at most 16,384 ciphertexts of a Paillier-2048 key run both halves on the
 four-lane s80 kernel (one quad of lanes per exponentiation).
@@ -17,7 +17,7 @@ from conftest import golden_key, load_golden
 
 pytestmark = pytest.mark.gpu
 
-SPLIT_MAX = 65536     # dec_split_lanes() default (one lane per ciphertext at P-1024 and P-2048)
+SPLIT_MAX = 393216    # dec_split_lanes() default = chunk_lanes() (one lane per ciphertext at P-1024, P-2048)
 QUAD_MAX = 16384      # dec_quad_max() default
 
 
@@ -38,7 +38,7 @@ def test_split_matches_single_stream(dev, name):
     m = rng.integers(0, 2**64, big, dtype=np.uint64)
     m[:4] = [0, 1, 2**64 - 1, 2**63]
     c_big = pl.encrypt_u64(m, seed=77)
-    for cnt in (1, 2, 3, 1000, QUAD_MAX, QUAD_MAX + 1, 20000):   # below: two streams (and s80 decrypts)
+    for cnt in (1, 2, 3, 1000, QUAD_MAX, QUAD_MAX + 1, 20000, 200000):   # below: two streams (and s80 decrypts)
         c_small = pl.encrypt_u64(m[:cnt], seed=77)
         assert np.array_equal(c_small, c_big[:cnt]), cnt
         lo, full = pl.decrypt_u64(c_big[:cnt], full=True)
