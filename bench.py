@@ -25,6 +25,7 @@ host's cores, cores and CPU model stated).
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -579,7 +580,24 @@ def run(a, world):
             "concurrent_adds_per_s": round(nthr * per / conc_s),
             "note": "one ciphertext add per call through the key's coalescing queue, as GHPair::operator+ / += "
                     "issue them (host rows in and out, one four-lane product launch per merged batch); the "
-                    "batch entry points (merge, histogram, reduce_segments) are the throughput path"}
+                    "batch entry points (merge, histogram, reduce_segments) are the throughput path; Python "
+                    "threads (GIL between calls): the C++ OpenMP rate is histogram_loop_unchanged_callers"}
+        # the same operators from C++ OpenMP threads, as FedTree's histogram loop issues them unchanged
+        # (integration/ghpair_rate.cpp, hist_tree_builder.cpp:572-591): a child process, its own context
+        exe = os.path.join(ROOT, "tools", "bin", "ghpair_rate")
+        hl = {"note": "integration/ghpair_rate.cpp: OpenMP over features, `dest = dest + src` per instance through "
+                      "GHPair::operator+ on the USE_HIP key (2 fthe_add_shared per operator; empty bins promoted "
+                      "by 2 fthe_encrypt_shared), every bin checked by decryption; compare cpu_baseline.ops."
+                      "p2048_add (the reference's host Paillier_GMP::add, all lease threads)"}
+        for thr in (16, 64):
+            try:
+                r = subprocess.run([exe, str(KEY_BITS), str(thr), "512", "16"], capture_output=True, text=True,
+                                   timeout=180)
+                hl[f"threads_{thr}"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                    {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+            except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
+                hl[f"threads_{thr}"] = {"error": repr(ex)[:300]}
+        secondary["histogram_loop_unchanged_callers"] = hl
         # key generation (homo_init; re-run every round in the vertical simulation, FLtrainer.cpp:556):
         # host prime search on up to 16 threads + device key set-up
         t0 = time.perf_counter()

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -274,6 +275,10 @@ struct Coalescer {
     std::vector<OpReq *> opending;           // fthe_add_shared / _scalar_mul_u64_shared: a third one
     bool leader = false, eleader = false, oleader = false;
     fthe_ctx *ctx = nullptr, *ectx = nullptr, *octx = nullptr;   // the key's own contexts, one leader each
+    // group-commit linger (linger() below): requests in each queue's previous batch, a leader waiting
+    std::condition_variable lcv;
+    size_t last = 0, elast = 0, olast = 0;
+    bool lingering = false, elingering = false, olingering = false;
     std::vector<uint32_t> ct, full, eout, oa, ob, oout;
     std::vector<uint64_t> lo, em;
     ~Coalescer() {
@@ -3681,6 +3686,33 @@ static Coalescer *key_coalescer(fthe_key *k) {
     return k->co.get();
 }
 
+// Group commit with a linger.  The callers of a finished batch come back one at a time (each wakes from
+// notify_all, re-takes the mutex, returns, issues its next call), so a new leader that took the queue at
+// once would run a batch of one and leave the others to the round trip after: FedTree's OpenMP loops of
+// single-element calls (hist_tree_builder.cpp:574-591 through GHPair's operators; decrypt_gh per node,
+// FLtrainer.cpp:758-764) then ran ~6x below the batch-per-round-trip rate.  A new leader waits until as
+// many requests are pending as the previous batch held, at most FTHE_LINGER_US (default 200 us; 0: off);
+// a lone caller (previous batch of one) never waits.  Arrivals wake it when the count is reached.
+static int linger_us() {
+    static const int v = [] {
+        const char *e = getenv("FTHE_LINGER_US");
+        return e ? std::max(0, atoi(e)) : 200;
+    }();
+    return v;
+}
+template <class Req>
+static void linger(Coalescer *co, std::unique_lock<std::mutex> &lk, const std::vector<Req *> &pend, size_t last,
+                   bool &lingering) {
+    if (last <= 1 || pend.size() >= last || linger_us() <= 0) return;
+    lingering = true;
+    co->lcv.wait_for(lk, std::chrono::microseconds(linger_us()), [&] { return pend.size() >= last; });
+    lingering = false;
+}
+template <class Req>
+static void arrived(Coalescer *co, const std::vector<Req *> &pend, size_t last, bool lingering) {
+    if (lingering && pend.size() >= last) co->lcv.notify_all();
+}
+
 extern "C" int fthe_decrypt_shared(fthe_key *k, const uint32_t *ct, size_t count, uint64_t *m_low, uint32_t *m_full,
                                    int short_pt) {
     if (!k || (!ct && count)) return FTHE_ERR_ARG;
@@ -3691,12 +3723,15 @@ extern "C" int fthe_decrypt_shared(fthe_key *k, const uint32_t *ct, size_t count
     DecReq r{ct, count, m_low, m_full, short_pt != 0};
     std::unique_lock<std::mutex> lk(co->mu);
     try { co->pending.push_back(&r); } catch (...) { return FTHE_ERR_NOMEM; }
+    arrived(co, co->pending, co->last, co->lingering);
     for (;;) {
         if (r.done) return r.rc;
         if (!co->leader) {
             co->leader = true;
+            linger(co, lk, co->pending, co->last, co->lingering);
             std::vector<DecReq *> batch;
             batch.swap(co->pending);                 // includes r
+            co->last = batch.size();
             lk.unlock();
             coalesced_batch(k, co, batch);
             lk.lock();
@@ -3847,12 +3882,15 @@ extern "C" int fthe_encrypt_shared(fthe_key *k, const uint64_t *m, size_t count,
     EncReq r{m, count, out, flags};
     std::unique_lock<std::mutex> lk(co->mu);
     try { co->epending.push_back(&r); } catch (...) { return FTHE_ERR_NOMEM; }
+    arrived(co, co->epending, co->elast, co->elingering);
     for (;;) {
         if (r.done) return r.rc;
         if (!co->eleader) {
             co->eleader = true;
+            linger(co, lk, co->epending, co->elast, co->elingering);
             std::vector<EncReq *> batch;
             batch.swap(co->epending);                // includes r
+            co->elast = batch.size();
             lk.unlock();
             coalesced_encrypt(k, co, batch);
             lk.lock();
@@ -3914,12 +3952,15 @@ static int op_shared(fthe_key *k, OpReq &r) {
     if (!co) return FTHE_ERR_NOMEM;
     std::unique_lock<std::mutex> lk(co->mu);
     try { co->opending.push_back(&r); } catch (...) { return FTHE_ERR_NOMEM; }
+    arrived(co, co->opending, co->olast, co->olingering);
     for (;;) {
         if (r.done) return r.rc;
         if (!co->oleader) {
             co->oleader = true;
+            linger(co, lk, co->opending, co->olast, co->olingering);
             std::vector<OpReq *> batch;
             batch.swap(co->opending);                // includes r
+            co->olast = batch.size();
             lk.unlock();
             try {
                 coalesced_ops_impl(k, co, batch);
