@@ -36,6 +36,7 @@ def test_shim_compiles_and_links(tmp_path):
     _build(str(tmp_path / "concurrency_test"), "concurrency_test.cpp")
     _build(str(tmp_path / "shim_abort"), extra=("-DFTHE_SHIM_ABORT",))
     _build(str(tmp_path / "ghpair_test"), "ghpair_test.cpp", extra=("-DFTHE_REFERENCE_SHARED_R",))
+    _build(str(tmp_path / "ghpair_rate"), "ghpair_rate.cpp", extra=("-fopenmp",))
 
 
 def test_nonreference_modes_need_the_build_opt_in(tmp_path):
