@@ -278,6 +278,7 @@ struct Coalescer {
     // group-commit linger (linger() below): requests in each queue's previous batch, a leader waiting
     std::condition_variable lcv;
     size_t last = 0, elast = 0, olast = 0;
+    int64_t last_us = 0, elast_us = 0, olast_us = 0;   // the previous batch's duration
     bool lingering = false, elingering = false, olingering = false;
     std::vector<uint32_t> ct, full, eout, oa, ob, oout;
     std::vector<uint64_t> lo, em;
@@ -3690,9 +3691,11 @@ static Coalescer *key_coalescer(fthe_key *k) {
 // notify_all, re-takes the mutex, returns, issues its next call), so a new leader that took the queue at
 // once would run a batch of one and leave the others to the round trip after: FedTree's OpenMP loops of
 // single-element calls (hist_tree_builder.cpp:574-591 through GHPair's operators; decrypt_gh per node,
-// FLtrainer.cpp:758-764) then ran ~6x below the batch-per-round-trip rate.  A new leader waits until as
-// many requests are pending as the previous batch held, at most FTHE_LINGER_US (default 200 us; 0: off);
-// a lone caller (previous batch of one) never waits.  Arrivals wake it when the count is reached.
+// FLtrainer.cpp:758-764) ran two launches per round.  A new leader waits until as many requests are pending
+// as there were callers in the previous round (its batch plus the requests that arrived while it ran), at
+// most FTHE_LINGER_US (default 200 us; 0: off) or a quarter of the previous batch's duration if that is
+// longer (a merged decrypt takes ~10 ms); a lone caller never waits.  Arrivals wake it when the count is
+// reached.
 static int linger_us() {
     static const int v = [] {
         const char *e = getenv("FTHE_LINGER_US");
@@ -3702,11 +3705,15 @@ static int linger_us() {
 }
 template <class Req>
 static void linger(Coalescer *co, std::unique_lock<std::mutex> &lk, const std::vector<Req *> &pend, size_t last,
-                   bool &lingering) {
+                   bool &lingering, int64_t last_us) {
     if (last <= 1 || pend.size() >= last || linger_us() <= 0) return;
     lingering = true;
-    co->lcv.wait_for(lk, std::chrono::microseconds(linger_us()), [&] { return pend.size() >= last; });
+    const int64_t bound = std::max<int64_t>(linger_us(), last_us / 4);   // a quarter of a long batch (decrypts)
+    co->lcv.wait_for(lk, std::chrono::microseconds(bound), [&] { return pend.size() >= last; });
     lingering = false;
+}
+static int64_t us_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 template <class Req>
 static void arrived(Coalescer *co, const std::vector<Req *> &pend, size_t last, bool lingering) {
@@ -3728,14 +3735,16 @@ extern "C" int fthe_decrypt_shared(fthe_key *k, const uint32_t *ct, size_t count
         if (r.done) return r.rc;
         if (!co->leader) {
             co->leader = true;
-            linger(co, lk, co->pending, co->last, co->lingering);
+            linger(co, lk, co->pending, co->last, co->lingering, co->last_us);
             std::vector<DecReq *> batch;
             batch.swap(co->pending);                 // includes r
-            co->last = batch.size();
             lk.unlock();
+            const auto t_batch = std::chrono::steady_clock::now();
             coalesced_batch(k, co, batch);
+            co->last_us = us_since(t_batch);
             lk.lock();
             for (DecReq *q : batch) q->done = true;
+            co->last = batch.size() + co->pending.size();   // callers active in this round
             co->leader = false;
             co->cv.notify_all();
             return r.rc;
@@ -3887,14 +3896,16 @@ extern "C" int fthe_encrypt_shared(fthe_key *k, const uint64_t *m, size_t count,
         if (r.done) return r.rc;
         if (!co->eleader) {
             co->eleader = true;
-            linger(co, lk, co->epending, co->elast, co->elingering);
+            linger(co, lk, co->epending, co->elast, co->elingering, co->elast_us);
             std::vector<EncReq *> batch;
             batch.swap(co->epending);                // includes r
-            co->elast = batch.size();
             lk.unlock();
+            const auto t_batch = std::chrono::steady_clock::now();
             coalesced_encrypt(k, co, batch);
+            co->elast_us = us_since(t_batch);
             lk.lock();
             for (EncReq *q : batch) q->done = true;
+            co->elast = batch.size() + co->epending.size();   // callers active in this round
             co->eleader = false;
             co->cv.notify_all();
             return r.rc;
@@ -3957,18 +3968,20 @@ static int op_shared(fthe_key *k, OpReq &r) {
         if (r.done) return r.rc;
         if (!co->oleader) {
             co->oleader = true;
-            linger(co, lk, co->opending, co->olast, co->olingering);
+            linger(co, lk, co->opending, co->olast, co->olingering, co->olast_us);
             std::vector<OpReq *> batch;
             batch.swap(co->opending);                // includes r
-            co->olast = batch.size();
             lk.unlock();
             try {
+                const auto t_batch = std::chrono::steady_clock::now();
                 coalesced_ops_impl(k, co, batch);
+                co->olast_us = us_since(t_batch);
             } catch (...) {
                 for (OpReq *q : batch) q->rc = FTHE_ERR_NOMEM;
             }
             lk.lock();
             for (OpReq *q : batch) q->done = true;
+            co->olast = batch.size() + co->opending.size();   // callers active in this round
             co->oleader = false;
             co->cv.notify_all();
             return r.rc;
