@@ -238,8 +238,10 @@ int fthe_decrypt_short(fthe_key *key, fthe_ctx *ctx, const uint32_t *c, size_t c
  * FLtrainer.cpp:758-764).  Thread-safe, no context argument: requests that
  * arrive while a batch runs are merged into the next one, run by one of the
  * waiting callers on a context the key owns, so N concurrent single-pair
- * calls cost about two batch latencies instead of N (small launches from
+ * calls cost about one batch latency instead of N (small launches from
  * separate contexts share the process's few hardware queues and serialise).
+ * A new leader lingers until the previous round's callers are back, at most
+ * FTHE_LINGER_US (200 us) or a quarter of the previous batch (0: off).
  * short_pt != 0: fthe_decrypt_short semantics.  Same results as fthe_decrypt. */
 int fthe_decrypt_shared(fthe_key *key, const uint32_t *c, size_t count,
                         uint64_t *m_low, uint32_t *m_full, int short_pt);
