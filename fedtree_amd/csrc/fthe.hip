@@ -3758,12 +3758,31 @@ extern "C" int fthe_decrypt_short(fthe_key *k, fthe_ctx *c, const uint32_t *ct, 
     return decrypt_host(k, c, ct, count, m_low, m_full, true);
 }
 
+// Host-resident pair ops of at most this many rows take the single-stream path (FTHE_SMALL_HOST; 0: never).
+static size_t small_host_rows() {
+    static const size_t v = [] {
+        const char *e = getenv("FTHE_SMALL_HOST");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
+    }();
+    return v;
+}
 static int pair_host(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,
                      bool sub) {
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     size_t row = 2 * (size_t)k->n_words * 4;
     int rc;
+    if (count <= small_host_rows()) {
+        // small batches (GHPair operators through fthe_add_shared): one stream, no staging pipeline --
+        // the pipe's copy-stream / compute-stream event hand-offs cost more than its overlap saves here
+        HostIO io{c}; void *da, *db, *dout;
+        if ((rc = io.in(0, a, count * row, &da)) || (rc = io.in(1, b, count * row, &db)) ||
+            (rc = io.outbuf(2, count * row, &dout)))
+            return rc;
+        if ((rc = pair_impl(k, c, (const uint32_t *)da, (const uint32_t *)db, count, (uint32_t *)dout, nullptr, sub)))
+            return rc;
+        return io.back(out, dout, count * row);
+    }
     for (int i = 0; i < 3; i++) if ((rc = c->io[i].ensure(std::max<size_t>(4, count * row)))) return rc;
     HostPipe pipe{c};
     pipe.add_in(a, c->io[0].p, row);
