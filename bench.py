@@ -526,7 +526,7 @@ def run(a, world):
         secondary["single_pair_latency_ms"]["decrypt_short"] = round((time.perf_counter() - t0) / 5 * 1e3, 2)
         # decrypt_gh from 32 OpenMP-style threads on one key: merged by the key's coalescing queue
         import threading
-        nthr, rounds = 32, 4
+        nthr, rounds = 32, 12                      # the first round has no linger history
         cts = [pl.encrypt_u64(np.array([7 * i, 11 * i], dtype=np.uint64), seed=50 + i) for i in range(nthr)]
         ok = [True] * nthr
         go = threading.Barrier(nthr + 1)
