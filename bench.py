@@ -252,11 +252,18 @@ def dry_run(a, world):
     times = timed_steps(lambda i: time.sleep(0.02), a, world, sync=lambda: None)
     per = gather_ranks({"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
                         "elapsed_s": times}, world)
+    # the per-rank add batch (a sleep standing in for the device adds) and rank 0's CPU stage, in the
+    # order and with the collectives of the real run
+    adds = rank_adds(lambda: time.sleep(0.01) or 0.01, 1 << 20, world, rank, sync=lambda: None)
     if rank == 0:
+        cpu = {"dry_run": True, "value": None, "unit": "encrypts/s", "cores": host_cpu()["threads_used"],
+               "kind": None, "sample": "dry run: no CPU baseline measured"}
         print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": a.steps,
                           "warmup": a.warmup, "elapsed_max_s": max(p["elapsed_s"] for p in per),
+                          "roofline": {"dry_run": True}, "cpu_baseline": cpu, "ciphertext_adds": adds,
                           "per_rank": per}), flush=True)
     if world > 1:
+        dist.barrier()                                 # ranks wait for rank 0's CPU stage, as in run()
         dist.destroy_process_group()
 
 
@@ -291,6 +298,29 @@ def gather_ranks(obj, world):
     out = [None] * world
     dist.all_gather_object(out, obj)
     return out
+
+
+def rank_adds(call, count, world, rank, sync):
+    """The metric's second half, "ciphertext adds/s" at N GPUs: every rank times `count` device-resident
+    P-2048 adds (x y mod n^2 on its own GPU; call() runs one batch and returns its kernel seconds) --
+    one untimed call, then the median of 5 -- between barriers; the aggregate is all ranks' adds over
+    the slowest rank's median (weak scaling, no data-path collective)."""
+    import torch.distributed as dist
+    call()
+    sync()
+    if world > 1:
+        dist.barrier()
+    ts = []
+    for _ in range(5):
+        ts.append(call())
+    sync()
+    med = sorted(ts)[2]
+    per = gather_ranks({"rank": rank, "adds": count, "median_s": round(med, 6),
+                        "adds_per_s": round(count / med)}, world)
+    slow = max(p["median_s"] for p in per)
+    return {"per_rank": per, "aggregate_adds_per_s": round(world * count / slow), "adds_per_rank": count,
+            "note": "device-resident P-2048 ciphertext adds (one classical 4096-bit product per add, "
+                    "fthe_add_dev), median of 5 per rank, aggregate = ranks x adds / slowest rank"}
 
 
 def run(a, world):
@@ -367,6 +397,17 @@ def run(a, world):
     elapsed = max(p["elapsed_s"] for p in per_rank)
     enc_total = world * enc_rank
     value = enc_total / elapsed
+    na_rank = min(2 * P, 1 << 20)
+    add_out = torch.empty((na_rank, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
+    add_b = c[na_rank:2 * na_rank] if 2 * na_rank <= 2 * P else c[:na_rank]
+
+    def _add_call():
+        pl.add_dev(c[:na_rank], add_b, add_out)
+        dev.sync()
+        return lib.fthe_last_kernel_ms(dev.ctx) * 1e-3
+
+    adds = rank_adds(_add_call, na_rank, world, rank, sync)
+    del add_out, add_b
 
     # -- roofline of the dominant kernel family (the exponentiation kernels, per-launch HIP
     # events on the engine stream, this rank).  Algorithmic work = the 32-bit MACs of the
@@ -400,6 +441,19 @@ def run(a, world):
                                "Barrett reductions of every product on the matrix cores (v_mfma_i32_32x32x32_i8, "
                                "136 per squaring per wave); still VALU-bound (VALUBusy in the PMC profile), so "
                                "achieved/frac stay in VALU MAC units; DESIGN.md 3 'Matrix-core Barrett'")
+    # the metric's unit of SURVEY 8(d) (W(64) Montgomery products, 1.2 e products per e-bit exponent) for
+    # the work the direct-y CRT encrypt must do -- two exponentiations mod P^2 (s = 64) by the 1024-bit P:
+    # above 1 because the P-adic digits need 2.1x fewer MACs than Montgomery products mod P^2, not because
+    # work is skipped (tests/test_gpu_direct_y.py pins the timed path bit-exactly)
+    survey_macs_direct = 2 * 1.2 * 1024 * W64
+    roof["frac_survey_unit"] = round(value / world * survey_macs_direct / PEAK_MAC_S, 4)
+    roof["frac_survey_unit_textbook_crt"] = round(value / world * ALG_MACS_PER_CRT_ENC / PEAK_MAC_S, 4)
+    roof["frac_survey_unit_note"] = (
+        "value x 2 x 1.2 x 1024 x W(64) MACs (two Montgomery exponentiations mod P^2 by the 1024-bit P) over the "
+        "39.3 T MAC/s peak; _textbook_crt charges 4.06e7 (exponent n mod P(P-1)).  Both exceed 1 because the "
+        "executed P-adic algorithm needs 9.49e6 MACs per encrypt (alg_macs_per_encrypt), 2.1x fewer than the "
+        "Montgomery count of the same exponentiations; frac (the algorithmic unit) and issue_frac (executed "
+        "instructions) measure the hardware")
     if xmacs.value and "fthe_padic_k37" in roof["avg_expo_launch_ms_by_kernel"]:
         # the P-adic kernel in issue terms: its v_mad instructions (radix 2^28, counted per program by the
         # engine) over its own launch time, against the same 39.3 T/s issue peak
@@ -424,13 +478,26 @@ def run(a, world):
         roof["traffic"] = pmc.get("enc", {}).get(expo_kernel, {}).get("hbm_bytes_per_launch")
         roof["traffic_source"] = f"profiles/{PMC_FILE} ({expo_kernel} full-chunk launch)"
         ek = pmc.get("enc", {}).get(expo_kernel, {})
-        if ek.get("SQ_INSTS_MFMA") and roof["avg_expo_launch_ms"]:
-            # matrix-core share of the launch: SQ_VALU_MFMA_BUSY_CYCLES counts 32 cycles per i8 32x32x32
-            # MFMA, over every SIMD's cycles of the launch (1,024 SIMDs x 2.4 GHz x the HIP-event duration)
-            simd_cycles = 1024 * 2.4e9 * roof["avg_expo_launch_ms"] * 1e-3
+        kms_expo = roof["avg_expo_launch_ms_by_kernel"].get(expo_kernel) or roof["avg_expo_launch_ms"]
+        simd_cycles = 1024 * 2.4e9 * kms_expo * 1e-3     # every SIMD's cycles over the live launch time
+        if ek.get("SQ_INSTS_VALU") and kms_expo:
+            # executed issue: the kernel's VALU wave-instructions (PMC, per launch) x 4 cycles (a wave64
+            # v_mad_u64_u32, 80+% of the stream, issues once per 4 cycles per SIMD) over the SIMD cycles
+            roof["issue_frac"] = round(ek["SQ_INSTS_VALU"] * 4 / simd_cycles, 4)
+            roof["issue_note"] = (f"{expo_kernel}: SQ_INSTS_VALU {ek['SQ_INSTS_VALU']:.4g} wave-instructions per full-chunk "
+                                  f"launch (profiles/{PMC_FILE}) x 4 cycles / (1,024 SIMDs x 2.4 GHz x {kms_expo} ms, "
+                                  "this run's HIP-event launch time)")
+        if ek.get("SQ_INSTS_MFMA") and kms_expo:
+            # matrix cores: SQ_VALU_MFMA_BUSY_CYCLES counts 32 cycles per i8 32x32x32 MFMA; the i8 dense peak
+            # is 2x the bf16 rate (MI355X_MICROARCH.md MFMA table): 32x32x32x2 ops per 32 cycles per SIMD
+            i8_peak = 1024 * 2.4e9 * (32 * 32 * 32 * 2) / 32
+            i8_ops = ek["SQ_INSTS_MFMA"] * 32 * 32 * 32 * 2 / (kms_expo * 1e-3)
             roof["matrix_core"] = {"mfma_per_launch": ek["SQ_INSTS_MFMA"],
                                    "mfma_busy_frac": round(ek.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / simd_cycles, 4),
-                                   "valu_busy_pct": ek.get("VALUBusy"), "source": f"profiles/{PMC_FILE}"}
+                                   "i8_tops": round(i8_ops / 1e12, 1), "i8_dense_peak_tops": round(i8_peak / 1e12, 1),
+                                   "frac_of_i8_peak": round(i8_ops / i8_peak, 4),
+                                   "valu_busy_pct": ek.get("VALUBusy"), "source": f"profiles/{PMC_FILE}",
+                                   "note": "v_mfma_i32_32x32x32_i8: both Barrett products of every P-adic product"}
     # what the traffic is: SURVEY 8(d) algorithmic bytes (772 B per encrypt, half per prime launch) vs the
     # operand reads of the one-lane design (each window multiplication reads a 296-B table entry per lane)
     lanes = 393216
@@ -586,18 +653,32 @@ def run(a, world):
         # (integration/ghpair_rate.cpp, hist_tree_builder.cpp:572-591): a child process, its own context
         exe = os.path.join(ROOT, "tools", "bin", "ghpair_rate")
         hl = {"note": "integration/ghpair_rate.cpp: OpenMP over features, `dest = dest + src` per instance through "
-                      "GHPair::operator+ on the USE_HIP key (2 fthe_add_shared per operator; empty bins promoted "
-                      "by 2 fthe_encrypt_shared), every bin checked by decryption; compare cpu_baseline.ops."
-                      "p2048_add (the reference's host Paillier_GMP::add, all lease threads)"}
+                      "GHPair::operator+ on the USE_HIP key (2 host adds x y mod n^2 per operator; empty bins "
+                      "promoted from the key's GPU-filled randomizer pool), every bin checked by decryption; "
+                      "reference_add_same_threads_per_s: the reference's Paillier_GMP::add (mpz_mul + mpz_mod) on "
+                      "the same threads and operands in the same run; compare cpu_baseline.ops.p2048_add too"}
         for thr in (16, 64):
             try:
-                r = subprocess.run([exe, str(KEY_BITS), str(thr), "512", "16"], capture_output=True, text=True,
+                r = subprocess.run([exe, str(KEY_BITS), str(thr), "8192", "16"], capture_output=True, text=True,
                                    timeout=180)
                 hl[f"threads_{thr}"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                     {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
             except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
                 hl[f"threads_{thr}"] = {"error": repr(ex)[:300]}
         secondary["histogram_loop_unchanged_callers"] = hl
+        # the batch boundary at FedTree's own types: Paillier_HIP::encrypt / decrypt(SyncArray<GHPair>&) with
+        # mpz_t marshalling of every ciphertext (integration/ghpair_e2e.cpp; server.h:105-135)
+        try:
+            r = subprocess.run([os.path.join(ROOT, "tools", "bin", "ghpair_e2e"), str(KEY_BITS), "2000000", "2"],
+                               capture_output=True, text=True, timeout=240)
+            ge = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+        except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
+            ge = {"error": repr(ex)[:300]}
+        ge["note"] = ("Server::encrypt_gh_pairs / decrypt_gh_pairs through Paillier_HIP on SyncArray<GHPair> with "
+                      "mpz_t fields (host in and out, PCIe, mpz import/export per ciphertext); compare "
+                      "e2e_host_encrypt_per_s (numpy rows) and the device-resident value")
+        secondary["ghpair_e2e"] = ge
         # key generation (homo_init; re-run every round in the vertical simulation, FLtrainer.cpp:556):
         # host prime search on up to 16 threads + device key set-up
         t0 = time.perf_counter()
@@ -796,6 +877,9 @@ def run(a, world):
         ch = pl.encrypt_u64(mh, seed=3)
         dt = time.perf_counter() - t0
         secondary["e2e_host_encrypt_per_s"] = round(ne / dt)
+        if "encrypts_per_s" in secondary.get("ghpair_e2e", {}):
+            secondary["ghpair_e2e"]["vs_e2e_host_encrypt"] = round(
+                secondary["ghpair_e2e"]["encrypts_per_s"] / secondary["e2e_host_encrypt_per_s"], 3)
         secondary["e2e_note"] = (f"{ne} ciphertexts, pageable numpy in/out ({ch.nbytes / 1e6:.0f} MB out), "
                                  "pinned staging + copy stream overlapped with compute")
         # the same with page-locked caller buffers (direct DMA)
@@ -862,8 +946,12 @@ def run(a, world):
                 bytes(hb_[int(ho_[i]):int(ho_[i + 1])].numpy()).decode() for i in range(256)])})
         del ch, strs, back, fr, g_, dbuf, doffs, dback, hb_, ho_
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a, pl, p1k_cpu, m, c, dev)
+    if rank == 0 and not a.no_cpu:                # after the timed region and its barrier, at every N
+        ca = argparse.Namespace(**vars(a))
+        if world > 1:
+            ca.cpu_scale = a.cpu_scale / 4             # N > 1: a quarter sample keeps the scaling runs short
+        cpu = cpu_baseline(ca, pl, p1k_cpu, m, c, dev)
+        cpu["n_gpus_of_run"] = world
 
     if rank == 0:
         line = {
@@ -874,7 +962,7 @@ def run(a, world):
             "config": {"workload": "Paillier-2048 encrypt of gradient pairs, device-resident, CRT (key holder)",
                        "pairs_per_gpu": P, "ciphertexts_per_gpu_per_step": 2 * P, "key_bits": KEY_BITS,
                        "parallelism": f"independent shards x{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "secondary": secondary,
+            "roofline": roof, "cpu_baseline": cpu, "ciphertext_adds": adds, "secondary": secondary,
             "per_rank": per_rank, "rank_time_max_s": round(elapsed, 4),
             "rank_time_min_s": round(min(p["elapsed_s"] for p in per_rank), 4),
         }
@@ -884,6 +972,7 @@ def run(a, world):
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()                                 # the other ranks wait for rank 0's CPU stage
         dist.destroy_process_group()
 
 

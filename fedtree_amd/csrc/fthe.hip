@@ -3694,8 +3694,10 @@ static Coalescer *key_coalescer(fthe_key *k) {
 // FLtrainer.cpp:758-764) ran two launches per round.  A new leader waits until as many requests are pending
 // as there were callers in the previous round (its batch plus the requests that arrived while it ran), at
 // most FTHE_LINGER_US (default 200 us; 0: off) or a quarter of the previous batch's duration if that is
-// longer (a merged decrypt takes ~10 ms); a lone caller never waits.  Arrivals wake it when the count is
-// reached.
+// longer (a merged decrypt takes ~10 ms), the latter capped at kLingerCapUs so one huge batch (a bulk
+// add_shared of millions of rows) cannot make the next leader wait for callers that never come back; a lone
+// caller never waits.  Arrivals wake it when the count is reached.
+static constexpr int64_t kLingerCapUs = 3000;
 static int linger_us() {
     static const int v = [] {
         const char *e = getenv("FTHE_LINGER_US");
@@ -3708,7 +3710,8 @@ static void linger(Coalescer *co, std::unique_lock<std::mutex> &lk, const std::v
                    bool &lingering, int64_t last_us) {
     if (last <= 1 || pend.size() >= last || linger_us() <= 0) return;
     lingering = true;
-    const int64_t bound = std::max<int64_t>(linger_us(), last_us / 4);   // a quarter of a long batch (decrypts)
+    // a quarter of a long batch (decrypts), capped: one huge batch must not make the next lone caller wait long
+    const int64_t bound = std::max<int64_t>(linger_us(), std::min<int64_t>(last_us / 4, kLingerCapUs));
     co->lcv.wait_for(lk, std::chrono::microseconds(bound), [&] { return pend.size() >= last; });
     lingering = false;
 }

@@ -140,6 +140,15 @@ class PublicBases(list):
         self.exp_bits = list(exp_bits)
 
 
+
+def _check_out(out, shape, what):
+    """A caller's output rows: the engine writes count x row words straight into them, so they must be a
+    C-contiguous uint32 array of exactly the operand's shape (a converted copy would take the result)."""
+    if not (isinstance(out, np.ndarray) and out.dtype == np.uint32 and out.flags.c_contiguous
+            and out.flags.writeable and out.shape == tuple(shape)):
+        raise ValueError(f"{what}: out must be a writable C-contiguous uint32 array of shape {tuple(shape)}")
+    return out
+
 class Paillier:
     """Paillier key + batch engine (mirror of Paillier / Paillier_GPU).
 
@@ -393,14 +402,16 @@ class Paillier:
         Paillier object, concurrent calls share a launch; out may be a or b (alias-safe)."""
         a = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self._cw())
         b = np.ascontiguousarray(b, dtype=np.uint32).reshape(-1, self._cw())
-        out = np.zeros_like(a) if out is None else out
+        if b.shape != a.shape:
+            raise ValueError(f"add_shared: operand shapes differ ({a.shape} vs {b.shape})")
+        out = np.zeros_like(a) if out is None else _check_out(out, a.shape, "add_shared")
         _lib.check(self.lib.fthe_add_shared(self._key, _ptr(a), _ptr(b), len(a), _ptr(out)), "add_shared")
         return out
 
     def scalar_mul_shared(self, x, k, out=None):
         """scalar_mul through the key's coalescing queue (fthe_scalar_mul_u64_shared)."""
         x = np.ascontiguousarray(x, dtype=np.uint32).reshape(-1, self._cw())
-        out = np.zeros_like(x) if out is None else out
+        out = np.zeros_like(x) if out is None else _check_out(out, x.shape, "scalar_mul_shared")
         _lib.check(self.lib.fthe_scalar_mul_u64_shared(self._key, _ptr(x), int(k), len(x), _ptr(out)),
                    "scalar_mul_shared")
         return out

@@ -88,13 +88,19 @@ public:
     // than 2^900 of them at P-2048 -- takes the p half of the CRT only (fthe_decrypt_short,
     // ~2x the decrypts/s, the same low 64 bits).  Not in the reference; off by default.
     bool dec_short = false;
-    // key_length = bits of n (the NTL meaning).  The default is the reference GPU build's
-    // key: Paillier_GPU::keygen() is paillier_cpu.keyGen(BITS = 1024), GMP semantics, a 512-bit n
-    // (paillier_gpu.cu:119-121, paillier_gpu.h:13), which is what homo_init's USE_CUDA branch
-    // (server.h:58-60) gets when it calls keygen() unchanged.  keygen(keylength) honours
-    // FLParam.key_length instead.
-    Paillier_HIP() : key_length(512) {}
+    // key_length = bits of n (the NTL meaning).  The default is a 2048-bit n.  The reference
+    // GPU build's keygen() is paillier_cpu.keyGen(BITS = 1024), GMP semantics, a 512-bit n
+    // (paillier_gpu.cu:119-121, paillier_gpu.h:13) -- factorable, so it is only the default when the
+    // build asks for the reference's weak key explicitly (-DFTHE_REFERENCE_GPU_KEYLEN).  keygen(keylength)
+    // honours FLParam.key_length.
+#ifdef FTHE_REFERENCE_GPU_KEYLEN
+    static constexpr uint32_t kDefaultKeyLength = 512;
+#else
+    static constexpr uint32_t kDefaultKeyLength = 2048;
+#endif
+    Paillier_HIP() : key_length(kDefaultKeyLength) {}
     Paillier_HIP(const Paillier_HIP &o) : key_length(o.key_length) { copy_public(o); }
+    ~Paillier_HIP() { disown(); }
 
     // Paillier_GPU::operator= (paillier_gpu.h:32-37): public part, re-uploaded.
     Paillier_HIP &operator=(const Paillier_HIP &source) {
@@ -198,11 +204,11 @@ public:
         message.h = fthe_shim::decode(m[1]);
     }
 
-    // Paillier_GPU::add / mul (paillier_gpu.cu:58-68): single values, alias-safe, through the key's
-    // shared queue (the GHPair key, paillier_cpu, is the same engine key).  Batch callers should use
-    // the helpers below or fthe_add / fthe_reduce_kway directly.
+    // Paillier_GPU::add / mul (paillier_gpu.cu:57-68): single values, alias-safe, into an initialised
+    // result -- add on the host (one product, as the reference), mul through the key's shared queue.
+    // Batch callers should use the helpers below or fthe_add / fthe_reduce_kway directly.
     void add(mpz_t &result, mpz_t &x, mpz_t &y) { paillier_cpu.add(result, x, y); }
-    void mul(mpz_t result, mpz_t &x, mpz_t &y) { paillier_cpu.mul(*reinterpret_cast<mpz_t *>(result), x, y); }
+    void mul(mpz_t result, mpz_t &x, mpz_t &y) { paillier_cpu.mul_into(result, x, y); }
 
     // ---- batch helpers for FedTree's HE call sites (not Paillier_GPU members) ----
     // Each replaces a loop of per-pair GHPair operators (CPU GMP, ~11.5 us per add) with one engine call.
@@ -354,9 +360,20 @@ private:
         return FTHE_ENC_DEFAULT;
     }
     void reset_bases() { bases_.clear(); base_bits_.clear(); nbases_ = 0; }
+    fthe_shim::KeyCell *owned_cell_ = nullptr;   // the cell whose randomizer pool this object keeps alive
+    void disown() {
+        if (owned_cell_) owned_cell_->release();
+        owned_cell_ = nullptr;
+    }
     void adopt(const fthe_key_ref &k) {
         key_ = k;
         paillier_cpu.bind(k, key_length);
+        fthe_shim::KeyCell *c = paillier_cpu.cell();
+        if (c != owned_cell_) {
+            c->retain();                          // first owner: the pool starts filling in the background
+            disown();
+            owned_cell_ = c;
+        }
     }
     void set_enc(GHPair &p, const uint32_t *g, const uint32_t *h, int cw) const {
         fthe_shim::from_words(p.g_enc, g, cw);
@@ -405,7 +422,7 @@ private:
         reset_bases();
         key_.reset();
         paillier_cpu = Paillier_HIP_Pub();
-        if (!o.key_) return;
+        if (!o.key_) { disown(); return; }
         const int nw = fthe_key_n_words(o.key_.get());
         std::vector<uint32_t> w(nw);
         fthe_shim::to_words(o.paillier_cpu.n, w.data(), nw);

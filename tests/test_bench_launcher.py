@@ -31,6 +31,14 @@ def test_spawns_n_ranks():
     assert len({p["pid"] for p in per}) == 2             # two processes
     assert line["elapsed_max_s"] == max(p["elapsed_s"] for p in per)
     assert line["elapsed_max_s"] >= 3 * 0.02
+    # the N > 1 line carries the same blocks as N = 1: roofline, rank 0's CPU baseline and every
+    # rank's ciphertext adds/s with the aggregate over the slowest rank
+    assert "roofline" in line and "cpu_baseline" in line and line["cpu_baseline"]["cores"] >= 1
+    adds = line["ciphertext_adds"]
+    assert sorted(p["rank"] for p in adds["per_rank"]) == [0, 1]
+    assert all(p["adds_per_s"] > 0 for p in adds["per_rank"])
+    slow = max(p["median_s"] for p in adds["per_rank"])
+    assert adds["aggregate_adds_per_s"] == round(2 * adds["adds_per_rank"] / slow)
 
 
 def test_single_rank_default():

@@ -37,6 +37,48 @@ def test_shim_compiles_and_links(tmp_path):
     _build(str(tmp_path / "shim_abort"), extra=("-DFTHE_SHIM_ABORT",))
     _build(str(tmp_path / "ghpair_test"), "ghpair_test.cpp", extra=("-DFTHE_REFERENCE_SHARED_R",))
     _build(str(tmp_path / "ghpair_rate"), "ghpair_rate.cpp", extra=("-fopenmp",))
+    _build(str(tmp_path / "host_ops_test"), "host_ops_test.cpp", extra=("-fopenmp",))
+    _build(str(tmp_path / "pool_test"), "pool_test.cpp", extra=("-fopenmp",))
+    _build(str(tmp_path / "shim_refkeylen"), extra=("-DFTHE_REFERENCE_GPU_KEYLEN",))
+
+
+def test_default_key_length_is_2048_unless_reference_keylen_requested(tmp_path):
+    """keygen() with no argument makes a 2048-bit n; the reference GPU build's factorable 512-bit n
+    (paillier_gpu.cu:119-121) only with -DFTHE_REFERENCE_GPU_KEYLEN."""
+    src = tmp_path / "kl.cpp"
+    src.write_text('#include "paillier_hip.h"\n#include <cstdio>\n'
+                   'int main() { Paillier_HIP s; std::printf("%u\\n", s.key_length); return 0; }\n')
+    for extra, want in (((), "2048"), (("-DFTHE_REFERENCE_GPU_KEYLEN",), "512")):
+        exe = str(tmp_path / ("kl" + str(len(extra))))
+        r = subprocess.run(["g++", "-std=c++17", "-pthread", *extra, "-I" + INTEG, "-I" + os.path.join(INTEG, "mock"),
+                            "-I" + os.path.join(ROOT, "include"), "-idirafter", "/opt/conda/include", str(src), "-o",
+                            exe, "-L" + os.path.join(ROOT, "fedtree_amd"), "-lfthe",
+                            "-Wl,-rpath," + os.path.join(ROOT, "fedtree_amd"), "-l:libgmp.so.10"],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        out = subprocess.run([exe], capture_output=True, text=True)
+        assert out.returncode == 0 and out.stdout.strip() == want, out.stdout + out.stderr
+
+
+def _adds_fixture(path, name):
+    g = load_golden(name)
+    p, q = golden_key(g)
+    cts = [int(c["c"], 16) for c in g["cases"]]
+    lines = [f"{p * q:x}"] + [f"{cts[a['i']]:x} {cts[a['j']]:x} {_hx(a['c'])}" for a in g["adds"]]
+    path.write_text("\n".join(lines) + "\n")
+
+
+@pytest.mark.parametrize("name", ["ref_gmp_L1024.json", "ref_gmp_L2048.json", "ref_gmp_L4096.json"])
+def test_ghpair_host_add_bit_exact_without_gpu(tmp_path, name):
+    """The GHPair key's add runs on the host (one product x y mod n^2, as paillier_gpu.cu:57-61): bound to
+    a public n only, operator+, the aliased += and add(s, s, c) give the reference's golden adds, also for
+    unreduced operands; key copies share one cell and read n, n^2, g through views (no GPU needed)."""
+    fx = tmp_path / "adds.txt"
+    _adds_fixture(fx, name)
+    exe = str(tmp_path / "host_ops_test")
+    _build(exe, "host_ops_test.cpp", extra=("-fopenmp",))
+    r = subprocess.run([exe, "check", str(fx)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "host ops OK" in r.stdout, r.stdout + r.stderr
 
 
 def test_nonreference_modes_need_the_build_opt_in(tmp_path):
@@ -150,3 +192,52 @@ def test_ghpair_operators_bit_exact_on_engine(tmp_path, name):
     _build(exe, "ghpair_test.cpp", extra=("-DFTHE_REFERENCE_SHARED_R",))
     r = subprocess.run([exe, str(fx)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ghpair OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def _rebuild_r(p, q, yp, yq):
+    """r = CRT(y_p^(q^-1 mod p-1) mod p, y_q^(p^-1 mod q-1) mod q) (the direct-y draw, tests/test_gpu_direct_y.py)."""
+    ep, eq, qinv = pow(q, -1, p - 1), pow(p, -1, q - 1), pow(q, -1, p)
+    rp, rq = pow(yp, ep, p), pow(yq, eq, q)
+    return (rq + q * ((rp - rq) * qinv % p)) % (p * q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_gmp_L1024.json", "ref_gmp_L4096.json"])
+def test_pooled_promotions_equal_oracle_encrypt(tmp_path, name):
+    """GHPair promotions (homo_encrypt, common.h:75-97) from the key's randomizer pool: (1 + m n) rho mod n^2
+    with rho an engine Enc(0).  With deterministic pool batches, the r behind each pooled row is rebuilt
+    from the engine's direct-y draws and the promoted ciphertext equals the oracle's full-PowerMod
+    encrypt(m, r) (paillier.cpp:134-137), across three pool batches, for m = 0, 1, 2^64 - 1 and codec values."""
+    from fedtree_amd.paillier import Device, Paillier
+    g = load_golden(name)
+    p, q = golden_key(g)
+    key = pyoracle.keygen_from_primes(p, q)
+    ms = [0, 1, 2**64 - 1, 2**63, 123456789, (2**64 - 300000), 5, 0, 77, 2**32 + 1, 999999, 42, 0, 3, 2**62 + 7]
+    exe = str(tmp_path / "pool_test")
+    _build(exe, "pool_test.cpp", extra=("-fopenmp",))
+    seed0, batch = 7001, 6
+    r = subprocess.run([exe, "trace", f"{p:x}", f"{q:x}", str(seed0), str(batch)] + [str(m) for m in ms],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rows = [ln.split() for ln in r.stdout.strip().splitlines()]
+    assert len(rows) == len(ms)
+    pl = Paillier.from_primes(p, q, Device(0))
+    pw = (max(p.bit_length(), q.bit_length()) + 31) // 32
+    for k, (m_s, seed_s, idx_s, c_hex) in enumerate(rows):
+        m, seed, idx = int(m_s), int(seed_s), int(idx_s)
+        assert m == ms[k] and seed == seed0 + k // batch and idx == k % batch
+        yp, yq = pl.direct_y(seed, idx, 1)
+        r_ = _rebuild_r(p, q, pyoracle.words_to_ints(yp.reshape(1, pw))[0], pyoracle.words_to_ints(yq.reshape(1, pw))[0])
+        assert int(c_hex, 16) == pyoracle.encrypt(key, m, r_), (k, m)
+
+
+@pytest.mark.gpu
+def test_pooled_promotions_from_threads(tmp_path):
+    """16 OpenMP threads promote 2 x 16 x 300 plain GHPairs (codec values and zeros) at once: every pair
+    decrypts to its codec values and no pooled randomizer is used twice (all 19,200 ciphertexts distinct)."""
+    g = load_golden("ref_gmp_L4096.json")
+    p, q = golden_key(g)
+    exe = str(tmp_path / "pool_test")
+    _build(exe, "pool_test.cpp", extra=("-fopenmp",))
+    r = subprocess.run([exe, "threads", f"{p:x}", f"{q:x}", "16", "300"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "pool OK" in r.stdout, r.stdout + r.stderr

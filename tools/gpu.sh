@@ -1,0 +1,94 @@
+#!/bin/bash
+# The one GPU lease script: run the named steps in order on the gpurun box, stop at the first failure.
+#   bash tools/gpu.sh TAG STEP [STEP ...]
+# Steps (outputs under gpurun_out/, prefixed with TAG):
+#   suite          python -m pytest tests -m gpu (thread timeouts: a hang names its test)
+#   smoke          __graft_entry__.smoke()
+#   bench          python bench.py (the driver's default line)              -> TAG_bench.json
+#   bench:ARGS     python bench.py ARGS (comma-separated, e.g. bench:--steps,3)
+#   trace          the bench's timed region under rocprofv3 --kernel-trace --stats
+#   pmc:W          separate PMC passes (one counter group per run, never with tracing) over workload W:
+#                    enc  the bench's encrypt at 262,144 pairs (fthe_padic_m37 + s74 tails)
+#                    add  one device-resident P-2048 add of 1M ciphertexts (s152 row I/O)
+#                    kway one 8-party merge of 262,144 bins
+#                    pub  public-key encrypt of 131,072 ciphertexts (tools/nadic_ab.py)
+#                  then: python tools/rocprof_summary.py pmc gpurun_out/TAG_pmc_W_* out.json (CPU side)
+#   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo)
+#   ghpair         tools/bin/ghpair_rate at 16 and 64 threads, tools/bin/ghpair_e2e
+#   py:SCRIPT[,ARGS]  python SCRIPT ARGS (a tools/ measurement), appended to TAG_SCRIPT.jsonl
+R=${1:?tag}
+shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out/${R}
+fail() { echo "step $1 failed (rc $2)"; tail -30 "$3" 2>/dev/null; exit 1; }
+pmc_pass() {  # workload tag counters...
+  local w=$1 tag=$2; shift 2
+  local cmd
+  case $w in
+    enc)  cmd="python3 bench.py --pairs 262144 --steps 1 --warmup 0 --no-cpu --no-secondary";;
+    add)  cmd="python3 tools/prof_ops.py --n 1048576 --ops add";;
+    kway) cmd="python3 tools/prof_ops.py --n 262144 --ops kway";;
+    pub)  cmd="python3 tools/nadic_ab.py 131072";;
+    *) echo "unknown pmc workload $w"; exit 2;;
+  esac
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d ${O}_pmc_${w}_${tag} -- $cmd \
+    > ${O}_pmc_${w}_${tag}.log 2>&1 || fail "pmc:$w:$tag" $? ${O}_pmc_${w}_${tag}.log
+}
+for step in "$@"; do
+  echo "[gpu.sh] $step at $(date +%T)"
+  case $step in
+    suite)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > ${O}_pytest_gpu.txt 2>&1 || fail suite $? ${O}_pytest_gpu.txt
+      tail -3 ${O}_pytest_gpu.txt;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.txt 2>&1 \
+        || fail smoke $? ${O}_smoke.txt
+      cat ${O}_smoke.txt;;
+    bench)
+      timeout -k 10 900 python bench.py > ${O}_bench.json 2> ${O}_bench.err || fail bench $? ${O}_bench.err
+      cut -c1-600 ${O}_bench.json;;
+    bench:*)
+      args=${step#bench:}
+      timeout -k 10 900 python bench.py ${args//,/ } > ${O}_bench_args.json 2> ${O}_bench_args.err \
+        || fail "$step" $? ${O}_bench_args.err
+      cut -c1-600 ${O}_bench_args.json;;
+    trace)
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_trace -o bench -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu --no-secondary > ${O}_bench_under_rocprof.json \
+        2> ${O}_rocprof.err || fail trace $? ${O}_rocprof.err;;
+    pmc:*)
+      w=${step#pmc:}
+      pmc_pass $w fetch FETCH_SIZE
+      pmc_pass $w write WRITE_SIZE
+      pmc_pass $w vb VALUBusy
+      pmc_pass $w occ OccupancyPercent
+      pmc_pass $w sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE
+      pmc_pass $w mf SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY;;
+    rehearse)
+      FTHE_BENCH_REHEARSE=1 timeout -k 10 600 python bench.py --gpus 2 --pairs 1048576 --steps 2 --warmup 1 \
+        > ${O}_rehearse_2rank_1gpu.json 2> ${O}_rehearse.err || fail rehearse $? ${O}_rehearse.err
+      cut -c1-600 ${O}_rehearse_2rank_1gpu.json;;
+    ghpair)
+      for t in 16 64; do
+        timeout -k 10 300 tools/bin/ghpair_rate 2048 $t 8192 16 >> ${O}_ghpair_rate.jsonl 2>> ${O}_ghpair.err \
+          || fail ghpair_rate $? ${O}_ghpair.err
+      done
+      timeout -k 10 300 tools/bin/ghpair_e2e 2048 2000000 2 >> ${O}_ghpair_e2e.jsonl 2>> ${O}_ghpair.err \
+        || fail ghpair_e2e $? ${O}_ghpair.err
+      cat ${O}_ghpair_rate.jsonl ${O}_ghpair_e2e.jsonl;;
+    py:*)
+      spec=${step#py:}
+      script=${spec%%,*}
+      args=""
+      [ "$script" != "$spec" ] && args=${spec#*,}
+      name=$(basename $script .py)
+      timeout -k 10 600 python $script ${args//,/ } >> ${O}_${name}.jsonl 2>> ${O}_${name}.err \
+        || fail "$step" $? ${O}_${name}.err
+      tail -5 ${O}_${name}.jsonl;;
+    *) echo "unknown step $step"; exit 2;;
+  esac
+done
+echo "[gpu.sh] done at $(date +%T)"
