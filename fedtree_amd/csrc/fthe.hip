@@ -508,6 +508,18 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
     return FTHE_OK;
 }
 
+extern "C" int fthe_host_alloc(size_t bytes, void **out) {
+    if (!out) return FTHE_ERR_ARG;
+    *out = nullptr;
+    if (bytes == 0) return FTHE_OK;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) { *out = nullptr; return FTHE_ERR_HIP; }
+    return FTHE_OK;
+}
+
+extern "C" void fthe_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);

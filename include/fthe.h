@@ -67,6 +67,11 @@ void  fthe_ctx_destroy(fthe_ctx *ctx);
 int   fthe_ctx_sync(fthe_ctx *ctx);
 void *fthe_ctx_stream(fthe_ctx *ctx);       /* hipStream_t */
 int   fthe_ctx_device(fthe_ctx *ctx);
+/* Page-locked host memory for caller row buffers: host-resident calls then DMA straight from / into
+ * it instead of staging through the context's pinned chunks (the drop-in class keeps one per thread for
+ * encrypt / decrypt(SyncArray<GHPair>&), reused across calls: pinning is paid once). */
+int   fthe_host_alloc(size_t bytes, void **out);
+void  fthe_host_free(void *p);
 
 /* ---- keys ----------------------------------------------------------------
  * fthe_key_generate      Paillier::keygen(int keyLength), paillier.cpp:66-90:

@@ -55,6 +55,28 @@ inline void parallel_for(size_t n, F f) {
     for (auto &x : th) x.join();
     for (auto &e : err) if (e) std::rethrow_exception(e);
 }
+// Page-locked row buffers of the calling thread (fthe_host_alloc), grown on demand and kept across calls:
+// the batch calls then DMA straight from / into them (no pinned staging copy, no page faults on a fresh
+// multi-GB vector), and pinning is paid once per thread, not per encrypt_gh_pairs.
+template <class T>
+inline T *pinned(int slot, size_t count) {
+    struct Buf {
+        void *p = nullptr;
+        size_t cap = 0;
+        ~Buf() { fthe_host_free(p); }
+    };
+    static thread_local Buf bufs[2];
+    Buf &b = bufs[slot];
+    const size_t bytes = std::max<size_t>(1, count) * sizeof(T);
+    if (b.cap < bytes) {
+        fthe_host_free(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+        check(fthe_host_alloc(bytes, &b.p), "host_alloc");
+        b.cap = bytes;
+    }
+    return static_cast<T *>(b.p);
+}
 // codec of common.h:81-86 and paillier_gpu.cu:487
 inline uint64_t encode(float_type v) { long l = (long)(v * 1e6); return (uint64_t)l; }
 inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 1e6; }
@@ -151,13 +173,14 @@ public:
     void encrypt(SyncArray<GHPair> &message) {
         auto *d = message.host_data();
         size_t n = message.size();
+        if (n == 0) return;
         int nw = fthe_key_n_words(key()), cw = 2 * nw;
-        std::vector<uint64_t> m(2 * n);
+        uint64_t *m = fthe_shim::pinned<uint64_t>(0, 2 * n);
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
         });
-        std::vector<uint32_t> c(2 * n * (size_t)cw);
-        fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m.data(), 2 * n, nullptr, 0, 0, c.data(),
+        uint32_t *c = fthe_shim::pinned<uint32_t>(1, 2 * n * (size_t)cw);
+        fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m, 2 * n, nullptr, 0, 0, c,
                                           eff_flags()), "encrypt");
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) {
@@ -171,18 +194,23 @@ public:
     void decrypt(SyncArray<GHPair> &message) {
         auto *d = message.host_data();
         size_t n = message.size();
+        if (n == 0) return;
         int nw = fthe_key_n_words(key()), cw = 2 * nw;
-        std::vector<uint32_t> c(2 * n * (size_t)cw, 0);
+        uint32_t *c = fthe_shim::pinned<uint32_t>(1, 2 * n * (size_t)cw);
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {      // to_words throws only on oversize input
             for (size_t i = b; i < e; i++) {
-                if (!d[i].encrypted) continue;
+                if (!d[i].encrypted) {                               // rows of unencrypted pairs: zeros
+                    std::fill(&c[i * cw], &c[(i + 1) * cw], 0u);
+                    std::fill(&c[(n + i) * cw], &c[(n + i + 1) * cw], 0u);
+                    continue;
+                }
                 fthe_shim::to_words(d[i].g_enc, &c[i * cw], cw);
                 fthe_shim::to_words(d[i].h_enc, &c[(n + i) * cw], cw);
             }
         });
-        std::vector<uint64_t> m(2 * n);
-        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key(), fthe_shim::thread_ctx(), c.data(),
-                                                                         2 * n, m.data(), nullptr), "decrypt");
+        uint64_t *m = fthe_shim::pinned<uint64_t>(0, 2 * n);
+        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key(), fthe_shim::thread_ctx(), c,
+                                                                         2 * n, m, nullptr), "decrypt");
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++)
                 if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }

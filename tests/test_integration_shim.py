@@ -68,6 +68,47 @@ def _adds_fixture(path, name):
     path.write_text("\n".join(lines) + "\n")
 
 
+REF_INC = "/root/reference/include"
+PATCH = os.path.join(INTEG, "common_h_use_hip.patch")
+
+
+def _cmake_configure(template, out):
+    """config.h from the reference's config.h.in the way CMake's configure_file writes it with none of the
+    options set (every `#cmakedefine VAR ...` becomes `/* #undef VAR */`): the generated header of a
+    plain build, produced by the same rule, not a stand-in written for the test."""
+    lines = []
+    for ln in open(template).read().splitlines():
+        m = re.match(r"#cmakedefine\s+(\w+)", ln)
+        lines.append(f"/* #undef {m.group(1)} */" if m else ln)
+    out.write_text("\n".join(lines) + "\n")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_COMMON), reason="reference sources absent (GPU box)")
+@pytest.mark.parametrize("name", ["ref_gmp_L1024.json", "ref_gmp_L4096.json"])
+def test_reference_common_h_patched_compiles_and_adds(tmp_path, name):
+    """The reference's own common.h, copied into a temporary tree and patched with
+    integration/common_h_use_hip.patch, compiles with -DUSE_HIP against
+    fthe_ghpair_key.h (hipcc: common.h includes thrust/tuple.h), and its unchanged operator bodies give
+    the golden adds through operator+, += and dest = dest + src on a host-bound key."""
+    fed = tmp_path / "inc" / "FedTree"
+    fed.mkdir(parents=True)
+    (fed / "common.h").write_text(open(REF_COMMON).read())
+    r = subprocess.run(["patch", "-s", "-p3", "-d", str(fed), "-i", PATCH], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    _cmake_configure(os.path.join(REF_INC, "FedTree", "config.h.in"), fed / "config.h")
+    exe = str(tmp_path / "real_common_test")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O2", "-DUSE_HIP", "--offload-arch=gfx950",
+                        "-I" + str(tmp_path / "inc"), "-I" + REF_INC, "-I" + INTEG, "-I" + os.path.join(ROOT, "include"),
+                        "-idirafter", "/opt/conda/include", os.path.join(INTEG, "real_common_test.cpp"), "-o", exe,
+                        "-L" + os.path.join(ROOT, "fedtree_amd"), "-lfthe", "-Wl,-rpath," + os.path.join(ROOT, "fedtree_amd"),
+                        "-l:libgmp.so.10", "-pthread"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    fx = tmp_path / "adds.txt"
+    _adds_fixture(fx, name)
+    r = subprocess.run([exe, str(fx)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "real common.h OK" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("name", ["ref_gmp_L1024.json", "ref_gmp_L2048.json", "ref_gmp_L4096.json"])
 def test_ghpair_host_add_bit_exact_without_gpu(tmp_path, name):
     """The GHPair key's add runs on the host (one product x y mod n^2, as paillier_gpu.cu:57-61): bound to
