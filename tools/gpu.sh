@@ -13,6 +13,7 @@
 #                    kway one 8-party merge of 262,144 bins
 #                    pub  public-key encrypt of 131,072 ciphertexts (tools/nadic_ab.py)
 #                  then: python tools/rocprof_summary.py pmc gpurun_out/TAG_pmc_W_* out.json (CPU side)
+#   opstrace       kernel trace of tools/prof_ops.py add,kway (the add / merge launch durations for pmc:add)
 #   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo)
 #   ghpair         tools/bin/ghpair_rate at 16 and 64 threads, tools/bin/ghpair_e2e
 #   py:SCRIPT[,ARGS]  python SCRIPT ARGS (a tools/ measurement), appended to TAG_SCRIPT.jsonl
@@ -67,6 +68,9 @@ for step in "$@"; do
       pmc_pass $w sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS \
         SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE
       pmc_pass $w mf SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY;;
+    opstrace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_ops_trace -o ops -- \
+        python3 tools/prof_ops.py --n 1048576 --ops add,kway > ${O}_ops_trace.log 2>&1 || fail opstrace $? ${O}_ops_trace.log;;
     rehearse)
       FTHE_BENCH_REHEARSE=1 timeout -k 10 600 python bench.py --gpus 2 --pairs 1048576 --steps 2 --warmup 1 \
         > ${O}_rehearse_2rank_1gpu.json 2> ${O}_rehearse.err || fail rehearse $? ${O}_rehearse.err

@@ -110,7 +110,7 @@ def pmc_round(tag, out):
     res = {}
     for w in ("enc", "add", "kway", "pub"):
         per = {}
-        for t in ("fetch", "write", "vb", "occ", "sq"):
+        for t in ("fetch", "write", "vb", "occ", "sq", "mf"):
             for f in glob.glob(f"gpurun_out/{tag}_pmc_{w}_{t}/**/*counter_collection.csv", recursive=True):
                 acc = {}
                 for r in csv.DictReader(open(f)):
