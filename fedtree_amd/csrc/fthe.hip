@@ -33,6 +33,7 @@
 #include "../../include/fthe.h"
 #include "bn_host.hpp"
 #include "padic_tiles.hpp"
+#include "addb_image.hpp"
 #include "fthe_glue.h"
 #include "gen/montprog_blobs.h"
 
@@ -55,6 +56,7 @@ const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {
                                        {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}, {kNadicS, 27, 4},
                                        {kPadicMfmaS, 28, 1}};
 constexpr Shape kLatShape{80, 27, 4};
+constexpr int kAddbBlob = 3152;           // fthe_addb_q152's code object in gen/montprog_blobs.h
 
 int variant_index(int S) {
     for (int i = 0; i < MAX_VARIANTS; i++) if (kVariants[i].S == S) return i;
@@ -219,6 +221,8 @@ struct fthe_ctx {
     hipEvent_t ev_done[2] = {}, ev_copied[2] = {}, ev_in[2] = {};
     hipModule_t mod[MAX_VARIANTS] = {};
     hipFunction_t fn[MAX_VARIANTS] = {};
+    hipModule_t mod_addb = nullptr;           // fthe_addb_q152 (gen_addb.py): P-2048 adds, matrix-core Barrett
+    hipFunction_t fn_addb = nullptr;
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
     DevBuf hb[6];                           // histogram CSR / segmented-product plan (device)
     DevBuf ezm;                             // zero-first folds: Enc(0) rows masked to the populated segments
@@ -337,6 +341,7 @@ struct fthe_key {
         if (d_progs) (void)hipFree(d_progs);
         if (d_nwords) (void)hipFree(d_nwords);
         if (d_pqwords) (void)hipFree(d_pqwords);
+        if (d_addb) (void)hipFree(d_addb);
         for (uint32_t *p : {fb.d_tab_pub, fb.d_tab_p, fb.d_tab_q, fb.d_prog}) if (p) (void)hipFree(p);
         for (uint32_t *p : {xb.d_tab[0], xb.d_tab[1], xb.d_prog}) if (p) (void)hipFree(p);
         if (pb.d_prog) (void)hipFree(pb.d_prog);           // pb.tab: shared, freed by its last key
@@ -370,6 +375,7 @@ struct fthe_key {
     PH pr_add_w, pr_sub_w;     // row-I/O forms (four-lane kernel, 128-word rows)
     bool rowio = false;
     bool add_classical = false;               // pr_add_w is one classical product (no R^2 constant)
+    void *d_addb = nullptr;                   // fthe_addb_q152's per-key context (addb_image.hpp): n of 2048 bits
     PH pr_enc_pub, pr_add, pr_sub, pr_enc_p, pr_enc_q, pr_enc_p_nt, pr_enc_tail, pr_dec_pl, pr_dec_ql, pr_enc_pl, pr_enc_ql, pr_dec_p, pr_dec_q, pr_dec_hp, pr_dec_hq, pr_dec_t;
     PH pr_encA_p, pr_encA_q;      // stage A of the CRT encrypt (mod p, q; small kernel)
     // P-adic form of stage B: the exponentiation (P-adic kernel), then the rest on s74
@@ -501,6 +507,10 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         HIPOK(hipModuleGetFunction(&c->fn[i], c->mod[i], name));
         HIPOK(hipFuncGetAttribute(&c->static_lds[i], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, c->fn[i]));
     }
+    if (const unsigned char *blob = fthe_montprog_blob(kAddbBlob)) {
+        HIPOK(hipModuleLoadData(&c->mod_addb, blob));
+        HIPOK(hipModuleGetFunction(&c->fn_addb, c->mod_addb, "fthe_addb_q152"));
+    }
     HIPOK(hipEventCreate(&c->ev0));
     HIPOK(hipEventCreate(&c->ev1));
     HIPOK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
@@ -527,6 +537,7 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->side) (void)hipStreamSynchronize(c->side);
     for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) (void)hipModuleUnload(c->mod[i]);
+    if (c->mod_addb) (void)hipModuleUnload(c->mod_addb);
     if (c->cub_tmp) (void)hipFree(c->cub_tmp);
     for (auto &e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -796,6 +807,13 @@ static int key_finish(fthe_key *k) {
             Prog sw;
             sw.loadw(1); sw.mul(SL_C0); sw.pow_ones(64, SL_T0, SL_T1); sw.mulw(0); sw.storew(2); sw.end();
             k->pr_sub_w = k->add_prog(sw);
+            // pairwise adds with the Barrett reduction on the matrix cores (fthe_addb_q152) when n has 2048
+            // bits; FTHE_ADD_NO_ADDB=1 keeps the classical product on the four-lane kernel (bit-identical)
+            std::vector<uint8_t> img;
+            if (k->add_classical && !getenv("FTHE_ADD_NO_ADDB") && addb::build(k->n, img)) {
+                HIPOK(hipMalloc(&k->d_addb, img.size()));
+                HIPOK(hipMemcpy(k->d_addb, img.data(), img.size(), hipMemcpyHostToDevice));
+            }
         }
     }
     if (k->priv) {
@@ -2934,6 +2952,40 @@ extern "C" int fthe_decrypt_short_dev(fthe_key *k, fthe_ctx *c, const uint32_t *
 
 // ---------------------------------------------------------------------------
 // Add / k-way product / scalar mul (mod n^2)
+
+// out = x y mod n^2 for count rows on fthe_addb_q152 (gen_addb.py): 16 rows per wave, 12 waves per workgroup
+static int launch_addb(fthe_ctx *c, const fthe_key *k, const uint32_t *x, const uint32_t *y, uint32_t *out,
+                       size_t count) {
+    if (count == 0) return FTHE_OK;
+    if (count > 0xFFFFFFFFu / 2) return FTHE_ERR_ARG;
+    struct { const void *x, *y; void *o; const void *kc; uint32_t count, pad; } args = {x, y, out, k->d_addb,
+                                                                                      (uint32_t)count, 0};
+    static_assert(sizeof(args) == 40, "kernarg layout of gen_addb.py");
+    size_t sz = sizeof(args);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    const unsigned blocks = (unsigned)((count + kAddbPerWg - 1) / kAddbPerWg);
+    if (hipModuleLaunchKernel(c->fn_addb, blocks, 1, 1, 64 * kAddbWaves, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
+        return FTHE_ERR_HIP;
+    return FTHE_OK;
+}
+
+// Test hook (include/fthe.h): the per-key context bytes of fthe_addb_q152, host only.
+extern "C" int fthe_debug_addb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len) {
+    if (!n || n_words <= 0 || !len) return FTHE_ERR_ARG;
+    mpz_t nn;
+    mpz_init(nn);
+    mpz_import(nn, (size_t)n_words, -1, 4, 0, 0, n);
+    std::vector<uint8_t> img;
+    const bool ok = addb::build(nn, img);
+    mpz_clear(nn);
+    if (!ok) return FTHE_ERR_UNSUPPORTED;
+    *len = img.size();
+    if (!out) return FTHE_OK;
+    if (cap < img.size()) return FTHE_ERR_ARG;
+    memcpy(out, img.data(), img.size());
+    return FTHE_OK;
+}
+
 static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out,
                      HostPipe *pipe, bool sub) {
     if (!k || !c || ((!a || !b || !out) && count)) return FTHE_ERR_ARG;
@@ -2945,12 +2997,16 @@ static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t
                       : begin_call(c, k, count, Lc, nslots_for(k), k->sn2);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
+    const bool addb = !sub && k->d_addb && c->fn_addb;
     if (sub || !k->rowio || !k->add_classical) Lc.fill(SL_C0, k->c_R2n2);    // the classical add needs no R^2
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);
         Lc.live = cnt;
         if (pipe && (rc = pipe->before(off, L, count))) return rc;
-        if (k->rowio) {
+        if (addb) {
+            if ((rc = launch_addb(c, k, a + off * cw, b + off * cw, out + off * cw, cnt))) return rc;
+            Lc.mm += (double)cnt;
+        } else if (k->rowio) {
             const void *rows[3] = {a + off * cw, b + off * cw, out + off * cw};
             if ((rc = Lc.prog(sub ? k->pr_sub_w : k->pr_add_w, k->mn2, rows, 3))) return rc;
         } else {

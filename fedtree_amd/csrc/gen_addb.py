@@ -1,0 +1,633 @@
+#!/usr/bin/env python3
+"""Generator of the Paillier-2048 ciphertext-add kernel with a matrix-core Barrett reduction (gfx950 assembly):
+fthe_addb_q152, out[g] = x[g] y[g] mod N for N = n^2 (4095-4096 bits), canonical 128-word rows in and out
+(paillier.cpp:92-105, paillier_gmp.cpp:16-21).  tools/addb_model.py is the bit-exact model of the
+arithmetic (parameters, bounds, column corrections); this file lays it out on the machine.
+
+One quad of lanes per ciphertext (lane j of the quad owns limbs [38j, 38j+38) of 27 bits), 16 ciphertexts
+per wave, 12 waves per workgroup (one workgroup per CU: its LDS holds the key's constant images once).
+
+  1. rows -> limbs (the row I/O of gen_montprog.gen_quad); y's limbs become the wave's A column in LDS.
+  2. z = x y on the VALU: 152 operand-scanning steps, 38 v_mad_u64_u32 per lane per step into a ring of
+     64-bit columns; the lowest column of lane 0 retires as limb z_i (written back into the A column row i,
+     whose a_i was consumed the step before) -- the Montgomery step of gen_quad without its q N half.
+  3. The window (z >> 4104) is normalised; z >> 4104 and z mod 2^4104 become dwords in the quad layout
+     (lane j: dwords [32j, 32j+32)); q1 = z >> 4072 = [bits 4072..4103, (z >> 4104)] goes to a staging row
+     per ciphertext, bytes fed as b ^ 0x80 (= b - 128, signed), padded with zero (fed 0) bytes.
+  4. Product 1 (q1 mu, output byte columns 512..1039) on v_mfma_i32_16x16x64_i8: the B operand is 64 bytes x
+     16 ciphertexts (lane l: ciphertext l & 15, bytes 16 (l >> 4) .. +15 of the K-block), the A operand a
+     16 x 64 Toeplitz tile of mu's balanced digits (lane l: output row l & 15, the same 16 K bytes), read
+     from one of 16 byte-shifted copies of mu so every read is one aligned ds_read_b128; the int32
+     accumulators start from the column corrections (128 sum mu[s - k], and the -2^4121 bias).  Only the
+     tiles whose constant entries are not all zero are issued (185 of 297).
+  5. Each lane folds its 4 rows of a tile into an int64 group P_G = sum_i C_i 256^i (G = 4 t + (l >> 4)),
+     the groups go through LDS, and quad lane j normalises the groups of chunk j (output tiles 8j .. 8j+7,
+     chunk 3: 24 .. 32) into dwords with a signed carry handed on by DPP: q3 = floor(N1 / 2^4128) = the
+     dwords of groups 1..128 (clamped to 0 when the sum is negative).
+  6. q3 -> staging -> B; product 2 (q3 N mod 2^4104, columns 0..527, 153 tiles; q3 has 129 dwords so that
+     rows >= N, which the reference reduces too, stay exact) and its fold give r2;
+     r = (z - r2) mod 2^4104 (dword borrow chains, rippled across the quad) lies in [0, 3N); two
+     conditional subtractions of N (dwords from the key's context) make it canonical; rows are stored.
+
+kernarg: 0 u64 x rows, 8 u64 y rows, 16 u64 out rows, 24 u64 kctx, 32 u32 count.
+kctx: the LDS image (IMG_BYTES: mu copies, N copies, corrections), then N as 128 dwords.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# ---- layout constants shared with the host image builder (fthe.hip addb_image) and tools/addb_model.py ----
+S, Q, B = 152, 38, 27
+MASK = (1 << B) - 1
+WAVES = 12                       # waves per workgroup (one workgroup per CU, 3 waves per SIMD)
+CT_PER_WAVE = 16
+RB = 68                          # A-column row: 16 ciphertexts x 4 B + pad (gen_quad's QUAD_ROWB)
+COPY = 800                       # one byte-shifted copy of a constant (== 32 mod 256: conflict-free reads)
+KO1, KO2 = 64, 560               # copy offsets: y = KO + 16 (4 kb - t) + 16 h
+A1_OFF = 0
+A2_OFF = A1_OFF + 16 * COPY
+TILES1, TILES2 = 33, 33
+CORR1_OFF = A2_OFF + 16 * COPY
+CORR2_OFF = CORR1_OFF + TILES1 * 64
+IMG_BYTES = CORR2_OFF + TILES2 * 64          # 29,824
+N_OFF = IMG_BYTES                            # N dwords in kctx (not copied to LDS)
+KCTX_BYTES = N_OFF + 512
+WAVE_AREA = S * RB                           # 10,336: A column / q staging (16 x 576) / groups (16 x 296)
+LDS_WAVES = IMG_BYTES
+LDS_BYTES = LDS_WAVES + WAVES * WAVE_AREA    # 153,856
+QROW = 576                                   # q staging row (9 K-blocks of 64 bytes)
+GROW = 296                                   # group staging row (36 int64 groups + pad: conflict-free)
+KB1, KB2 = 9, 9
+NQ1, NQ3 = 129, 129                          # q1, q3 dwords (rows >= N: q3 < 2^4098)
+MU_SHIFT = 4072 + 4128                       # mu = floor(2^(A + C) / N)
+S1_BASE = 512                                # product-1 output byte columns from 512
+BIAS_COL, BIAS_DIGIT = 515, -2               # -2^4121 in product 1's corrections
+M_A = (0, 1, 2, 3, 12, 13, 14, 15)           # rows whose copies sit in slots 0..7 (ds_read_b128 lane groups)
+M_B = (4, 5, 6, 7, 8, 9, 10, 11)             # slots 8..15
+assert IMG_BYTES % 16 == 0 and WAVE_AREA % 16 == 0 and LDS_BYTES <= 160 * 1024
+
+
+def layout_header():
+    """gen/addb_layout.h: the constants the host image builder (addb_image.hpp) and launcher need"""
+    vals = dict(kAddbMuShift=MU_SHIFT, kAddbNd1=515, kAddbNd2=513, kAddbKctxBytes=KCTX_BYTES, kAddbA1Off=A1_OFF,
+                kAddbA2Off=A2_OFF, kAddbS1Base=S1_BASE, kAddbKO1=KO1, kAddbKO2=KO2, kAddbCopy=COPY,
+                kAddbTiles1=TILES1, kAddbTiles2=TILES2, kAddbNq1=NQ1, kAddbNq3=NQ3, kAddbBiasCol=BIAS_COL,
+                kAddbBiasDigit=BIAS_DIGIT, kAddbCorr1Off=CORR1_OFF, kAddbCorr2Off=CORR2_OFF, kAddbNOff=N_OFF,
+                kAddbImgBytes=IMG_BYTES, kAddbWaves=WAVES, kAddbPerWg=WAVES * CT_PER_WAVE, kAddbLdsBytes=LDS_BYTES)
+    lines = ["// generated by fedtree_amd/build.py from gen_addb.py -- layout of fthe_addb_q152", "#pragma once"]
+    lines += [f"constexpr int {k} = {v};" for k, v in vals.items()]
+    return "\n".join(lines) + "\n"
+
+
+def copy_slot(m):
+    return M_A.index(m) if m in M_A else 8 + M_B.index(m)
+
+
+def band(nd, s0, k0):
+    """the A tile of output bytes [s0, s0+16) x input bytes [k0, k0+64) has a nonzero digit c[s - k]"""
+    lo, hi = s0 - k0 - 63, s0 + 15 - k0
+    return not (hi < 0 or lo >= nd)
+
+
+ND1, ND2 = 515, 513                          # balanced digits of mu and N
+ACT1 = [[kb for kb in range(KB1) if band(ND1, 512 + 16 * t, 64 * kb)] for t in range(TILES1)]
+ACT2 = [[kb for kb in range(KB2) if band(ND2, 16 * t, 64 * kb)] for t in range(TILES2)]
+CHUNKS = [list(range(0, 8)), list(range(8, 16)), list(range(16, 24)), list(range(24, 33))]
+
+
+def gen_addb(name: str) -> str:
+    o = []
+    e = o.append
+    DPP = "row_mask:0xf bank_mask:0xf"
+    # ---- VGPRs ---------------------------------------------------------------------------------------
+    V_TID, V_ROW, V_LDSI, V_AI, V_SH = 0, 1, 2, (3, 4), 5
+    V_TMP = 6                                     # pair 6:7
+    XB = 8                                        # X limbs v8..v45 (product phase), later other limbs
+    TB = 46                                       # ring of NT 64-bit columns v46..v125
+    NT = Q + 2
+    WD = 46                                       # W dwords (after the product) v46..v77
+    ZLB = 80                                      # z mod 2^4104 dwords v80..v111, v112 = bits 4096..4103
+    ZL128 = 112
+    BQ = 8                                        # B operands, 9 x 4 = v8..v43
+    DQ = 44                                       # fold output dwords v44..v79 (36)
+    ACC = (114, 118)                              # two accumulator sets
+    AOP = (122, 126, 130, 134)                    # four A-operand buffers (reads two MFMAs ahead)
+    PG, FV, CR, CR2 = 162, 164, 166, 6            # int64 pairs (CR2 = V_TMP, free in the MFMA phases)
+    V_A1, V_A2, V_C, V_B, V_G, V_GR, V_Q3W, V_ZR = 138, 139, 140, 141, 142, 143, 144, 145
+    GB = 146                                      # group read buffer, 8 int64 = v146..v161
+    NV = 8                                        # N dwords for the canonicalisation (v8..v39, BQ dead)
+    RR = 44                                       # r dwords (reuses DQ after the subtraction) v44..v75, v76
+    R128 = 76
+    TT, TT128 = 114, 146                          # r - N dwords v114..v145 (+ dword 128)
+    NVGPR = 168
+
+    def X(k):
+        return f"v{XB + k}"
+
+    def T(k):
+        k %= NT
+        return f"v[{TB + 2 * k}:{TB + 2 * k + 1}]"
+
+    def Tlo(k):
+        return f"v{TB + 2 * (k % NT)}"
+
+    def Thi(k):
+        return f"v{TB + 2 * (k % NT) + 1}"
+
+    def pair(n):
+        return f"v[{n}:{n + 1}]"
+
+    def quad4(n):
+        return f"v[{n}:{n + 3}]"
+
+    tmp = pair(V_TMP)
+    # ---- SGPRs ---------------------------------------------------------------------------------------
+    # s[0:1] kernarg, s2 wg id, s[4:5] x rows, s[6:7] y rows, s[8:9] out rows, s[10:11] kctx, s12 count,
+    # s13 first ciphertext of this wave, s[14:15] scratch, s[16:17] saved exec, s18 loop counter,
+    # lane masks: s[20:21] quad lane 3, s[22:23] lane 0, s[24:25] lane 1, s[26:27] lane 2,
+    # s[28:29] live lanes, s30 = 256, s31 = 65536, s32 = 2^24, s33 = 0x80808080
+    LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
+    LIVE = "s[28:29]"
+    NSGPR = 40
+
+    e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
+    e('.amdhsa_code_object_version 5')
+    e('.text')
+    e(f'.globl {name}')
+    e('.p2align 8')
+    e(f'.type {name},@function')
+    e(f'{name}:')
+    e('  s_load_dwordx2 s[4:5], s[0:1], 0x0')
+    e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
+    e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
+    e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
+    e('  s_load_dword s12, s[0:1], 0x20')
+    for j, pat in ((3, 0x88888888), (0, 0x11111111), (1, 0x22222222), (2, 0x44444444)):
+        lo, hi = LANE_MASK[j][2:-1].split(':')
+        e(f'  s_mov_b32 s{lo}, {hex(pat)}')
+        e(f'  s_mov_b32 s{hi}, {hex(pat)}')
+    e('  s_movk_i32 s30, 0x100')
+    e('  s_mov_b32 s31, 0x10000')
+    e('  s_mov_b32 s32, 0x1000000')
+    e('  s_mov_b32 s33, 0x80808080')
+    e('  s_waitcnt lgkmcnt(0)')
+    # ---- constant image -> LDS: every thread copies 16 B per pass (768 threads x 16 B = 12,288 B) --------
+    e(f'  v_lshlrev_b32_e32 v{V_ROW}, 4, v{V_TID}')
+    passes = (IMG_BYTES + 64 * WAVES * 16 - 1) // (64 * WAVES * 16)
+    for p in range(passes):
+        off = p * 64 * WAVES * 16
+        part = off + 64 * WAVES * 16 > IMG_BYTES
+        if part:
+            e(f'  v_cmp_gt_u32_e32 vcc, {hex(IMG_BYTES - off)}, v{V_ROW}')
+            e('  s_and_saveexec_b64 s[16:17], vcc')
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(off)}, v{V_ROW}')
+        e(f'  global_load_dwordx4 v[8:11], v{V_LDSI}, s[10:11]')
+        e('  s_waitcnt vmcnt(0)')
+        e(f'  ds_write_b128 v{V_LDSI}, v[8:11]')
+        if part:
+            e('  s_mov_b64 exec, s[16:17]')
+    e('  s_waitcnt lgkmcnt(0)')
+    e('  s_barrier')
+    # ---- this wave's ciphertexts: g = wg*192 + wave*16 + (lane >> 2); leave if none is live ------------
+    e(f'  v_lshrrev_b32_e32 v{V_SH}, 6, v{V_TID}')                     # wave
+    e('  v_readfirstlane_b32 s14, v5')
+    e(f'  s_mul_i32 s13, s2, {WAVES * CT_PER_WAVE}')
+    e(f'  s_lshl_b32 s15, s14, 4')
+    e('  s_add_u32 s13, s13, s15')                                      # first ciphertext of the wave
+    e('  s_cmp_ge_u32 s13, s12')
+    e('  s_cbranch_scc1 .Lend')
+    # ROW = g*512 + j*128 = wg*98304 + tid*128
+    e(f'  s_mul_i32 s15, s2, {WAVES * CT_PER_WAVE * 512}')
+    e(f'  v_lshlrev_b32_e32 v{V_ROW}, 7, v{V_TID}')
+    e(f'  v_add_u32_e32 v{V_ROW}, s15, v{V_ROW}')
+    # live lanes: g < count
+    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
+    e(f'  v_cmp_gt_u32_e32 vcc, s12, v{V_TMP}')
+    e(f'  s_mov_b64 {LIVE}, vcc')
+    # wave area base + 4c; lane j's A-column write base (rows 38j ..), the ciphertext's A column
+    e(f'  s_mul_i32 s15, s14, {WAVE_AREA}')
+    e(f'  s_add_u32 s15, s15, {LDS_WAVES}')
+    e(f'  v_and_b32_e32 v{V_TMP}, 63, v{V_TID}')
+    e(f'  v_lshrrev_b32_e32 v{V_TMP + 1}, 2, v{V_TMP}')                # c
+    e(f'  v_lshl_add_u32 v{V_LDSI}, v{V_TMP + 1}, 2, s15')             # area + 4c
+    e(f'  v_and_b32_e32 v{V_TMP + 1}, 3, v{V_TMP}')                    # j
+    e(f'  v_mul_u32_u24_e32 v{V_ZR}, {Q * RB}, v{V_TMP + 1}')
+    e(f'  v_add_u32_e32 v{V_ZR}, v{V_ZR}, v{V_LDSI}')                  # area + 4c + 38 j RB
+    # MFMA-layout addresses: lane l, m = l & 15, h = l >> 4
+    e(f'  v_and_b32_e32 v{V_TMP + 1}, 15, v{V_TMP}')                   # m (= B column v)
+    e(f'  v_lshrrev_b32_e32 v{V_SH}, 4, v{V_TMP}')                     # h
+    e(f'  v_lshlrev_b32_e32 v{V_SH}, 4, v{V_SH}')                      # 16 h
+    # copy slot of row m: M_A -> 0..7, M_B -> 8..15: slot = m < 4 ? m : m < 12 ? m + 4 : m - 8
+    e(f'  v_add_u32_e32 v{V_A1}, 4, v{V_TMP + 1}')
+    e(f'  v_subrev_u32_e32 v{V_A2}, 8, v{V_TMP + 1}')
+    e(f'  v_cmp_gt_u32_e32 vcc, 12, v{V_TMP + 1}')
+    e(f'  v_cndmask_b32_e32 v{V_A1}, v{V_A2}, v{V_A1}, vcc')
+    e(f'  v_cmp_gt_u32_e32 vcc, 4, v{V_TMP + 1}')
+    e(f'  v_cndmask_b32_e32 v{V_A1}, v{V_A1}, v{V_TMP + 1}, vcc')         # slot
+    e(f'  v_mul_u32_u24_e32 v{V_A1}, {COPY}, v{V_A1}')
+    e(f'  v_add_u32_e32 v{V_A1}, v{V_A1}, v{V_SH}')                    # slot*COPY + 16 h
+    e(f'  v_add_u32_e32 v{V_A2}, {A2_OFF}, v{V_A1}')
+    if A1_OFF:
+        e(f'  v_add_u32_e32 v{V_A1}, {A1_OFF}, v{V_A1}')
+    e(f'  v_add_u32_e32 v{V_C}, {CORR1_OFF}, v{V_SH}')                 # corrections: + 64 t (+ CORR2-CORR1)
+    e(f'  v_mul_u32_u24_e32 v{V_B}, {QROW}, v{V_TMP + 1}')
+    e(f'  v_add3_u32 v{V_B}, v{V_B}, v{V_SH}, s15')                    # staging row m + 16 h
+    e(f'  v_mul_u32_u24_e32 v{V_G}, {GROW}, v{V_TMP + 1}')
+    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 1, v{V_SH}')                     # 8 h
+    e(f'  v_add3_u32 v{V_G}, v{V_G}, v{V_TMP}, s15')                   # group row m + 8 h
+    e(f'  v_and_b32_e32 v{V_TMP}, 63, v{V_TID}')
+    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 2, v{V_TMP}')                    # c
+    e(f'  v_mul_u32_u24_e32 v{V_GR}, {GROW}, v{V_TMP}')
+    e(f'  v_add_u32_e32 v{V_GR}, s15, v{V_GR}')                        # group row c (fold reads)
+    e(f'  v_mul_u32_u24_e32 v{V_Q3W}, {QROW}, v{V_TMP}')
+    e(f'  v_add_u32_e32 v{V_Q3W}, s15, v{V_Q3W}')                      # staging row c (+ 128 j below)
+    e(f'  v_bfe_u32 v{V_SH}, v{V_ROW}, 7, 2')                          # j
+    e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_SH}')
+    e(f'  v_add_u32_e32 v{V_Q3W}, v{V_Q3W}, v{V_TMP}')
+    e(f'  v_subrev_u32_e32 v{V_Q3W}, 4, v{V_Q3W}')                    # + 128 j - 4 (dword 32 j - 1)
+    e(f'  v_lshlrev_b32_e32 v{V_SH}, 1, v{V_SH}')                      # 2 j (the row-I/O shift)
+
+    # ---- row I/O helpers (gen_montprog.gen_quad's LOADW / STOREW, for this register plan) ---------------
+    W0 = TB                                       # 33 loaded row words (ring area, free outside the product)
+
+    def load_row_limbs(sbase, dst):
+        e(f'  s_mov_b64 exec, {LIVE}')
+        for i in range(8):
+            e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v{V_ROW}, {sbase} offset:{16 * i}')
+        e(f'  v_add_u32_e32 v{V_TMP}, 0x80, v{V_ROW}')
+        e(f'  v_add_u32_e32 v{V_TMP + 1}, 0x7c, v{V_ROW}')
+        e(f'  v_cndmask_b32_e64 v{V_TMP}, v{V_TMP}, v{V_TMP + 1}, s[20:21]')
+        e(f'  global_load_dword v{W0 + 32}, v{V_TMP}, {sbase}')
+        e('  s_waitcnt vmcnt(0)')
+        e('  s_not_b64 exec, exec')                                      # dead lanes: zero operand
+        for i in range(33):
+            e(f'  v_mov_b32_e32 v{W0 + i}, 0')
+        e('  s_mov_b64 exec, -1')
+        e(f'  v_cndmask_b32_e64 v{W0 + 32}, v{W0 + 32}, 0, s[20:21]')
+        for i in range(32):
+            e(f'  v_alignbit_b32 v{W0 + i}, v{W0 + i + 1}, v{W0 + i}, v{V_SH}')
+        e(f'  v_lshrrev_b32_e32 v{W0 + 32}, v{V_SH}, v{W0 + 32}')
+        for jj in range(Q):
+            a, sh = (B * jj) >> 5, (B * jj) & 31
+            if sh + B <= 32:
+                e(f'  v_bfe_u32 {dst(jj)}, v{W0 + a}, {sh}, {B}')
+            else:
+                e(f'  v_alignbit_b32 {dst(jj)}, v{W0 + a + 1}, v{W0 + a}, {sh}')
+                e(f'  v_and_b32_e32 {dst(jj)}, {hex(MASK)}, {dst(jj)}')
+
+    def limbs_to_words(src, U, t1, bo):
+        """this lane's 38 limbs src(k) (bits [1026 j, 1026 j + 1026) of the number) -> dwords U(i) =
+        bits [32 (32 j + i), +32) of the number (lane 3: bits >= 4096 dropped); STOREW's conversion"""
+        for i in range(32):
+            lo, hi = 32 * i, 32 * i + 31
+            j0, j1 = lo // B, min(hi // B, Q - 1)
+            e(f'  v_lshrrev_b32_e32 {U(i)}, {lo - B * j0}, {src(j0)}')
+            for jj in range(j0 + 1, j1 + 1):
+                e(f'  v_lshl_or_b32 {U(i)}, {src(jj)}, {B * jj - lo}, {U(i)}')
+        e(f'  v_sub_u32_e32 {bo}, 31, v{V_SH}')                      # 31 - 2j
+        for i in range(31, 0, -1):
+            e(f'  v_lshrrev_b32_e32 {t1}, {bo}, {U(i - 1)}')
+            e(f'  v_lshrrev_b32_e32 {t1}, 1, {t1}')
+            e(f'  v_lshl_or_b32 {U(i)}, {U(i)}, v{V_SH}, {t1}')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp {t1}, {src(Q - 1)} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_sub_u32_e32 {bo}, {B}, v{V_SH}')                     # lane 0: shift 27 -> no bits
+        e(f'  v_lshrrev_b32_e32 {t1}, {bo}, {t1}')
+        e(f'  v_lshl_or_b32 {U(0)}, {U(0)}, v{V_SH}, {t1}')
+
+    def ripple_quad(lab, vals, nv, carry, signed=False, width=B, t=(V_TMP + 0, None)):
+        """vals(k) (k < nv) limbs of `width` bits, a pending 64-bit carry-out in `carry` (per lane): the
+        carries move to the next lane's limb 0 (lane 0 gets none) and ripple until none is left."""
+        shr = 'v_ashrrev_i64' if signed else 'v_lshrrev_b64'
+        c0, c1 = carry
+        a0, a1 = V_AI
+        e(f'{lab}_loop:')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{a0}, v{c0} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_mov_b32_dpp v{a1}, v{c1} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 v{c0}, v{a0}, 0, s[22:23]')
+        e(f'  v_cndmask_b32_e64 v{c1}, v{a1}, 0, s[22:23]')
+        e(f'  v_or_b32_e32 v{a0}, v{c0}, v{c1}')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{a0}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        for k in range(nv):
+            e(f'  v_mad_u64_u32 v[{c0}:{c1}], vcc, {vals(k)}, 1, v[{c0}:{c1}]')
+            e(f'  v_and_b32_e32 {vals(k)}, {hex((1 << width) - 1)}, v{c0}')
+            e(f'  {shr} v[{c0}:{c1}], {width}, v[{c0}:{c1}]')
+        e(f'  s_branch {lab}_loop')
+        e(f'{lab}_done:')
+
+    # ---- 1. x -> X limbs; y -> limbs -> the wave's A column (rows 38j + k of column c) ------------------
+    load_row_limbs('s[4:5]', X)
+    load_row_limbs('s[6:7]', lambda k: f"v{TB + 40 + k}")              # y limbs (ring area above W0)
+    for k in range(Q):
+        e(f'  ds_write_b32 v{V_ZR}, v{TB + 40 + k} offset:{k * RB}')
+    e('  s_waitcnt lgkmcnt(0)')
+
+    # ---- 2. z = x y: 152 steps; step i reads a_i (prefetched), adds a_i X into the window, retires the
+    #         lowest column: its carry stays in the lane's next column, its low 27 bits go one lane down (the
+    #         top column of lane j-1), and lane 0's -- the product limb z_i -- into A-column row i ---------
+    for k in range(NT):
+        e(f'  v_mov_b64_e32 {T(k)}, 0')
+    e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
+    e('  s_waitcnt lgkmcnt(0)')
+
+    def step(u, row, prefetch):
+        ai, nai = f"v{V_AI[u % 2]}", f"v{V_AI[(u + 1) % 2]}"
+        for k in range(Q):
+            e(f'  v_mad_u64_u32 {T(u + k)}, vcc, {ai}, {X(k)}, {T(u + k)}')
+            if k == 2:
+                e(f'  v_lshrrev_b64 {tmp}, {B}, {T(u)}')
+            if k == 5:
+                e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
+            if k == 7:
+                e(f'  v_and_b32_e32 {Tlo(u)}, {hex(MASK)}, {Tlo(u)}')
+            if k == 10:
+                e('  s_mov_b64 exec, s[22:23]')
+                e(f'  ds_write_b32 v{V_LDSI}, {Tlo(u)} offset:{row * RB}')
+                e('  s_mov_b64 exec, -1')
+            if k == 12 and prefetch is not None:
+                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{prefetch * RB}')
+            if k == 14:
+                e(f'  v_cndmask_b32_e64 {Tlo(u)}, {Tlo(u)}, 0, s[22:23]')
+        e(f'  v_mov_b32_dpp {Tlo(u + Q)}, {Tlo(u)} quad_perm:[1,2,3,0] {DPP}')
+        e(f'  v_mov_b32_e32 {Thi(u + Q)}, 0')
+        e('  s_waitcnt lgkmcnt(0)')
+
+    NTRIP, TL = S // NT, S % NT
+    assert NT % 2 == 0
+    e(f'  s_mov_b32 s18, {NTRIP}')
+    e('.Ltrip:')
+    for u in range(NT):
+        step(u, u, u + 1)
+    e(f'  v_add_u32_e32 v{V_LDSI}, {hex(NT * RB)}, v{V_LDSI}')
+    e('  s_sub_u32 s18, s18, 1')
+    e('  s_cmp_lg_u32 s18, 0')
+    e('  s_cbranch_scc1 .Ltrip')
+    for u in range(TL):
+        step(u, u, u + 1 if u + 1 < TL else None)
+    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB)}, v{V_LDSI}')
+
+    # ---- 3. window -> W limbs (X), W -> dwords WD; z mod 2^4104 limbs (LDS) -> dwords ZL ---------------
+    e(f'  v_mov_b64_e32 {tmp}, 0')
+    for k in range(Q):
+        e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TL + k)}')
+        e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+        e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+    ripple_quad('.Lrw', X, Q, (V_TMP, V_TMP + 1))
+    limbs_to_words(X, lambda i: f"v{WD + i}", f"v{ZL128}", f"v{V_AI[0]}")
+    for k in range(Q):
+        e(f'  ds_read_b32 {X(k)}, v{V_ZR} offset:{k * RB}')
+    e('  s_waitcnt lgkmcnt(0)')
+    limbs_to_words(X, lambda i: f"v{ZLB + i}", f"v{V_AI[1]}", f"v{V_AI[0]}")
+    e(f'  v_lshrrev_b32_e32 v{ZL128}, 19, {X(Q - 1)}')                # lane 3: bits 4096..4103 (limb 151 >> 19)
+
+    # ---- 4. q1 staging: dword 0 = bits 4072..4103 (lane 3), dwords 1.. = W, 129..143 = 0 (fed 0) --------
+    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 8, v{ZLB + 31}')
+    e(f'  v_lshl_or_b32 v{V_TMP}, v{ZL128}, 24, v{V_TMP}')
+    e(f'  v_xor_b32_e32 v{V_TMP}, s33, v{V_TMP}')
+    e(f'  v_subrev_u32_e32 v{V_TMP + 1}, {3 * 128 - 4}, v{V_Q3W}')     # lane 3: the row base
+    e('  s_mov_b64 exec, s[20:21]')
+    e(f'  ds_write_b32 v{V_TMP + 1}, v{V_TMP}')
+    e('  s_mov_b64 exec, s[22:23]')
+    e(f'  v_mov_b32_e32 v{V_TMP}, 0')
+    for d in range(NQ1, QROW // 4):
+        e(f'  ds_write_b32 v{V_Q3W}, v{V_TMP} offset:{4 + 4 * d}')      # lane 0: row - 4
+    e('  s_mov_b64 exec, -1')
+    for i in range(32):
+        e(f'  v_xor_b32_e32 v{WD + i}, s33, v{WD + i}')
+        e(f'  ds_write_b32 v{V_Q3W}, v{WD + i} offset:{8 + 4 * i}')
+    e('  s_waitcnt lgkmcnt(0)')
+    for kb in range(KB1):
+        e(f'  ds_read_b128 {quad4(BQ + 4 * kb)}, v{V_B} offset:{64 * kb}')
+    e('  s_waitcnt lgkmcnt(0)')
+
+    # ---- 5/6. the two MFMA products, each folded chunk by chunk into DQ (quad lane j: chunk j) ----------
+    def mfma_product(prod):
+        """The tiles of one product chunk by chunk: every A read is issued two MFMAs ahead into one of four
+        buffers, each tile's corrections (srcC) into its accumulator set right after the fold of the tile
+        that used the set last, and s_waitcnt lgkmcnt(n) waits for exactly the read an MFMA needs (LDS
+        returns in order); tile t-1 is folded after tile t's MFMAs are issued."""
+        A = V_A1 if prod == 1 else V_A2
+        KO = KO1 if prod == 1 else KO2
+        act = ACT1 if prod == 1 else ACT2
+        corr = 0 if prod == 1 else CORR2_OFF - CORR1_OFF
+        e(f'  v_mov_b64_e32 {pair(CR)}, 0')
+        for j, tiles in enumerate(CHUNKS):
+            t0 = tiles[0]
+            ops = [(n, t, kb) for n, t in enumerate(tiles) for kb in act[t]]
+            q = []                                   # outstanding LDS ops, oldest first (tags)
+
+            def issue(tag, ins):
+                e(ins)
+                q.append(tag)
+
+            def wait_for(tag):
+                if tag not in q:                     # completed with a later op already waited for
+                    return
+                i = q.index(tag)
+                left = len(q) - i - 1
+                e(f'  s_waitcnt lgkmcnt({min(left, 15)})')
+                del q[:i + 1]
+
+            def read_a(x):
+                n, t, kb = ops[x]
+                off = KO + 16 * (4 * kb - t)
+                assert 0 <= off and off + 48 + 16 <= COPY
+                issue(('a', x), f'  ds_read_b128 {quad4(AOP[x % 4])}, v{A} offset:{off}')
+
+            def read_corr(n, t):
+                issue(('c', n), f'  ds_read_b128 {quad4(ACC[n % 2])}, v{V_C} offset:{corr + 64 * t}')
+
+            read_corr(0, tiles[0])
+            for x in range(min(2, len(ops))):
+                read_a(x)
+            for x, (n, t, kb) in enumerate(ops):
+                first = x == 0 or ops[x - 1][0] != n
+                if first:
+                    wait_for(('c', n))
+                wait_for(('a', x))
+                e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
+                  f'{quad4(ACC[n % 2])}')
+                if x + 2 < len(ops):
+                    read_a(x + 2)
+                last = x + 1 == len(ops) or ops[x + 1][0] != n
+                if last:
+                    if n >= 1:                       # fold tile n-1 (its set is then free for tile n+1)
+                        e('  s_nop 7')
+                        e('  s_nop 7')
+                        fold_tile(ACC[(n - 1) % 2], 4 * (tiles[n - 1] - t0))
+                        q.append(('w', n - 1))
+                    if n + 1 < len(tiles):
+                        read_corr(n + 1, tiles[n + 1])
+            e('  s_nop 7')
+            e('  s_nop 7')
+            e('  s_nop 7')
+            fold_tile(ACC[(len(tiles) - 1) % 2], 4 * (tiles[-1] - t0))
+            e('  s_waitcnt lgkmcnt(0)')
+            # carry in: lane j's chunk starts from lane j-1's final carry (lane 0: none)
+            if j:
+                e('  s_nop 1')
+                e(f'  v_mov_b32_dpp v{CR2}, v{CR} quad_perm:[0,0,1,2] {DPP}')
+                e(f'  v_mov_b32_dpp v{CR2 + 1}, v{CR + 1} quad_perm:[0,0,1,2] {DPP}')
+                e(f'  v_mov_b64_e32 {pair(CR)}, {pair(CR2)}')
+            e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
+            ng = 4 * len(tiles)
+            for g0 in range(0, ng, 8):
+                for g in range(g0, min(ng, g0 + 8)):
+                    e(f'  ds_read_b64 {pair(GB + 2 * (g - g0))}, v{V_GR} offset:{8 * g}')
+                e('  s_waitcnt lgkmcnt(0)')
+                for g in range(g0, min(ng, g0 + 8)):
+                    e(f'  v_lshl_add_u64 {pair(FV)}, {pair(GB + 2 * (g - g0))}, 0, {pair(CR)}')
+                    e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
+                    e(f'  v_ashrrev_i64 {pair(CR)}, 32, {pair(FV)}')
+            e('  s_mov_b64 exec, -1')
+
+    def fold_tile(acc, gl):
+        """acc's 4 int32 rows (output bytes 4h..4h+3 of the tile) -> int64 group -> LDS (group 4 (t - t0) + h)"""
+        e(f'  v_ashrrev_i32_e32 v{PG + 1}, 31, v{acc}')
+        e(f'  v_mov_b32_e32 v{PG}, v{acc}')
+        e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 1}, s30, {pair(PG)}')
+        e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 2}, s31, {pair(PG)}')
+        e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 3}, s32, {pair(PG)}')
+        e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{8 * gl}')
+
+    mfma_product(1)
+    # clamp: a negative N1 (lane 3's final carry) -> q3 = 0
+    e('  s_nop 1')
+    e(f'  v_mov_b32_dpp v{CR2}, v{CR + 1} quad_perm:[3,3,3,3] {DPP}')
+    e(f'  v_cmp_gt_i32_e32 vcc, 0, v{CR2}')
+    for g in range(36):
+        e(f'  v_cndmask_b32_e64 v{DQ + g}, v{DQ + g}, 0, vcc')
+    # q3 dword i = D_{i+1}: lane j writes its D_{32j+k} (k = 0..31; lane 3 also k = 32, 33) at dword 32j + k - 1
+    for k in range(34):
+        e(f'  v_xor_b32_e32 v{DQ + k}, s33, v{DQ + k}')
+    e(f'  s_mov_b64 exec, {LANE_MASK[0]}')
+    e('  s_not_b64 exec, exec')                                          # lanes 1..3: D_{32j} at dword 32j - 1
+    e(f'  ds_write_b32 v{V_Q3W}, v{DQ}')
+    e('  s_mov_b64 exec, -1')
+    for k in range(1, 32):
+        e(f'  ds_write_b32 v{V_Q3W}, v{DQ + k} offset:{4 * k}')
+    e(f'  s_mov_b64 exec, {LANE_MASK[3]}')
+    e(f'  ds_write_b32 v{V_Q3W}, v{DQ + 32} offset:128')
+    e(f'  ds_write_b32 v{V_Q3W}, v{DQ + 33} offset:132')                   # q3 dword 128 (rows >= N only)
+    e('  s_mov_b64 exec, -1')
+    e('  s_waitcnt lgkmcnt(0)')
+    for kb in range(KB2):
+        e(f'  ds_read_b128 {quad4(BQ + 4 * kb)}, v{V_B} offset:{64 * kb}')
+    e('  s_waitcnt lgkmcnt(0)')
+    mfma_product(2)
+    # lane 3 keeps D2_128's low 8 bits (r2 mod 2^4104)
+
+    # ---- 7. r = (z - r2) mod 2^4104: borrow chains per lane, rippled across the quad --------------------
+    def borrow_ripple(lab, R, R128_, bo, bin_):
+        """lane k (k < 3) hands its borrow bo (0/1) to lane k+1, which subtracts it from its dwords R(0..31)
+        and (lane 3) its dword 128; repeated until no lane receives a borrow (lane 3's own is dropped: the
+        arithmetic is mod 2^4128 on the quad, the caller keeps the bits it needs)"""
+        e(f'{lab}_loop:')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{bin_}, v{bo} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 v{bin_}, v{bin_}, 0, s[22:23]')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{bin_}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        e(f'  v_sub_co_u32_e32 v{R}, vcc, v{R}, v{bin_}')
+        for i in range(1, 32):
+            e(f'  v_subb_co_u32_e64 v{R + i}, vcc, v{R + i}, 0, vcc')
+        e(f'  v_cndmask_b32_e64 v{bo}, 0, 1, vcc')
+        e(f'  v_subb_co_u32_e64 v{R128_}, vcc, v{R128_}, 0, vcc')
+        e(f'  s_branch {lab}_loop')
+        e(f'{lab}_done:')
+
+    e(f'  v_sub_co_u32_e32 v{RR}, vcc, v{ZLB}, v{DQ}')
+    for i in range(1, 32):
+        e(f'  v_subb_co_u32_e32 v{RR + i}, vcc, v{ZLB + i}, v{DQ + i}, vcc')
+    e(f'  v_cndmask_b32_e64 v{V_AI[0]}, 0, 1, vcc')                     # borrow out of dword 31
+    e(f'  v_subb_co_u32_e32 v{R128}, vcc, v{ZL128}, v{DQ + 32}, vcc')    # lane 3: dword 128 (others: unused)
+    borrow_ripple('.Lrb', RR, R128, V_AI[0], V_AI[1])
+    e(f'  v_and_b32_e32 v{R128}, 0xff, v{R128}')                        # r = (z - r2) mod 2^4104, < 3N
+
+    # ---- 8. two conditional subtractions of N, then the canonical row ------------------------------------
+    e(f'  v_bfe_u32 v{V_TMP}, v{V_ROW}, 7, 2')
+    e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_TMP}')                     # 128 j
+    e(f'  v_add_u32_e32 v{V_TMP}, {hex(N_OFF)}, v{V_TMP}')
+    for i in range(8):
+        e(f'  global_load_dwordx4 {quad4(NV + 4 * i)}, v{V_TMP}, s[10:11] offset:{16 * i}')
+    e('  s_waitcnt vmcnt(0)')
+    for rnd in range(2):
+        e(f'  v_sub_co_u32_e32 v{TT}, vcc, v{RR}, v{NV}')
+        for i in range(1, 32):
+            e(f'  v_subb_co_u32_e32 v{TT + i}, vcc, v{RR + i}, v{NV + i}, vcc')
+        e(f'  v_cndmask_b32_e64 v{V_AI[0]}, 0, 1, vcc')
+        e(f'  v_subb_co_u32_e64 v{TT128}, vcc, v{R128}, 0, vcc')
+        borrow_ripple(f'.Lcn{rnd}', TT, TT128, V_AI[0], V_AI[1])
+        # r < N  <=>  r - N < 0  <=>  lane 3's dword 128 of r - N is negative
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{V_AI[0]}, v{TT128} quad_perm:[3,3,3,3] {DPP}')
+        e(f'  v_cmp_le_i32_e32 vcc, 0, v{V_AI[0]}')                      # r >= N: take r - N
+        for i in range(32):
+            e(f'  v_cndmask_b32_e32 v{RR + i}, v{RR + i}, v{TT + i}, vcc')
+        e(f'  v_cndmask_b32_e32 v{R128}, v{R128}, v{TT128}, vcc')
+    e(f'  s_mov_b64 exec, {LIVE}')
+    for i in range(8):
+        e(f'  global_store_dwordx4 v{V_ROW}, {quad4(RR + 4 * i)}, s[8:9] offset:{16 * i}')
+    e('  s_waitcnt vmcnt(0)')
+    e('.Lend:')
+    e('  s_endpgm')
+    e(f'.Lfunc_end_{name}:')
+    e(f'  .size {name}, .Lfunc_end_{name}-{name}')
+    e('')
+    return "\n".join(o) + "\n" + descriptor(name, LDS_BYTES, NVGPR, NSGPR)
+
+
+def descriptor(name, lds_bytes, nvgpr, nsgpr):
+    o = []
+    e = o.append
+    e('.rodata')
+    e('.p2align 6')
+    e(f'.amdhsa_kernel {name}')
+    e(f'  .amdhsa_group_segment_fixed_size {lds_bytes}')
+    e('  .amdhsa_private_segment_fixed_size 0')
+    e('  .amdhsa_kernarg_size 40')
+    e('  .amdhsa_user_sgpr_count 2')
+    e('  .amdhsa_user_sgpr_kernarg_segment_ptr 1')
+    e('  .amdhsa_system_sgpr_workgroup_id_x 1')
+    e('  .amdhsa_system_vgpr_workitem_id 0')
+    e(f'  .amdhsa_next_free_vgpr {nvgpr}')
+    e(f'  .amdhsa_next_free_sgpr {nsgpr}')
+    e(f'  .amdhsa_accum_offset {((nvgpr + 3) // 4) * 4}')
+    e('  .amdhsa_reserve_vcc 1')
+    e('  .amdhsa_ieee_mode 0')
+    e('  .amdhsa_dx10_clamp 0')
+    e('.end_amdhsa_kernel')
+    e('')
+    e('.amdgpu_metadata')
+    e('---')
+    e('amdhsa.kernels:')
+    e('  - .args:')
+    for off_, sz, kind in ((0, 8, 'global_buffer'), (8, 8, 'global_buffer'), (16, 8, 'global_buffer'),
+                           (24, 8, 'global_buffer'), (32, 4, 'by_value')):
+        e(f'      - .offset: {off_}')
+        e(f'        .size: {sz}')
+        e(f'        .value_kind: {kind}')
+        if kind == 'global_buffer':
+            e('        .address_space: global')
+    e(f'    .group_segment_fixed_size: {lds_bytes}')
+    e('    .kernarg_segment_align: 8')
+    e('    .kernarg_segment_size: 40')
+    e(f'    .max_flat_workgroup_size: {64 * WAVES}')
+    e(f'    .name: {name}')
+    e('    .private_segment_fixed_size: 0')
+    e(f'    .sgpr_count: {nsgpr + 2}')
+    e(f'    .symbol: {name}.kd')
+    e(f'    .vgpr_count: {nvgpr}')
+    e('    .wavefront_size: 64')
+    e('amdhsa.target: amdgcn-amd-amdhsa--gfx950')
+    e('amdhsa.version:')
+    e('  - 1')
+    e('  - 2')
+    e('...')
+    e('.end_amdgpu_metadata')
+    return "\n".join(o) + "\n"

@@ -428,6 +428,13 @@ int fthe_decode_fixed_dev(fthe_ctx *ctx, const uint64_t *m, size_t count, float 
 int fthe_debug_direct_y(fthe_key *key, fthe_ctx *ctx, uint64_t rng_seed, uint64_t index0, size_t count,
                         uint32_t *yp, uint32_t *yq);
 
+/* ---- test hook: the per-key context of the matrix-core Barrett add ---------
+ * The bytes fthe_addb_q152 reads (mu and N copies, column corrections, N), built
+ * on the host from n (n_words little-endian words) exactly as at key set-up;
+ * out == NULL: only *len.  FTHE_ERR_UNSUPPORTED unless n^2 has 4095-4096 bits.
+ * Host only (tests compare it with tools/addb_model.py addb_image). */
+int fthe_debug_addb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len);
+
 /* ---- profiling hooks: time of the last call's kernels on the stream ------ */
 double fthe_last_kernel_ms(fthe_ctx *ctx);
 /* Montgomery products executed by the last call (for roofline accounting). */

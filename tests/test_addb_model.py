@@ -1,0 +1,81 @@
+"""The matrix-core Barrett add (fthe_addb_q152, fedtree_amd/csrc/gen_addb.py) without a GPU:
+
+* tools/addb_model.py, the bit-exact model of its arithmetic (Barrett cut points, truncated product with
+  its bias, int32 column sums, signed group folds), against Python's x y mod N -- the reference's add
+  (paillier.cpp:92-105, paillier_gmp.cpp:16-21) -- on random and extreme operands, n of 2048 bits at both
+  ends of the range;
+* the host builder of the per-key context in the library (addb_image.hpp, through the
+  fthe_debug_addb_image hook) byte for byte against the model's;
+* the generated gfx950 assembly itself, run on tools/wave_emu.py (64-lane wavefronts: DPP, EXEC/VCC,
+  LDS, v_mfma_i32_16x16x64_i8 with the lane map measured on the GPU), one workgroup of adds vs x y mod N.
+"""
+import ctypes
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "fedtree_amd", "csrc"))
+
+import addb_model as am  # noqa: E402
+
+KEYS = [None, (1 << 2047) + 1, (1 << 2048) - 1]
+
+
+def _n(i):
+    return KEYS[i] if KEYS[i] else am.rand_n(random.Random(4))
+
+
+@pytest.mark.parametrize("ki", [0, 1, 2])
+def test_model_reduces_exactly(ki):
+    n = _n(ki)
+    k = am.AddbKey(n * n)
+    N = k.N
+    rng = random.Random(ki)
+    top = (1 << 4096) - 1                             # rows >= N: not ciphertexts, reduced all the same
+    cases = [(N - 1, N - 1), (0, N - 1), (1, 1), (N - 1, 1), (1 << 2048, (1 << 2048) - 1), (top, top), (N, N),
+             (top, 1)]
+    cases += [(rng.randrange(N), rng.randrange(N)) for _ in range(3)]
+    for x, y in cases:
+        r, q3 = k.reduce(x * y)                       # asserts every bound and q3 in [q - 2, q]
+        assert 0 <= r < 3 * N
+        assert k.add(x, y) == x * y % N
+
+
+def test_model_rejects_short_moduli():
+    with pytest.raises(AssertionError):
+        am.AddbKey(((1 << 2046) + 1) ** 2)            # n of 2047 bits: N below 2^4094
+
+
+@pytest.mark.parametrize("ki", [0, 1, 2])
+def test_host_context_matches_model(ki):
+    lib = ctypes.CDLL(os.path.join(ROOT, "fedtree_amd", "libfthe.so"))
+    n = _n(ki)
+    nw = np.frombuffer(n.to_bytes(256, "little"), dtype=np.uint32).copy()
+    ln = ctypes.c_size_t()
+    assert lib.fthe_debug_addb_image(ctypes.c_void_p(nw.ctypes.data), 64, None, ctypes.c_size_t(0),
+                                     ctypes.byref(ln)) == 0
+    buf = np.zeros(ln.value, np.uint8)
+    assert lib.fthe_debug_addb_image(ctypes.c_void_p(nw.ctypes.data), 64, ctypes.c_void_p(buf.ctypes.data),
+                                     ctypes.c_size_t(buf.size), ctypes.byref(ln)) == 0
+    assert bytes(buf) == am.addb_image(n * n)
+
+
+def test_host_context_refuses_short_n():
+    lib = ctypes.CDLL(os.path.join(ROOT, "fedtree_amd", "libfthe.so"))
+    n = (1 << 2040) + 7
+    nw = np.frombuffer(n.to_bytes(256, "little"), dtype=np.uint32).copy()
+    ln = ctypes.c_size_t()
+    assert lib.fthe_debug_addb_image(ctypes.c_void_p(nw.ctypes.data), 64, None, ctypes.c_size_t(0),
+                                     ctypes.byref(ln)) == -4          # FTHE_ERR_UNSUPPORTED
+
+
+def test_generated_kernel_on_wave_emulator():
+    """the gfx950 assembly of fthe_addb_q152, one workgroup: a full wave of 16 adds (N - 1 squared,
+    0 (N - 1), 1 1 and random rows) and a partly live wave (13 of 16), every row vs x y mod N"""
+    import wave_emu
+    wave_emu.selftest()

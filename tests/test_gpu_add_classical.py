@@ -13,8 +13,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def pl():
+    """the classical product on the four-lane kernel: FTHE_ADD_NO_ADDB=1 at key set-up keeps the pairwise add
+    off the matrix-core Barrett kernel (tests/test_gpu_addb.py compares the two)"""
+    import os
     from fedtree_amd.paillier import Device, Paillier
-    return Paillier(Device(0)).keygen(2048, seed=20261016)
+    os.environ["FTHE_ADD_NO_ADDB"] = "1"
+    try:
+        return Paillier(Device(0)).keygen(2048, seed=20261016)
+    finally:
+        del os.environ["FTHE_ADD_NO_ADDB"]
 
 
 def _rows(vals, cw):

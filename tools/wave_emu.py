@@ -1,0 +1,479 @@
+#!/usr/bin/env python3
+"""Emulator of whole wavefronts (64 lanes) for the instruction subset of the matrix-core Barrett add kernel
+(fedtree_amd/csrc/gen_addb.py): per-lane VGPRs, SGPRs, EXEC / VCC / SCC, DPP quad_perm, LDS, global
+memory, v_mfma_i32_16x16x64_i8 (lane map measured on the GPU: profiles/r03c_mfma16_probe.txt) -- so that
+register plans, lane layouts, LDS offsets and control flow are checked on the CPU before the kernel
+runs on a GPU.  A workgroup is emulated wave by wave: every wave up to its s_barrier, then each wave to
+its end (the kernel's waves share only what they wrote before the barrier).
+
+  python tools/wave_emu.py         (self-test: 16 random adds mod n^2 and edge cases vs Python integers)
+"""
+import os
+import random
+import re
+import sys
+
+M32 = (1 << 32) - 1
+M64 = (1 << 64) - 1
+ALL = (1 << 64) - 1
+
+
+def s32(x):
+    x &= M32
+    return x - (1 << 32) if x >> 31 else x
+
+
+def s64(x):
+    x &= M64
+    return x - (1 << 64) if x >> 63 else x
+
+
+class Mem:
+    """flat global memory: buffers at fixed bases"""
+
+    def __init__(self):
+        self.bufs = []            # (base, bytearray)
+
+    def alloc(self, data, base):
+        self.bufs.append((base, bytearray(data)))
+        return base
+
+    def find(self, addr, n):
+        for b, ba in self.bufs:
+            if b <= addr and addr + n <= b + len(ba):
+                return ba, addr - b
+        raise IndexError(f"global access out of bounds: {addr:#x} +{n}")
+
+    def read(self, addr, n):
+        ba, o = self.find(addr, n)
+        return int.from_bytes(ba[o:o + n], 'little')
+
+    def write(self, addr, n, v):
+        ba, o = self.find(addr, n)
+        ba[o:o + n] = (v & ((1 << (8 * n)) - 1)).to_bytes(n, 'little')
+
+
+class Wave:
+    def __init__(self, prog, labels, lds, mem, sgpr_init, tid0, nvgpr):
+        self.prog, self.labels, self.lds, self.mem = prog, labels, lds, mem
+        self.v = [[0] * 64 for _ in range(nvgpr)]      # v[reg][lane]
+        for lane in range(64):
+            self.v[0][lane] = tid0 + lane
+        self.s = [0] * 128
+        for k, val in sgpr_init.items():
+            self.s[k] = val & M32
+        self.exec = ALL
+        self.vcc = 0
+        self.scc = 0
+        self.pc = 0
+        self.done = False
+        self.at_barrier = False
+        self.count = 0
+
+    # ---- operand helpers ----------------------------------------------------------------------------
+    @staticmethod
+    def rr(tok):
+        m = re.fullmatch(r'([vs])\[(\d+):(\d+)\]', tok)
+        if m:
+            return m.group(1), int(m.group(2)), int(m.group(3)) - int(m.group(2)) + 1
+        m = re.fullmatch(r'([vs])(\d+)', tok)
+        if m:
+            return m.group(1), int(m.group(2)), 1
+        return None
+
+    def sget(self, tok, width=1):
+        if tok == 'vcc':
+            return self.vcc
+        if tok == 'exec':
+            return self.exec
+        r = self.rr(tok)
+        if r is None:
+            return int(tok, 0) & (M64 if width == 2 else M32)
+        kind, b, n = r
+        assert kind == 's', tok
+        val = 0
+        for i in range(n):
+            val |= self.s[b + i] << (32 * i)
+        return val
+
+    def sset(self, tok, val):
+        if tok == 'vcc':
+            self.vcc = val & M64
+            return
+        if tok == 'exec':
+            self.exec = val & M64
+            return
+        kind, b, n = self.rr(tok)
+        assert kind == 's'
+        for i in range(n):
+            self.s[b + i] = (val >> (32 * i)) & M32
+
+    def vget(self, lane, tok, width=1):
+        """operand of a lane: a VGPR / VGPR range (all its registers), an SGPR / SGPR range, vcc or a literal
+        (masked to 32 bits, or 64 when width == 2)"""
+        r = self.rr(tok)
+        if r is None:
+            if tok == 'vcc':
+                return self.vcc
+            return int(tok, 0) & (M64 if width == 2 else M32)
+        kind, b, n = r
+        val = 0
+        for i in range(n):
+            val |= (self.s[b + i] if kind == 's' else self.v[b + i][lane]) << (32 * i)
+        return val
+
+    def vset(self, lane, tok, val):
+        kind, b, n = self.rr(tok)
+        assert kind == 'v', tok
+        for i in range(n):
+            self.v[b + i][lane] = (val >> (32 * i)) & M32
+
+    def lanes(self):
+        ex = self.exec
+        return [l for l in range(64) if ex >> l & 1]
+
+    # ---- execution ----------------------------------------------------------------------------------
+    def run(self, max_steps=5_000_000):
+        while not self.done and not self.at_barrier:
+            assert self.count < max_steps, "runaway"
+            op, args = self.prog[self.pc]
+            self.pc += 1
+            self.count += 1
+            self.step(op, args)
+
+    def step(self, op, a):
+        if op == 's_endpgm':
+            self.done = True
+            return
+        if op == 's_barrier':
+            self.at_barrier = True
+            return
+        if op in ('s_nop', 's_waitcnt'):
+            return
+        if op == 's_branch':
+            self.pc = self.labels[a[0]]
+            return
+        if op == 's_cbranch_scc1':
+            if self.scc:
+                self.pc = self.labels[a[0]]
+            return
+        if op == 's_cbranch_vccz':
+            if (self.vcc & self.exec) == 0:
+                self.pc = self.labels[a[0]]
+            return
+        if op.startswith('s_'):
+            return self.salu(op, a)
+        if op.startswith('ds_'):
+            return self.ds(op, a)
+        if op.startswith('global_'):
+            return self.glob(op, a)
+        if op == 'v_mfma_i32_16x16x64_i8':
+            return self.mfma(a)
+        if op == 'v_readfirstlane_b32':
+            ln = self.lanes()
+            self.sset(a[0], self.vget(ln[0] if ln else 0, a[1]))
+            return
+        if op == 'v_mov_b32_dpp':
+            perm = [int(x) for x in re.search(r'quad_perm:\[([0-9,]+)\]', ' '.join(a)).group(1).split(',')]
+            src = self.rr(a[1])[1]
+            dst = self.rr(a[0])[1]
+            old = list(self.v[src])
+            for l in self.lanes():
+                sl = (l & ~3) + perm[l & 3]
+                assert self.exec >> sl & 1, "DPP source lane disabled"
+                self.v[dst][l] = old[sl]
+            return
+        return self.valu(op, a)
+
+    def salu(self, op, a):
+        g = self.sget
+        if op == 's_load_dwordx2':
+            addr = g(a[1], 2) + int(a[2], 0)
+            self.sset(a[0], self.mem.read(addr, 8))
+        elif op == 's_load_dword':
+            addr = g(a[1], 2) + int(a[2], 0)
+            self.sset(a[0], self.mem.read(addr, 4))
+        elif op in ('s_mov_b32', 's_movk_i32'):
+            self.sset(a[0], g(a[1]))
+        elif op == 's_mov_b64':
+            self.sset(a[0], g(a[1], 2) if a[1] != '-1' else ALL)
+        elif op == 's_not_b64':
+            self.sset(a[0], ~g(a[1], 2) & M64)
+            self.scc = int(self.sget(a[0], 2) != 0)
+        elif op == 's_and_saveexec_b64':
+            self.sset(a[0], self.exec)
+            self.exec = self.exec & g(a[1], 2)
+            self.scc = int(self.exec != 0)
+        elif op == 's_mul_i32':
+            self.sset(a[0], g(a[1]) * g(a[2]))
+        elif op == 's_lshl_b32':
+            r = (g(a[1]) << g(a[2])) & M32
+            self.sset(a[0], r)
+            self.scc = int(r != 0)
+        elif op == 's_add_u32':
+            r = g(a[1]) + g(a[2])
+            self.sset(a[0], r)
+            self.scc = r >> 32
+        elif op == 's_sub_u32':
+            r = g(a[1]) - g(a[2])
+            self.sset(a[0], r)
+            self.scc = int(r < 0)
+        elif op == 's_cmp_ge_u32':
+            self.scc = int(g(a[0]) >= g(a[1]))
+        elif op == 's_cmp_lg_u32':
+            self.scc = int(g(a[0]) != g(a[1]))
+        elif op == 's_cmp_eq_u32':
+            self.scc = int(g(a[0]) == g(a[1]))
+        else:
+            raise NotImplementedError(op)
+
+    def ds(self, op, a):
+        width = {'ds_read_b32': 4, 'ds_read_b64': 8, 'ds_read_b128': 16, 'ds_write_b32': 4, 'ds_write_b64': 8,
+                 'ds_write_b128': 16}[op]
+        off = 0
+        for t in a[2:]:
+            if t.startswith('offset:'):
+                off = int(t[7:], 0)
+        write = op.startswith('ds_write')
+        addr_tok = a[0] if write else a[1]
+        data_tok = a[1] if write else a[0]
+        for l in self.lanes():
+            addr = self.vget(l, addr_tok) + off
+            assert 0 <= addr and addr + width <= len(self.lds), f"LDS out of range {addr}"
+            assert addr % width == 0, f"misaligned LDS b{8 * width} at {addr}"
+            if write:
+                self.lds[addr:addr + width] = self.vget(l, data_tok, 2 if width >= 8 else 1).to_bytes(
+                    8 if width >= 8 else 4, 'little')[:width] if width <= 8 else self.vq(l, data_tok)
+            else:
+                self.vset(l, data_tok, int.from_bytes(self.lds[addr:addr + width], 'little'))
+
+    def vq(self, lane, tok):
+        kind, b, n = self.rr(tok)
+        val = 0
+        for i in range(n):
+            val |= self.v[b + i][lane] << (32 * i)
+        return val.to_bytes(4 * n, 'little')
+
+    def glob(self, op, a):
+        width = {'global_load_dword': 4, 'global_load_dwordx4': 16, 'global_store_dwordx4': 16}[op]
+        off = 0
+        for t in a[3:]:
+            if t.startswith('offset:'):
+                off = int(t[7:], 0)
+        store = op.startswith('global_store')
+        vaddr, sbase = a[1] if not store else a[0], a[2]
+        data_tok = a[0] if not store else a[1]
+        base = self.sget(sbase, 2)
+        for l in self.lanes():
+            addr = base + self.vget(l, vaddr) + off
+            if store:
+                self.mem.write(addr, width, int.from_bytes(self.vq(l, data_tok), 'little'))
+            else:
+                self.vset(l, data_tok, self.mem.read(addr, width))
+
+    def mfma(self, a):
+        D, A, Bt, C = (self.rr(t) for t in a)
+        Am = [[0] * 64 for _ in range(16)]
+        Bm = [[0] * 16 for _ in range(64)]
+        for l in range(64):
+            r, h = l & 15, l >> 4
+            abytes = b''.join(self.v[A[1] + i][l].to_bytes(4, 'little') for i in range(4))
+            bbytes = b''.join(self.v[Bt[1] + i][l].to_bytes(4, 'little') for i in range(4))
+            for j in range(16):
+                Am[r][16 * h + j] = abytes[j] - 256 if abytes[j] > 127 else abytes[j]
+                Bm[16 * h + j][r] = bbytes[j] - 256 if bbytes[j] > 127 else bbytes[j]
+        out = [[0] * 16 for _ in range(16)]
+        for i in range(16):
+            for n in range(16):
+                out[i][n] = sum(Am[i][k] * Bm[k][n] for k in range(64))
+        newd = {}
+        for l in range(64):
+            h, col = l >> 4, l & 15
+            for g in range(4):
+                c = s32(self.v[C[1] + g][l])
+                newd[(g, l)] = (out[4 * h + g][col] + c) & M32
+        for (g, l), val in newd.items():
+            self.v[D[1] + g][l] = val
+
+    def valu(self, op, a):
+        lanes = self.lanes()
+        g = self.vget
+        if op in ('v_mad_u64_u32', 'v_mad_i64_i32'):
+            newvcc = self.vcc
+            for l in lanes:
+                x, y = g(l, a[2]), g(l, a[3])
+                c = g(l, a[4], 2)
+                if op == 'v_mad_i64_i32':
+                    r = s32(x) * s32(y) + s64(c)
+                else:
+                    r = x * y + c
+                self.vset(l, a[0], r & M64)
+            return
+        if op in ('v_sub_co_u32_e32', 'v_subb_co_u32_e32', 'v_subb_co_u32_e64'):
+            nv = self.vcc
+            for l in lanes:
+                x, y = g(l, a[2]), g(l, a[3])
+                bi = (self.vcc >> l) & 1 if op != 'v_sub_co_u32_e32' else 0
+                r = x - y - bi
+                self.vset(l, a[0], r & M32)
+                nv = (nv | (1 << l)) if r < 0 else (nv & ~(1 << l))
+            self.vcc = nv
+            return
+        if op == 'v_cmp_gt_u32_e32':
+            nv = 0
+            for l in lanes:
+                nv |= int(g(l, a[1]) > g(l, a[2])) << l
+            self.vcc = nv
+            return
+        if op == 'v_cmp_ne_u32_e32':
+            nv = 0
+            for l in lanes:
+                nv |= int(g(l, a[1]) != g(l, a[2])) << l
+            self.vcc = nv
+            return
+        if op == 'v_cmp_gt_i32_e32':
+            nv = 0
+            for l in lanes:
+                nv |= int(s32(g(l, a[1])) > s32(g(l, a[2]))) << l
+            self.vcc = nv
+            return
+        if op == 'v_cmp_le_i32_e32':
+            nv = 0
+            for l in lanes:
+                nv |= int(s32(g(l, a[1])) <= s32(g(l, a[2]))) << l
+            self.vcc = nv
+            return
+        for l in lanes:
+            if op == 'v_mov_b32_e32':
+                r = g(l, a[1])
+            elif op == 'v_mov_b64_e32':
+                r = g(l, a[1], 2)
+            elif op == 'v_lshlrev_b32_e32':
+                r = g(l, a[2]) << (g(l, a[1]) & 31)
+            elif op == 'v_lshrrev_b32_e32':
+                r = g(l, a[2]) >> (g(l, a[1]) & 31)
+            elif op == 'v_ashrrev_i32_e32':
+                r = s32(g(l, a[2])) >> (g(l, a[1]) & 31)
+            elif op == 'v_and_b32_e32':
+                r = g(l, a[1]) & g(l, a[2])
+            elif op == 'v_or_b32_e32':
+                r = g(l, a[1]) | g(l, a[2])
+            elif op == 'v_xor_b32_e32':
+                r = g(l, a[1]) ^ g(l, a[2])
+            elif op == 'v_add_u32_e32':
+                r = g(l, a[1]) + g(l, a[2])
+            elif op == 'v_sub_u32_e32':
+                r = g(l, a[1]) - g(l, a[2])
+            elif op == 'v_subrev_u32_e32':
+                r = g(l, a[2]) - g(l, a[1])
+            elif op == 'v_mul_u32_u24_e32':
+                r = (g(l, a[1]) & 0xFFFFFF) * (g(l, a[2]) & 0xFFFFFF)
+            elif op == 'v_add3_u32':
+                r = g(l, a[1]) + g(l, a[2]) + g(l, a[3])
+            elif op == 'v_lshl_add_u32':
+                r = (g(l, a[1]) << (g(l, a[2]) & 31)) + g(l, a[3])
+            elif op == 'v_lshl_or_b32':
+                r = ((g(l, a[1]) << (g(l, a[2]) & 31)) | g(l, a[3]))
+            elif op == 'v_bfe_u32':
+                off, w = g(l, a[2]) & 31, g(l, a[3]) & 31
+                r = (g(l, a[1]) >> off) & ((1 << w) - 1)
+            elif op == 'v_alignbit_b32':
+                r = (((g(l, a[1]) << 32) | g(l, a[2])) >> (g(l, a[3]) & 31))
+            elif op == 'v_lshl_add_u64':
+                r = (g(l, a[1], 2) << (g(l, a[2]) & 63)) + g(l, a[3], 2)
+            elif op == 'v_lshrrev_b64':
+                r = g(l, a[2], 2) >> (g(l, a[1]) & 63)
+            elif op == 'v_ashrrev_i64':
+                r = s64(g(l, a[2], 2)) >> (g(l, a[1]) & 63)
+            elif op == 'v_cndmask_b32_e64':
+                r = g(l, a[2]) if (self.sget(a[3], 2) >> l) & 1 else g(l, a[1])
+            elif op == 'v_cndmask_b32_e32':
+                r = g(l, a[2]) if (self.vcc >> l) & 1 else g(l, a[1])
+            else:
+                raise NotImplementedError(op)
+            self.vset(l, a[0], r & (M64 if self.rr(a[0])[2] == 2 else M32))
+
+
+def parse(asm):
+    prog, labels = [], {}
+    for raw in asm.splitlines():
+        s = raw.split('//')[0].strip()
+        if not s:
+            continue
+        if s.startswith('.amdhsa_kernel') or s.startswith('.rodata'):
+            break
+        if s.endswith(':'):
+            labels[s[:-1]] = len(prog)
+            continue
+        if s.startswith('.'):
+            continue
+        parts = s.split(None, 1)
+        op = parts[0]
+        args = []
+        if len(parts) > 1:
+            rest = parts[1]
+            # split on commas, then keep modifiers (offset:, quad_perm:...) as separate tokens
+            toks = [t.strip() for t in re.split(r',(?![^\[]*\])', rest)]
+            for t in toks:
+                args.extend(t.split())
+        prog.append((op, args))
+    return prog, labels
+
+
+def run_workgroup(asm, lds_bytes, waves, mem, kernarg_addr, wg, nvgpr):
+    prog, labels = parse(asm)
+    lds = bytearray(lds_bytes)
+    ws = [Wave(prog, labels, lds, mem, {0: kernarg_addr & M32, 1: kernarg_addr >> 32, 2: wg}, 64 * w, nvgpr)
+          for w in range(waves)]
+    for w in ws:
+        w.run()
+    for w in ws:
+        w.at_barrier = False
+        w.run()
+    return sum(w.count for w in ws)
+
+
+def selftest(ntests=16):
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
+    sys.path.insert(0, here)
+    import gen_addb as ga
+    import addb_model as am
+    rng = random.Random(5)
+    asm = ga.gen_addb('fthe_addb_q152')
+    for trial, n in enumerate((am.rand_n(rng), (1 << 2047) + 1)):
+        N = n * n
+        img = am.addb_image(N)
+        assert len(img) == ga.KCTX_BYTES
+        xs = [rng.randrange(N) for _ in range(ntests)]
+        ys = [rng.randrange(N) for _ in range(ntests)]
+        xs[0], ys[0] = N - 1, N - 1
+        xs[1], ys[1] = 0, N - 1
+        xs[2], ys[2] = 1, 1
+        xs[3], ys[3] = (1 << 4096) - 1, (1 << 4096) - 1          # rows >= N (reduced all the same)
+        xs[4], ys[4] = N, N + 5
+        count = ntests - (3 if trial else 0)         # a partly live wave on the second key
+        mem = Mem()
+        XB, YB, OB, KB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000, 0x50000000
+        mem.alloc(b''.join(x.to_bytes(512, 'little') for x in xs), XB)
+        mem.alloc(b''.join(y.to_bytes(512, 'little') for y in ys), YB)
+        mem.alloc(bytes(512 * ntests), OB)
+        mem.alloc(img, KB)
+        karg = XB.to_bytes(8, 'little') + YB.to_bytes(8, 'little') + OB.to_bytes(8, 'little') + \
+            KB.to_bytes(8, 'little') + count.to_bytes(4, 'little') + bytes(4)
+        mem.alloc(karg, KA)
+        steps = run_workgroup(asm, ga.LDS_BYTES, ga.WAVES, mem, KA, 0, 168)
+        bad = 0
+        for i in range(ntests):
+            got = mem.read(OB + 512 * i, 512)
+            want = xs[i] * ys[i] % N if i < count else 0
+            if got != want:
+                bad += 1
+                print(f"  ciphertext {i}: mismatch")
+        print(f"key {trial}: {count} adds, {bad} mismatches, {steps} wave-instructions emulated")
+        assert bad == 0
+    print("wave_emu selftest OK")
+
+
+if __name__ == '__main__':
+    selftest()
