@@ -2958,12 +2958,13 @@ static int launch_addb(fthe_ctx *c, const fthe_key *k, const uint32_t *x, const 
                        size_t count) {
     if (count == 0) return FTHE_OK;
     if (count > 0xFFFFFFFFu / 2) return FTHE_ERR_ARG;
-    struct { const void *x, *y; void *o; const void *kc; uint32_t count, pad; } args = {x, y, out, k->d_addb,
-                                                                                      (uint32_t)count, 0};
+    // persistent workgroups, one per CU at most: each wave sweeps batches of 16 rows across the grid
+    const unsigned blocks = (unsigned)std::min<size_t>((count + kAddbPerWg - 1) / kAddbPerWg, (size_t)c->n_cu);
+    struct { const void *x, *y; void *o; const void *kc; uint32_t count, nwg; } args = {x, y, out, k->d_addb,
+                                                                                      (uint32_t)count, blocks};
     static_assert(sizeof(args) == 40, "kernarg layout of gen_addb.py");
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    const unsigned blocks = (unsigned)((count + kAddbPerWg - 1) / kAddbPerWg);
     if (hipModuleLaunchKernel(c->fn_addb, blocks, 1, 1, 64 * kAddbWaves, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
         return FTHE_ERR_HIP;
     return FTHE_OK;
@@ -2998,6 +2999,12 @@ static int pair_impl(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, cw = 2 * k->n_words;
     const bool addb = !sub && k->d_addb && c->fn_addb;
+    if (addb && !pipe) {
+        // device rows: one launch of persistent workgroups for the whole batch (no chunk tails)
+        if ((rc = launch_addb(c, k, a, b, out, count))) return rc;
+        Lc.mm += (double)count;
+        return end_call(c, Lc);
+    }
     if (sub || !k->rowio || !k->add_classical) Lc.fill(SL_C0, k->c_R2n2);    // the classical add needs no R^2
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);

@@ -29,7 +29,8 @@ per wave, 12 waves per workgroup (one workgroup per CU: its LDS holds the key's 
      r = (z - r2) mod 2^4104 (dword borrow chains, rippled across the quad) lies in [0, 3N); two
      conditional subtractions of N (dwords from the key's context) make it canonical; rows are stored.
 
-kernarg: 0 u64 x rows, 8 u64 y rows, 16 u64 out rows, 24 u64 kctx, 32 u32 count.
+kernarg: 0 u64 x rows, 8 u64 y rows, 16 u64 out rows, 24 u64 kctx, 32 u32 count, 36 u32 workgroups launched
+(persistent: each wave takes batches of 16 ciphertexts wg*12 + wave, + 12 * workgroups, ...).
 kctx: the LDS image (IMG_BYTES: mu copies, N copies, corrections), then N as 128 dwords.
 """
 import os
@@ -119,7 +120,7 @@ def gen_addb(name: str) -> str:
     NV = 8                                        # N dwords for the canonicalisation (v8..v39, BQ dead)
     RR = 44                                       # r dwords (reuses DQ after the subtraction) v44..v75, v76
     R128 = 76
-    TT, TT128 = 114, 146                          # r - N dwords v114..v145 (+ dword 128)
+    TT, TT128 = 80, 112                           # r - N dwords v80..v111 (+ dword 128): ZL is dead by then
     NVGPR = 168
 
     def X(k):
@@ -189,22 +190,17 @@ def gen_addb(name: str) -> str:
             e('  s_mov_b64 exec, s[16:17]')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
-    # ---- this wave's ciphertexts: g = wg*192 + wave*16 + (lane >> 2); leave if none is live ------------
+    # ---- the wave's batches of 16 ciphertexts: batch b = wg * WAVES + wave, then b += nwg * WAVES (kernarg
+    #      36: the launch's workgroup count) -- persistent waves, no workgroup tails, phases desynchronise ----
     e(f'  v_lshrrev_b32_e32 v{V_SH}, 6, v{V_TID}')                     # wave
+    e('  s_nop 1')                                                      # VALU write -> v_readfirstlane: 1 state
     e('  v_readfirstlane_b32 s14, v5')
-    e(f'  s_mul_i32 s13, s2, {WAVES * CT_PER_WAVE}')
-    e(f'  s_lshl_b32 s15, s14, 4')
-    e('  s_add_u32 s13, s13, s15')                                      # first ciphertext of the wave
-    e('  s_cmp_ge_u32 s13, s12')
-    e('  s_cbranch_scc1 .Lend')
-    # ROW = g*512 + j*128 = wg*98304 + tid*128
-    e(f'  s_mul_i32 s15, s2, {WAVES * CT_PER_WAVE * 512}')
-    e(f'  v_lshlrev_b32_e32 v{V_ROW}, 7, v{V_TID}')
-    e(f'  v_add_u32_e32 v{V_ROW}, s15, v{V_ROW}')
-    # live lanes: g < count
-    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
-    e(f'  v_cmp_gt_u32_e32 vcc, s12, v{V_TMP}')
-    e(f'  s_mov_b64 {LIVE}, vcc')
+    e('  s_load_dword s19, s[0:1], 0x24')
+    e(f'  s_mul_i32 s13, s2, {WAVES}')
+    e('  s_add_u32 s13, s13, s14')
+    e(f'  s_lshl_b32 s13, s13, 4')                                      # first ciphertext of the wave
+    e('  s_waitcnt lgkmcnt(0)')
+    e(f'  s_mul_i32 s19, s19, {WAVES * CT_PER_WAVE}')                   # ciphertexts per sweep of the grid
     # wave area base + 4c; lane j's A-column write base (rows 38j ..), the ciphertext's A column
     e(f'  s_mul_i32 s15, s14, {WAVE_AREA}')
     e(f'  s_add_u32 s15, s15, {LDS_WAVES}')
@@ -242,11 +238,22 @@ def gen_addb(name: str) -> str:
     e(f'  v_add_u32_e32 v{V_GR}, s15, v{V_GR}')                        # group row c (fold reads)
     e(f'  v_mul_u32_u24_e32 v{V_Q3W}, {QROW}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_Q3W}, s15, v{V_Q3W}')                      # staging row c (+ 128 j below)
-    e(f'  v_bfe_u32 v{V_SH}, v{V_ROW}, 7, 2')                          # j
+    e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_TID}')                         # j
     e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_SH}')
     e(f'  v_add_u32_e32 v{V_Q3W}, v{V_Q3W}, v{V_TMP}')
     e(f'  v_subrev_u32_e32 v{V_Q3W}, 4, v{V_Q3W}')                    # + 128 j - 4 (dword 32 j - 1)
     e(f'  v_lshlrev_b32_e32 v{V_SH}, 1, v{V_SH}')                      # 2 j (the row-I/O shift)
+    e(f'  v_and_b32_e32 v{V_TID}, 63, v{V_TID}')
+    e(f'  v_lshlrev_b32_e32 v{V_TID}, 7, v{V_TID}')                    # v0 = lane * 128 from here on
+    e('.Lbatch:')
+    e('  s_cmp_ge_u32 s13, s12')
+    e('  s_cbranch_scc1 .Lend')
+    # ROW = g*512 + j*128 = first*512 + lane*128; live lanes: g < count
+    e('  s_lshl_b32 s17, s13, 9')
+    e(f'  v_add_u32_e32 v{V_ROW}, s17, v{V_TID}')
+    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 9, v{V_ROW}')
+    e(f'  v_cmp_gt_u32_e32 vcc, s12, v{V_TMP}')
+    e(f'  s_mov_b64 {LIVE}, vcc')
 
     # ---- row I/O helpers (gen_montprog.gen_quad's LOADW / STOREW, for this register plan) ---------------
     W0 = TB                                       # 33 loaded row words (ring area, free outside the product)
@@ -496,7 +503,7 @@ def gen_addb(name: str) -> str:
 
     mfma_product(1)
     # clamp: a negative N1 (lane 3's final carry) -> q3 = 0
-    e('  s_nop 1')
+    e('  s_nop 4')                                                      # EXEC written by SALU -> DPP
     e(f'  v_mov_b32_dpp v{CR2}, v{CR + 1} quad_perm:[3,3,3,3] {DPP}')
     e(f'  v_cmp_gt_i32_e32 vcc, 0, v{CR2}')
     for g in range(36):
@@ -573,8 +580,11 @@ def gen_addb(name: str) -> str:
     e(f'  s_mov_b64 exec, {LIVE}')
     for i in range(8):
         e(f'  global_store_dwordx4 v{V_ROW}, {quad4(RR + 4 * i)}, s[8:9] offset:{16 * i}')
-    e('  s_waitcnt vmcnt(0)')
+    e('  s_mov_b64 exec, -1')
+    e('  s_add_u32 s13, s13, s19')
+    e('  s_branch .Lbatch')
     e('.Lend:')
+    e('  s_waitcnt vmcnt(0)')
     e('  s_endpgm')
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
@@ -608,7 +618,7 @@ def descriptor(name, lds_bytes, nvgpr, nsgpr):
     e('amdhsa.kernels:')
     e('  - .args:')
     for off_, sz, kind in ((0, 8, 'global_buffer'), (8, 8, 'global_buffer'), (16, 8, 'global_buffer'),
-                           (24, 8, 'global_buffer'), (32, 4, 'by_value')):
+                           (24, 8, 'global_buffer'), (32, 4, 'by_value'), (36, 4, 'by_value')):
         e(f'      - .offset: {off_}')
         e(f'        .size: {sz}')
         e(f'        .value_kind: {kind}')

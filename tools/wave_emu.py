@@ -433,7 +433,7 @@ def run_workgroup(asm, lds_bytes, waves, mem, kernarg_addr, wg, nvgpr):
     return sum(w.count for w in ws)
 
 
-def selftest(ntests=16):
+def selftest(ntests=16, count0=None):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
     sys.path.insert(0, here)
@@ -453,6 +453,8 @@ def selftest(ntests=16):
         xs[3], ys[3] = (1 << 4096) - 1, (1 << 4096) - 1          # rows >= N (reduced all the same)
         xs[4], ys[4] = N, N + 5
         count = ntests - (3 if trial else 0)         # a partly live wave on the second key
+        if count0 is not None:
+            count = count0 - (3 if trial else 0)
         mem = Mem()
         XB, YB, OB, KB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000, 0x50000000
         mem.alloc(b''.join(x.to_bytes(512, 'little') for x in xs), XB)
@@ -460,7 +462,7 @@ def selftest(ntests=16):
         mem.alloc(bytes(512 * ntests), OB)
         mem.alloc(img, KB)
         karg = XB.to_bytes(8, 'little') + YB.to_bytes(8, 'little') + OB.to_bytes(8, 'little') + \
-            KB.to_bytes(8, 'little') + count.to_bytes(4, 'little') + bytes(4)
+            KB.to_bytes(8, 'little') + count.to_bytes(4, 'little') + (1).to_bytes(4, 'little')
         mem.alloc(karg, KA)
         steps = run_workgroup(asm, ga.LDS_BYTES, ga.WAVES, mem, KA, 0, 168)
         bad = 0
@@ -476,4 +478,7 @@ def selftest(ntests=16):
 
 
 if __name__ == '__main__':
-    selftest()
+    if len(sys.argv) > 1:                     # e.g. 211: wave 0 takes a second batch (the grid-stride loop)
+        selftest(ntests=int(sys.argv[1]), count0=int(sys.argv[1]))
+    else:
+        selftest()
