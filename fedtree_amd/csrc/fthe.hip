@@ -3060,6 +3060,22 @@ static int rowprod_impl(fthe_key *k, fthe_ctx *c, const uint32_t *const *xs, int
     const int base = nslots_for(k);               // inputs live after the standard slots
     const bool rowio = k->rowio && kk + 1 <= 16;
     Launch Lc;
+    bool chain = classical && kk >= 2 && k->d_addb && c->fn_addb;
+    for (int j = 2; j < kk && chain; j++) {       // out must not overlap an input still to be read
+        const size_t bytes = count * 8 * (size_t)k->n_words;
+        const char *o = (const char *)out, *x = (const char *)xs[j];
+        chain = o + bytes <= x || x + bytes <= o;
+    }
+    if (chain) {
+        // plain k-way products with a 2048-bit n: a chain of matrix-core Barrett adds over the whole batch,
+        // out = x_0 x_1, then out = out x_j (rows are independent, so out may alias x_0 or x_1)
+        int rc = begin_call(c, k, count, Lc, SL_C0 + 1, k->sn2, rowio_chunk_lanes());
+        if (rc) return rc;
+        for (int j = 1; j < kk; j++)
+            if ((rc = launch_addb(c, k, j == 1 ? xs[0] : out, xs[j], out, count))) return rc;
+        Lc.mm += (double)count * (kk - 1);
+        return end_call(c, Lc);
+    }
     int rc = rowio ? begin_call(c, k, count, Lc, SL_C0 + 1, k->sn2, rowio_chunk_lanes())   // constant slot only
                    : begin_call(c, k, count, Lc, base + kk, k->sn2);
     if (rc) return rc;

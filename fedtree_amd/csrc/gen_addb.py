@@ -54,10 +54,11 @@ CORR2_OFF = CORR1_OFF + TILES1 * 64
 IMG_BYTES = CORR2_OFF + TILES2 * 64          # 29,824
 N_OFF = IMG_BYTES                            # N dwords in kctx (not copied to LDS)
 KCTX_BYTES = N_OFF + 512
-WAVE_AREA = S * RB                           # 10,336: A column / q staging (16 x 576) / groups (16 x 296)
+WAVE_AREA = 10496                            # A column (152 x 68) / q staging (16 x 656) / groups (16 x 296)
 LDS_WAVES = IMG_BYTES
 LDS_BYTES = LDS_WAVES + WAVES * WAVE_AREA    # 153,856
-QROW = 576                                   # q staging row (9 K-blocks of 64 bytes)
+QROW = 656                                   # q staging row: 9 K-blocks of 64 bytes, stride = 4 (mod 32)
+                                             # dwords: the quads' staging writes 4-way, not 16-way, per bank
 GROW = 296                                   # group staging row (36 int64 groups + pad: conflict-free)
 KB1, KB2 = 9, 9
 NQ1, NQ3 = 129, 129                          # q1, q3 dwords (rows >= N: q3 < 2^4098)
@@ -67,6 +68,7 @@ BIAS_COL, BIAS_DIGIT = 515, -2               # -2^4121 in product 1's correction
 M_A = (0, 1, 2, 3, 12, 13, 14, 15)           # rows whose copies sit in slots 0..7 (ds_read_b128 lane groups)
 M_B = (4, 5, 6, 7, 8, 9, 10, 11)             # slots 8..15
 assert IMG_BYTES % 16 == 0 and WAVE_AREA % 16 == 0 and LDS_BYTES <= 160 * 1024
+assert WAVE_AREA >= max(S * RB, 16 * QROW) and QROW % 16 == 0 and (QROW // 4) % 32 == 4
 
 
 def layout_header():
@@ -107,7 +109,8 @@ def gen_addb(name: str) -> str:
     XB = 8                                        # X limbs v8..v45 (product phase), later other limbs
     TB = 46                                       # ring of NT 64-bit columns v46..v125
     NT = Q + 2
-    WD = 46                                       # W dwords (after the product) v46..v77
+    WD = 47                                       # W dwords (after the product) v47..v78: W[i], W[i+1] of odd i
+                                                  # is an even register pair (one ds_write_b64)
     ZLB = 80                                      # z mod 2^4104 dwords v80..v111, v112 = bits 4096..4103
     ZL128 = 112
     BQ = 8                                        # B operands, 9 x 4 = v8..v43
@@ -400,12 +403,16 @@ def gen_addb(name: str) -> str:
     e(f'  ds_write_b32 v{V_TMP + 1}, v{V_TMP}')
     e('  s_mov_b64 exec, s[22:23]')
     e(f'  v_mov_b32_e32 v{V_TMP}, 0')
-    for d in range(NQ1, QROW // 4):
+    for d in range(NQ1, 16 * KB1):                # the B reads cover 64 KB1 bytes
         e(f'  ds_write_b32 v{V_Q3W}, v{V_TMP} offset:{4 + 4 * d}')      # lane 0: row - 4
     e('  s_mov_b64 exec, -1')
     for i in range(32):
         e(f'  v_xor_b32_e32 v{WD + i}, s33, v{WD + i}')
-        e(f'  ds_write_b32 v{V_Q3W}, v{WD + i} offset:{8 + 4 * i}')
+    # W[i] at dword 1 + 32 j + i: W[0] and W[31] alone, the pairs (W[i], W[i+1]) of odd i 8-byte aligned
+    e(f'  ds_write_b32 v{V_Q3W}, v{WD} offset:8')
+    for i in range(1, 31, 2):
+        e(f'  ds_write_b64 v{V_Q3W}, v[{WD + i}:{WD + i + 1}] offset:{8 + 4 * i}')
+    e(f'  ds_write_b32 v{V_Q3W}, v{WD + 31} offset:{8 + 4 * 31}')
     e('  s_waitcnt lgkmcnt(0)')
     for kb in range(KB1):
         e(f'  ds_read_b128 {quad4(BQ + 4 * kb)}, v{V_B} offset:{64 * kb}')

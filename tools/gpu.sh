@@ -3,6 +3,7 @@
 #   bash tools/gpu.sh TAG STEP [STEP ...]
 # Steps (outputs under gpurun_out/, prefixed with TAG):
 #   suite          python -m pytest tests -m gpu (thread timeouts: a hang names its test)
+#   test:FILE      python -m pytest FILE -m gpu (one test file, same timeouts)
 #   smoke          __graft_entry__.smoke()
 #   bench          python bench.py (the driver's default line)              -> TAG_bench.json
 #   bench:ARGS     python bench.py ARGS (comma-separated, e.g. bench:--steps,3)
@@ -43,6 +44,11 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         > ${O}_pytest_gpu.txt 2>&1 || fail suite $? ${O}_pytest_gpu.txt
       tail -3 ${O}_pytest_gpu.txt;;
+    test:*)
+      f=${step#test:}
+      timeout -k 10 600 python -u -m pytest $f -m gpu -x -v --timeout 300 --timeout-method thread \
+        > ${O}_$(basename $f .py).txt 2>&1 || fail "$step" $? ${O}_$(basename $f .py).txt
+      tail -3 ${O}_$(basename $f .py).txt;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.txt 2>&1 \
         || fail smoke $? ${O}_smoke.txt
@@ -67,7 +73,8 @@ for step in "$@"; do
       pmc_pass $w occ OccupancyPercent
       pmc_pass $w sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS \
         SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE
-      pmc_pass $w mf SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY;;
+      pmc_pass $w mf SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
+      pmc_pass $w lds SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU;;
     opstrace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_ops_trace -o ops -- \
         python3 tools/prof_ops.py --n 1048576 --ops add,kway > ${O}_ops_trace.log 2>&1 || fail opstrace $? ${O}_ops_trace.log;;

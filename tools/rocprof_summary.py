@@ -67,7 +67,7 @@ def pmc(dirs, out):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 kn = r.get("Kernel_Name", "")
-                if not kn.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic")):
+                if not kn.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic", "fthe_addb")):
                     continue
                 key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                 agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
@@ -110,12 +110,12 @@ def pmc_round(tag, out):
     res = {}
     for w in ("enc", "add", "kway", "pub"):
         per = {}
-        for t in ("fetch", "write", "vb", "occ", "sq", "mf"):
+        for t in ("fetch", "write", "vb", "occ", "sq", "mf", "lds"):
             for f in glob.glob(f"gpurun_out/{tag}_pmc_{w}_{t}/**/*counter_collection.csv", recursive=True):
                 acc = {}
                 for r in csv.DictReader(open(f)):
                     kn = r["Kernel_Name"]
-                    if not kn.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic")):
+                    if not kn.startswith(("fthe_montprog", "fthe_padic", "fthe_nadic", "fthe_addb")):
                         continue
                     key = (kn, r["Dispatch_Id"], r["Counter_Name"])
                     acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
@@ -137,7 +137,7 @@ def pmc_round(tag, out):
     tr = glob.glob(f"gpurun_out/{tag}_ops_trace/*kernel_trace.csv")
     if tr:
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-                for r in csv.DictReader(open(tr[0])) if r["Kernel_Name"] == "fthe_montprog_s152"]
+                for r in csv.DictReader(open(tr[0])) if r["Kernel_Name"] in ("fthe_montprog_s152", "fthe_addb_q152")]
         h = len(durs) // 2
         full = lambda ds: [d for d in ds if d >= 0.9 * max(ds)] if ds else []
         add, kway = full(durs[:h]), full(durs[h:])
