@@ -117,7 +117,8 @@ def gen_addb(name: str) -> str:
     DQ = 44                                       # fold output dwords v44..v79 (36)
     ACC = (114, 118)                              # two accumulator sets
     AOP = (122, 126, 130, 134)                    # four A-operand buffers (reads two MFMAs ahead)
-    PG, FV, CR, CR2 = 162, 164, 166, 6            # int64 pairs (CR2 = V_TMP, free in the MFMA phases)
+    PG, FV = 162, 164                             # int64 pairs
+    CR, CR2 = 166, 6                              # int32 chunk carries (CR2 = V_TMP, free in the MFMA phases)
     V_A1, V_A2, V_C, V_B, V_G, V_GR, V_Q3W, V_ZR = 138, 139, 140, 141, 142, 143, 144, 145
     GB = 146                                      # group read buffer, 8 int64 = v146..v161
     NV = 8                                        # N dwords for the canonicalisation (v8..v39, BQ dead)
@@ -271,8 +272,11 @@ def gen_addb(name: str) -> str:
         e(f'  global_load_dword v{W0 + 32}, v{V_TMP}, {sbase}')
         e('  s_waitcnt vmcnt(0)')
         e('  s_not_b64 exec, exec')                                      # dead lanes: zero operand
+        lab = f'.Llive{len(o)}'
+        e(f'  s_cbranch_execz {lab}')                                    # (only in a partial batch)
         for i in range(33):
             e(f'  v_mov_b32_e32 v{W0 + i}, 0')
+        e(f'{lab}:')
         e('  s_mov_b64 exec, -1')
         e(f'  v_cndmask_b32_e64 v{W0 + 32}, v{W0 + 32}, 0, s[20:21]')
         for i in range(32):
@@ -329,6 +333,7 @@ def gen_addb(name: str) -> str:
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 
+    e('// @phase load')
     # ---- 1. x -> X limbs; y -> limbs -> the wave's A column (rows 38j + k of column c) ------------------
     load_row_limbs('s[4:5]', X)
     load_row_limbs('s[6:7]', lambda k: f"v{TB + 40 + k}")              # y limbs (ring area above W0)
@@ -336,6 +341,7 @@ def gen_addb(name: str) -> str:
         e(f'  ds_write_b32 v{V_ZR}, v{TB + 40 + k} offset:{k * RB}')
     e('  s_waitcnt lgkmcnt(0)')
 
+    e('// @phase product')
     # ---- 2. z = x y: 152 steps; step i reads a_i (prefetched), adds a_i X into the window, retires the
     #         lowest column: its carry stays in the lane's next column, its low 27 bits go one lane down (the
     #         top column of lane j-1), and lane 0's -- the product limb z_i -- into A-column row i ---------
@@ -354,17 +360,18 @@ def gen_addb(name: str) -> str:
                 e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
             if k == 7:
                 e(f'  v_and_b32_e32 {Tlo(u)}, {hex(MASK)}, {Tlo(u)}')
-            if k == 10:
+            if k == 10 and prefetch is not None:
+                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{prefetch * RB}')
+            if k == 12:                              # after the read: the step's wait leaves the write out
                 e('  s_mov_b64 exec, s[22:23]')
                 e(f'  ds_write_b32 v{V_LDSI}, {Tlo(u)} offset:{row * RB}')
                 e('  s_mov_b64 exec, -1')
-            if k == 12 and prefetch is not None:
-                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{prefetch * RB}')
             if k == 14:
                 e(f'  v_cndmask_b32_e64 {Tlo(u)}, {Tlo(u)}, 0, s[22:23]')
         e(f'  v_mov_b32_dpp {Tlo(u + Q)}, {Tlo(u)} quad_perm:[1,2,3,0] {DPP}')
         e(f'  v_mov_b32_e32 {Thi(u + Q)}, 0')
-        e('  s_waitcnt lgkmcnt(0)')
+        if prefetch is not None:
+            e('  s_waitcnt lgkmcnt(1)')
 
     NTRIP, TL = S // NT, S % NT
     assert NT % 2 == 0
@@ -380,6 +387,7 @@ def gen_addb(name: str) -> str:
         step(u, u, u + 1 if u + 1 < TL else None)
     e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB)}, v{V_LDSI}')
 
+    e('// @phase window')
     # ---- 3. window -> W limbs (X), W -> dwords WD; z mod 2^4104 limbs (LDS) -> dwords ZL ---------------
     e(f'  v_mov_b64_e32 {tmp}, 0')
     for k in range(Q):
@@ -394,6 +402,7 @@ def gen_addb(name: str) -> str:
     limbs_to_words(X, lambda i: f"v{ZLB + i}", f"v{V_AI[1]}", f"v{V_AI[0]}")
     e(f'  v_lshrrev_b32_e32 v{ZL128}, 19, {X(Q - 1)}')                # lane 3: bits 4096..4103 (limb 151 >> 19)
 
+    e('// @phase q1stage')
     # ---- 4. q1 staging: dword 0 = bits 4072..4103 (lane 3), dwords 1.. = W, 129..143 = 0 (fed 0) --------
     e(f'  v_lshrrev_b32_e32 v{V_TMP}, 8, v{ZLB + 31}')
     e(f'  v_lshl_or_b32 v{V_TMP}, v{ZL128}, 24, v{V_TMP}')
@@ -428,7 +437,7 @@ def gen_addb(name: str) -> str:
         KO = KO1 if prod == 1 else KO2
         act = ACT1 if prod == 1 else ACT2
         corr = 0 if prod == 1 else CORR2_OFF - CORR1_OFF
-        e(f'  v_mov_b64_e32 {pair(CR)}, 0')
+        e(f'  v_mov_b32_e32 v{CR}, 0')
         for j, tiles in enumerate(CHUNKS):
             t0 = tiles[0]
             ops = [(n, t, kb) for n, t in enumerate(tiles) for kb in act[t]]
@@ -485,36 +494,51 @@ def gen_addb(name: str) -> str:
             if j:
                 e('  s_nop 1')
                 e(f'  v_mov_b32_dpp v{CR2}, v{CR} quad_perm:[0,0,1,2] {DPP}')
-                e(f'  v_mov_b32_dpp v{CR2 + 1}, v{CR + 1} quad_perm:[0,0,1,2] {DPP}')
-                e(f'  v_mov_b64_e32 {pair(CR)}, {pair(CR2)}')
+            e('// @phase norm')
             e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
             ng = 4 * len(tiles)
+            # D_g = low dword of (group g + carry), carry = its high dword (signed): one v_mad_i64_i32 per
+            # group (carry x 1 + group); an even g writes the pair (D_g, D_g+1), D_g+1 holding the carry
+            # until the odd group's result replaces it
+            cv = f"v{CR2}" if j else f"v{CR}"
+            assert DQ % 2 == 0 and ng % 2 == 0
             for g0 in range(0, ng, 8):
                 for g in range(g0, min(ng, g0 + 8)):
                     e(f'  ds_read_b64 {pair(GB + 2 * (g - g0))}, v{V_GR} offset:{8 * g}')
                 e('  s_waitcnt lgkmcnt(0)')
                 for g in range(g0, min(ng, g0 + 8)):
-                    e(f'  v_lshl_add_u64 {pair(FV)}, {pair(GB + 2 * (g - g0))}, 0, {pair(CR)}')
-                    e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
-                    e(f'  v_ashrrev_i64 {pair(CR)}, 32, {pair(FV)}')
+                    if g % 2 == 0:
+                        e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
+                        cv = f"v{DQ + g + 1}"
+                    else:
+                        e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
+                        e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
+                        cv = f"v{FV + 1}"
+            e(f'  v_mov_b32_e32 v{CR}, {cv}')
             e('  s_mov_b64 exec, -1')
+            e(f'// @phase prod{prod}')
 
     def fold_tile(acc, gl):
         """acc's 4 int32 rows (output bytes 4h..4h+3 of the tile) -> int64 group -> LDS (group 4 (t - t0) + h)"""
-        e(f'  v_ashrrev_i32_e32 v{PG + 1}, 31, v{acc}')
-        e(f'  v_mov_b32_e32 v{PG}, v{acc}')
+        e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc}, 1, 0')                # sign-extended row 0
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 1}, s30, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 2}, s31, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 3}, s32, {pair(PG)}')
         e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{8 * gl}')
 
+    e('// @phase prod1')
     mfma_product(1)
+    e('// @phase q3stage')
     # clamp: a negative N1 (lane 3's final carry) -> q3 = 0
     e('  s_nop 4')                                                      # EXEC written by SALU -> DPP
-    e(f'  v_mov_b32_dpp v{CR2}, v{CR + 1} quad_perm:[3,3,3,3] {DPP}')
+    e(f'  v_mov_b32_dpp v{CR2}, v{CR} quad_perm:[3,3,3,3] {DPP}')
     e(f'  v_cmp_gt_i32_e32 vcc, 0, v{CR2}')
+    e('  s_and_saveexec_b64 s[16:17], vcc')
+    e('  s_cbranch_execz .Lnoclamp')                                   # (q1 = 0: z < 2^4072 only)
     for g in range(36):
-        e(f'  v_cndmask_b32_e64 v{DQ + g}, v{DQ + g}, 0, vcc')
+        e(f'  v_mov_b32_e32 v{DQ + g}, 0')
+    e('.Lnoclamp:')
+    e('  s_mov_b64 exec, s[16:17]')
     # q3 dword i = D_{i+1}: lane j writes its D_{32j+k} (k = 0..31; lane 3 also k = 32, 33) at dword 32j + k - 1
     for k in range(34):
         e(f'  v_xor_b32_e32 v{DQ + k}, s33, v{DQ + k}')
@@ -532,9 +556,11 @@ def gen_addb(name: str) -> str:
     for kb in range(KB2):
         e(f'  ds_read_b128 {quad4(BQ + 4 * kb)}, v{V_B} offset:{64 * kb}')
     e('  s_waitcnt lgkmcnt(0)')
+    e('// @phase prod2')
     mfma_product(2)
     # lane 3 keeps D2_128's low 8 bits (r2 mod 2^4104)
 
+    e('// @phase sub')
     # ---- 7. r = (z - r2) mod 2^4104: borrow chains per lane, rippled across the quad --------------------
     def borrow_ripple(lab, R, R128_, bo, bin_):
         """lane k (k < 3) hands its borrow bo (0/1) to lane k+1, which subtracts it from its dwords R(0..31)
@@ -563,6 +589,7 @@ def gen_addb(name: str) -> str:
     borrow_ripple('.Lrb', RR, R128, V_AI[0], V_AI[1])
     e(f'  v_and_b32_e32 v{R128}, 0xff, v{R128}')                        # r = (z - r2) mod 2^4104, < 3N
 
+    e('// @phase canon')
     # ---- 8. two conditional subtractions of N, then the canonical row ------------------------------------
     e(f'  v_bfe_u32 v{V_TMP}, v{V_ROW}, 7, 2')
     e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_TMP}')                     # 128 j
@@ -584,6 +611,7 @@ def gen_addb(name: str) -> str:
         for i in range(32):
             e(f'  v_cndmask_b32_e32 v{RR + i}, v{RR + i}, v{TT + i}, vcc')
         e(f'  v_cndmask_b32_e32 v{R128}, v{R128}, v{TT128}, vcc')
+    e('// @phase store')
     e(f'  s_mov_b64 exec, {LIVE}')
     for i in range(8):
         e(f'  global_store_dwordx4 v{V_ROW}, {quad4(RR + 4 * i)}, s[8:9] offset:{16 * i}')

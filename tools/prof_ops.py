@@ -38,9 +38,10 @@ def main():
         print("add", n, "ms", dev.last_kernel_ms())
     if "kway" in ops:
         x = torch.stack([c] * 8)
-        pl.reduce_kway_dev(x, 8, o)
-        dev.sync()
-        print("kway8", n, "ms", dev.last_kernel_ms())
+        for _ in range(3):                            # configs[3] at --n 2097152 (256 x 4096 bins x {g, h})
+            pl.reduce_kway_dev(x, 8, o)
+            dev.sync()
+            print("kway8", n, "ms", dev.last_kernel_ms())
     if "mont" in ops:                                 # Montgomery-resident add (one product per add)
         mr = torch.empty_like(c)
         pl.to_mont_dev(c, mr)

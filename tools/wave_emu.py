@@ -157,6 +157,10 @@ class Wave:
             if self.scc:
                 self.pc = self.labels[a[0]]
             return
+        if op == 's_cbranch_execz':
+            if self.exec == 0:
+                self.pc = self.labels[a[0]]
+            return
         if op == 's_cbranch_vccz':
             if (self.vcc & self.exec) == 0:
                 self.pc = self.labels[a[0]]
