@@ -47,7 +47,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
-PMC_FILE = "r03b_pmc.json"
+PMC_FILE = "r03n_pmc.json"
 
 
 def parse():
@@ -780,23 +780,34 @@ def run(a, world):
         add_s = sorted(add_ts)[2]
         secondary["p2048_add_per_s"] = round(na / add_s)
         secondary["p2048_add_per_s_range"] = [round(na / max(add_ts)), round(na / min(add_ts))]
-        prods = lib.fthe_last_montmuls(dev.ctx) / na          # 4096-bit products per add (1: classical MULWC)
+        prods = lib.fthe_last_montmuls(dev.ctx) / na          # 4096-bit products per add
         # the add kernel's HBM side (north star): algorithmic bytes (2 rows in, 1 out, 512 B each)
-        # over the live launch time, and the PMC-measured bytes of a full-chunk launch
-        pk = pmc.get("add", {}).get("fthe_montprog_s152", {})
+        # over the live launch time, and the PMC-measured bytes of one launch
+        padd = pmc.get("add", {})
+        kname = "fthe_addb_q152" if "fthe_addb_q152" in padd else "fthe_montprog_s152"
+        pk = padd.get(kname, {})
         rate = na / add_s
+        # fthe_addb_q152 (gen_addb.py): z = x y on the VALU, 152 x 152 radix-2^27 v_mad_u64_u32 per add; both
+        # Barrett products (q1 mu, q3 n^2) on the i8 matrix cores, 338 v_mfma_i32_16x16x64_i8 per 16 adds
+        valu_macs = 152 * 152
+        i8_macs = 338 * 16 * 16 * 64 / 16
+        i8_peak = 1024 * 2.4e9 * (32 * 32 * 32 * 2) / 32
         secondary["p2048_add_hbm"] = {"algorithmic_GBps": round(na * 1536 / add_s / 1e9, 1),
                                       "pmc_GBps": pk.get("hbm_GBps"), "pmc_VALUBusy": pk.get("VALUBusy"),
+                                      "pmc_kernel": kname if pk else None,
                                       "pmc_source": f"profiles/{PMC_FILE}" if pk else None,
                                       "peak_GBps": 8000,
-                                      "bound": f"valu ({prods:g} product(s) of 4096 bits per add: classical MSB-first "
-                                               "x y mod n^2, no R^2 correction)",
-                                      # VALU roofline: executed MADs (2*152^2 per product at radix
-                                      # 2^27) and the survey's unit, one W(128) = 2*128^2+128 MACs per add
+                                      "bound": "valu: x y on the VALU (one 4096-bit product per add), its Barrett "
+                                               "reduction by n^2 on the i8 matrix cores (fthe_addb_q152)",
+                                      # VALU roofline: executed VALU MADs per add and the survey's
+                                      # unit, one W(128) = 2*128^2+128 MACs per add
                                       "products_per_add": prods,
-                                      "executed_over_algorithmic_macs": round(prods * 2 * 152 * 152 / (2 * 128 * 128 + 128), 3),
-                                      "valu_frac_executed": round(rate * prods * 2 * 152 * 152 / PEAK_MAC_S, 4),
-                                      "valu_frac_survey_unit": round(rate * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4)}
+                                      "valu_macs_per_add": valu_macs,
+                                      "executed_over_algorithmic_macs": round(valu_macs / (2 * 128 * 128 + 128), 3),
+                                      "valu_frac_executed": round(rate * valu_macs / PEAK_MAC_S, 4),
+                                      "valu_frac_survey_unit": round(rate * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4),
+                                      "matrix_core": {"i8_macs_per_add": round(i8_macs),
+                                                      "frac_of_i8_dense_peak": round(rate * i8_macs * 2 / i8_peak, 4)}}
         # the same adds on Montgomery-resident rows (x R mod n^2, include/fthe.h): one product per add
         # instead of two; rows converted in/out once per chain (conversion not in this rate)
         mr = torch.empty((2 * na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
@@ -844,11 +855,17 @@ def run(a, world):
         if 2 * P >= bins:
             x = c[:bins].unsqueeze(0).expand(parties, bins, 2 * pl.n_words).contiguous()
             ho = torch.empty((bins, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
-            pl.reduce_kway_dev(x, parties, ho)
-            dev.sync()
-            ms_h = lib.fthe_last_kernel_ms(dev.ctx)
-            secondary["hist_merge_8party_1M_bins"] = {"ms": round(ms_h, 2), "ciphertexts_out": bins,
-                                                      "adds_per_s": round(bins * (parties - 1) / (ms_h * 1e-3))}
+            mts = []
+            for _ in range(3):                           # one merge: +-5% between calls on the same box
+                pl.reduce_kway_dev(x, parties, ho)
+                dev.sync()
+                mts.append(lib.fthe_last_kernel_ms(dev.ctx))
+            ms_h = sorted(mts)[1]
+            secondary["hist_merge_8party_1M_bins"] = {"ms": round(ms_h, 2), "ms_min": round(min(mts), 2),
+                                                      "ms_max": round(max(mts), 2), "ciphertexts_out": bins,
+                                                      "adds_per_s": round(bins * (parties - 1) / (ms_h * 1e-3)),
+                                                      "note": "median of 3 calls; seven launches of fthe_addb_q152 "
+                                                              "over the 2M bins (out = x0 x1, then out = out x_j)"}
             del x, ho
         # party-side node histogram on the device (hist_tree_builder.cpp:565-595): 1M instances
         # x 28 features x 255 bins, g and h planes = 55.7M member products, CSR built in HBM

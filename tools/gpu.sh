@@ -11,7 +11,7 @@
 #   pmc:W          separate PMC passes (one counter group per run, never with tracing) over workload W:
 #                    enc  the bench's encrypt at 262,144 pairs (fthe_padic_m37 + s74 tails)
 #                    add  one device-resident P-2048 add of 1M ciphertexts (s152 row I/O)
-#                    kway one 8-party merge of 262,144 bins
+#                    kway three 8-party merges of 1,048,576 bins
 #                    pub  public-key encrypt of 131,072 ciphertexts (tools/nadic_ab.py)
 #                  then: python tools/rocprof_summary.py pmc gpurun_out/TAG_pmc_W_* out.json (CPU side)
 #   opstrace       kernel trace of tools/prof_ops.py add,kway (the add / merge launch durations for pmc:add)
@@ -30,7 +30,7 @@ pmc_pass() {  # workload tag counters...
   case $w in
     enc)  cmd="python3 bench.py --pairs 262144 --steps 1 --warmup 0 --no-cpu --no-secondary";;
     add)  cmd="python3 tools/prof_ops.py --n 1048576 --ops add";;
-    kway) cmd="python3 tools/prof_ops.py --n 262144 --ops kway";;
+    kway) cmd="python3 tools/prof_ops.py --n 1048576 --ops kway";;
     pub)  cmd="python3 tools/nadic_ab.py 131072";;
     *) echo "unknown pmc workload $w"; exit 2;;
   esac

@@ -132,27 +132,36 @@ def pmc_round(tag, out):
                 d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
             wr[kn] = d
         res[w] = wr
-    # launch durations of the s152 row-I/O kernels (ops trace: add launches first, then as many
-    # kway launches); full launches = within 10% of the longest of their op
+    # launch durations from the ops trace (tools/prof_ops.py --ops add,kway): fthe_addb_q152 = one add launch
+    # over all rows, then the merge's launches (kk - 1 per merge, each over all rows); the s152 row-I/O
+    # kernel (FTHE_ADD_NO_ADDB) = add launches first, then as many kway launches, full launches within 10%
     tr = glob.glob(f"gpurun_out/{tag}_ops_trace/*kernel_trace.csv")
     if tr:
-        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-                for r in csv.DictReader(open(tr[0])) if r["Kernel_Name"] in ("fthe_montprog_s152", "fthe_addb_q152")]
-        h = len(durs) // 2
+        recs = [(r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+                for r in csv.DictReader(open(tr[0]))]
         full = lambda ds: [d for d in ds if d >= 0.9 * max(ds)] if ds else []
-        add, kway = full(durs[:h]), full(durs[h:])
-        rows = int(os.environ.get("FTHE_ROWIO_ROWS", "393216"))    # rows per full row-I/O launch
-        for w, ds, units in (("add", add, rows), ("kway", kway, rows)):
-            if ds and "fthe_montprog_s152" in res[w]:
-                k = res[w]["fthe_montprog_s152"]
+        ab = [d for kn, d in recs if kn == "fthe_addb_q152"]
+        if ab:
+            kern, add, kway = "fthe_addb_q152", ab[:1], ab[1:]
+            rows = int(os.environ.get("FTHE_OPS_ROWS", "1048576"))
+            ins_of = {"add": 3, "kway": 3}         # every launch: two rows in, one out per row
+        else:
+            durs = [d for kn, d in recs if kn == "fthe_montprog_s152"]
+            h = len(durs) // 2
+            kern, add, kway = "fthe_montprog_s152", full(durs[:h]), full(durs[h:])
+            rows = int(os.environ.get("FTHE_ROWIO_ROWS", "393216"))    # rows per full row-I/O launch
+            ins_of = {"add": 3, "kway": 9}         # add: x, y, out; kway: 8 in, 1 out
+        for w, ds in (("add", add), ("kway", kway)):
+            if ds and kern in res[w]:
+                k = res[w][kern]
                 ms = sum(ds) / len(ds)
-                k["full_chunk_launch_ms"] = round(ms, 4)
-                k["rows_out_per_launch"] = units
+                k["launch_ms"] = round(ms, 4)
+                k["launches_timed"] = len(ds)
+                k["rows_out_per_launch"] = rows
                 if "hbm_bytes_per_launch" in k:
                     k["hbm_GBps"] = round(k["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
                     k["hbm_frac_of_8TBps"] = round(k["hbm_bytes_per_launch"] / (ms * 1e-3) / 8e12, 4)
-                ins = 3 if w == "add" else 9       # rows read + written per output (add: x, y, out; kway: 8 in, 1 out)
-                k["algorithmic_bytes_per_launch"] = units * 512 * ins
+                k["algorithmic_bytes_per_launch"] = rows * 512 * ins_of[w]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
