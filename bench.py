@@ -319,8 +319,9 @@ def rank_adds(call, count, world, rank, sync):
                         "adds_per_s": round(count / med)}, world)
     slow = max(p["median_s"] for p in per)
     return {"per_rank": per, "aggregate_adds_per_s": round(world * count / slow), "adds_per_rank": count,
-            "note": "device-resident P-2048 ciphertext adds (one classical 4096-bit product per add, "
-                    "fthe_add_dev), median of 5 per rank, aggregate = ranks x adds / slowest rank"}
+            "note": "device-resident P-2048 ciphertext adds (fthe_add_dev: x y on the VALU, its Barrett "
+                    "reduction by n^2 on the matrix cores, fthe_addb_q152), median of 5 per rank, "
+                    "aggregate = ranks x adds / slowest rank"}
 
 
 def run(a, world):
