@@ -258,23 +258,68 @@ def gen_padic_mfma(name: str) -> str:
                 if "nomfma" not in AB:
                     e(f'  v_mfma_i32_32x32x32_i8 v[{G}:{G + 15}], v[{buf}:{buf + 3}], v[{XB + bo}:{XB + bo + 3}], {src_c}')
 
-    def exchange(G0x, G1x, waited=False):
-        """results -> VALU: wait out the last MFMA writing them (8-pass XDL: 11 wait states on gfx950), then
-        exchange the halves; waited: at least 30 VALU instructions already separate that MFMA from here"""
+    def consumed(prod, m):
+        """the rows (output columns rho of M-tile m) the fold reads: all of product 1; product 2 drops matrix
+        column 0 (the constant digit's) and the columns above 130"""
+        if prod == 1:
+            return set(range(32))
+        return {rho for rho in range(32) if 1 <= 32 * m + rho <= 130}
+
+    def plan(C):
+        """accumulator register rr holds row 8 (rr >> 2) + 4 h + (rr & 3) of the lane half h, i.e. output
+        column rho_a = 8 (rr >> 2) + (rr & 3) or rho_a + 4 after the exchange.  Even rr whose two rows are both
+        read (or both unread) in both halves are paired before the exchange, c_rho + 256 c_(rho+1) in 32-bit
+        arithmetic (|c| < 2^21.2: exact), so the odd register need not move; returns (paired even rr, the rr
+        to exchange)"""
+        paired, swaps = set(), []
+        for rr in range(0, 16, 2):
+            ra = 8 * (rr >> 2) + (rr & 3)
+            rhos = (ra, ra + 4)
+            if "noprepair" not in AB and all((r in C) == (r + 1 in C) for r in rhos) \
+                    and any(r in C for r in rhos):
+                paired.add(rr)
+        for rr in range(16):
+            ra = 8 * (rr >> 2) + (rr & 3)
+            if (ra in C or ra + 4 in C) and not (rr % 2 and rr - 1 in paired):
+                swaps.append(rr)
+        return paired, swaps
+
+    def exchange(G0x, G1x, waited=False, tile=None):
+        """results -> VALU: wait out the last MFMA writing them (8-pass XDL: 11 wait states on gfx950), pair
+        adjacent rows (plan), then exchange the halves of the registers still needed; waited: at least 30
+        VALU instructions already separate that MFMA from here"""
         if "nonop" not in AB and not waited:
             e('  s_nop 7')
             e('  s_nop 7')
             e('  s_nop 7')
-        for r in range(16 if "noswap" not in AB else 0):
-            e(f'  v_permlane32_swap_b32_e32 v{G0x + r}, v{G1x + r}')
+        paired, swaps = plan(consumed(*tile))
+        for rr in sorted(paired):
+            for G in (G0x, G1x):
+                e(f'  v_lshl_add_u32 v{G + rr}, v{G + rr + 1}, 8, v{G + rr}')
+        if paired:
+            e('  s_nop 1')
+        for rr in (swaps if "noswap" not in AB else []):
+            e(f'  v_permlane32_swap_b32_e32 v{G0x + rr}, v{G1x + rr}')
         e('  s_nop 1')
+
+    def tile_cols(prod, m, s_of, creg):
+        """(output column, register, pre-paired) of M-tile m in column order, after exchange()"""
+        C = consumed(prod, m)
+        paired, _ = plan(C)
+        out = []
+        for rho in sorted(C):
+            rr = (rho & 3) + 4 * (rho >> 3)
+            if rho % 2 and rr - 1 in paired:
+                continue                              # folded into rho - 1 before the exchange
+            out.append((s_of(rho), creg(rho), rho % 2 == 0 and rr in paired))
+        return out
 
     def mtile_mfmas(prod, m, ks, nxt=None):
         """one M-tile, issued and then waited for (single accumulator set)"""
         issue_tile(prod, m, ks, G0, G1)
         if nxt is not None:
             prefetch(*nxt)
-        exchange(G0, G1)
+        exchange(G0, G1, tile=(prod, m))
 
     def col_reg(rho, G0x=G0, G1x=G1):
         """register of column rho (0..31) of the M-tile after the exchange"""
@@ -305,7 +350,7 @@ def gen_padic_mfma(name: str) -> str:
                 nxt_issue = capture(lambda: prefetch(*nxt)) if nxt is not None else []
             ga, gb = sets[m % 2]
             # tiles after the first were issued inside the previous fold, whose last 40% has no MFMA
-            exchange(ga, gb, waited=separated)
+            exchange(ga, gb, waited=separated, tile=tuple(tiles[m][:2]))
             fold = capture(lambda: consume(m, lambda rho, ga=ga, gb=gb: col_reg(rho, ga, gb)))
             if "nointerleave" in AB:
                 for ins in nxt_issue + fold:
@@ -399,17 +444,19 @@ def gen_padic_mfma(name: str) -> str:
             self.pending = []
 
     def fold_columns(ch, cols):
-        """cols: [(s, reg)] of one tile in column order.  Two adjacent columns of the same chunk whose
-        shifts are sh and sh + 8 <= 24 are combined first, c_s + 256 c_(s+1) in 32-bit arithmetic (|c| <
-        2^21.2, so |sum| < 2^29.3: exact), and enter the chunk as one v_mad_i64_i32: ~2 instead of 3.5
-        64-bit multiply-adds per 28-bit chunk"""
+        """cols: [(s, reg, paired)] of one tile in column order (paired: reg already holds c_s + 256 c_(s+1),
+        formed before the exchange).  Two adjacent unpaired columns of the same chunk whose shifts are sh
+        and sh + 8 <= 24 are combined first, c_s + 256 c_(s+1) in 32-bit arithmetic (|c| < 2^21.2, so |sum| <
+        2^29.3: exact), and enter the chunk as one v_mad_i64_i32: ~2 instead of 3.5 64-bit multiply-adds per
+        28-bit chunk.  A pair whose second column lies in the next chunk enters this chunk at shift sh <= 24:
+        its bits above 28 leave through the chunk's carry, exactly."""
         i = 0
         while i < len(cols):
-            s_, r_ = cols[i]
-            if i + 1 < len(cols) and "nopair" not in AB:
-                s2_, r2_ = cols[i + 1]
+            s_, r_, pr_ = cols[i]
+            if not pr_ and i + 1 < len(cols) and "nopair" not in AB:
+                s2_, r2_, pr2_ = cols[i + 1]
                 t1, t2 = (8 * s_ - ch.base) // B, (8 * s2_ - ch.base) // B
-                if s2_ == s_ + 1 and t1 == t2 and 8 * s_ - ch.base - B * t1 <= 16:
+                if not pr2_ and s2_ == s_ + 1 and t1 == t2 and 8 * s_ - ch.base - B * t1 <= 16:
                     e(f'  v_lshl_add_u32 {r_}, {r2_}, 8, {r_}')
                     ch.column(s_, r_)
                     i += 2
@@ -435,7 +482,7 @@ def gen_padic_mfma(name: str) -> str:
         ch = Chunks(QBIT, (8 * S1_LO - QBIT) // B, 39, q3out, neg=False)
 
         def consume(m, creg):
-            fold_columns(ch, [(S1_LO + 32 * m + rho, creg(rho)) for rho in range(32)])
+            fold_columns(ch, tile_cols(1, m, lambda rho: S1_LO + 32 * m + rho, creg))
         run_tiles(P1_TILES, consume, P2_TILES[0], dbuf, setb=setb)
         ch.finish()
         if clamp:                                  # final carry = 0, or -1 when q1 = 0 (q3 = -1 -> 0)
@@ -459,7 +506,7 @@ def gen_padic_mfma(name: str) -> str:
         ch = Chunks(8, 0, K - 1, rout, neg=True, inits=Tl[:K], nocarry_last=True)
 
         def consume(m, creg):
-            fold_columns(ch, [(32 * m + rho, creg(rho)) for rho in range(32) if 1 <= 32 * m + rho <= 130])
+            fold_columns(ch, tile_cols(2, m, lambda rho: 32 * m + rho, creg))
         # dbuf: the caller's last use of q3 runs while tile 0 (first accumulator set) is in the matrix core;
         # the second set (q3's registers) is first written by tile 1
         run_tiles(P2_TILES, consume, P1_TILES[0] if nxt_p1 else None, dbuf,
