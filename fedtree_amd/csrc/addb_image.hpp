@@ -9,7 +9,8 @@
 //   corrections (int32 per output column, the MFMAs' srcC): product 1 column s = 512 + i:
 //     128 sum_{k < 516} mu'[s - k] (-2 at s = 515: the -2^4121 truncation bias), product 2 column s:
 //     128 sum_{k < 512} N'[s - k];
-//   then N as 128 little-endian dwords (the kernel's final conditional subtractions).
+//   then N as 128 little-endian dwords (the kernel's final conditional subtractions), then the integer 1 as a
+//   128-dword row (the operand of a gathered index < 0).
 // Layout constants: gen/addb_layout.h, written by fedtree_amd/build.py from gen_addb.py.
 #pragma once
 #include <gmp.h>
@@ -82,6 +83,7 @@ inline bool build(const mpz_t n, std::vector<uint8_t> &img) {
         }
         size_t cnt = 0;
         mpz_export(img.data() + kAddbNOff, &cnt, -1, 4, 0, 0, N);
+        img[kAddbOneOff] = 1;                                          // the row 1 (gathered index < 0)
     }
     mpz_clears(N, mu, nullptr);
     return ok;

@@ -2953,16 +2953,28 @@ extern "C" int fthe_decrypt_short_dev(fthe_key *k, fthe_ctx *c, const uint32_t *
 // ---------------------------------------------------------------------------
 // Add / k-way product / scalar mul (mod n^2)
 
-// out = x y mod n^2 for count rows on fthe_addb_q152 (gen_addb.py): 16 rows per wave, 12 waves per workgroup
+// out = x y mod n^2 for count rows on fthe_addb_q152 (gen_addb.py): 16 rows per wave, 12 waves per workgroup.
+// xi / yi (device int64 lists of count entries, nullable): operand row g is row xi[g] of x (xi[g] < 0: the
+// integer 1), the gathered products of the histogram scatter and segment sums.
 static int launch_addb(fthe_ctx *c, const fthe_key *k, const uint32_t *x, const uint32_t *y, uint32_t *out,
-                       size_t count) {
+                       size_t count, const int64_t *xi = nullptr, const int64_t *yi = nullptr) {
+    // the kernel addresses rows by 32-bit byte offsets (row * 512 < 2^32): launches of at most 4M rows
+    constexpr size_t kMaxRows = (size_t)1 << 22;
+    const size_t cw = 2 * (size_t)k->n_words;
+    while (count > kMaxRows) {
+        int rc = launch_addb(c, k, x, y, out, kMaxRows, xi, yi);
+        if (rc) return rc;
+        if (xi) xi += kMaxRows; else x += kMaxRows * cw;
+        if (yi) yi += kMaxRows; else y += kMaxRows * cw;
+        out += kMaxRows * cw;
+        count -= kMaxRows;
+    }
     if (count == 0) return FTHE_OK;
-    if (count > 0xFFFFFFFFu / 2) return FTHE_ERR_ARG;
     // persistent workgroups, one per CU at most: each wave sweeps batches of 16 rows across the grid
     const unsigned blocks = (unsigned)std::min<size_t>((count + kAddbPerWg - 1) / kAddbPerWg, (size_t)c->n_cu);
-    struct { const void *x, *y; void *o; const void *kc; uint32_t count, nwg; } args = {x, y, out, k->d_addb,
-                                                                                      (uint32_t)count, blocks};
-    static_assert(sizeof(args) == 40, "kernarg layout of gen_addb.py");
+    struct { const void *x, *y; void *o; const void *kc; uint32_t count, nwg; const void *xi, *yi; } args = {
+        x, y, out, k->d_addb, (uint32_t)count, blocks, xi, yi};
+    static_assert(sizeof(args) == 56, "kernarg layout of gen_addb.py");
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     if (hipModuleLaunchKernel(c->fn_addb, blocks, 1, 1, 64 * kAddbWaves, 1, 1, 0, c->stream, nullptr, cfg) != hipSuccess)
@@ -3212,6 +3224,15 @@ struct GatherProd {
     int run_dev(const uint32_t *src, const int64_t *gidx, size_t G, uint32_t *dst) {
         const int cw = 2 * k->n_words, S = Lc.S, L = Lc.L;
         int rc;
+        if (k->d_addb && c->fn_addb && dst != src) {
+            // 2048-bit n: K - 1 matrix-core Barrett add launches over all G rows, gathered operands
+            // (dst = src[i_0] src[i_1], then dst = dst src[i_j]; an index < 0 is the integer 1)
+            if ((rc = launch_addb(c, k, src, src, dst, G, gidx, gidx + G))) return rc;
+            for (int j = 2; j < K; j++)
+                if ((rc = launch_addb(c, k, dst, src, dst, G, nullptr, gidx + (size_t)j * G))) return rc;
+            Lc.mm += (double)G * (K - 1);
+            return FTHE_OK;
+        }
         for (size_t off = 0; off < G; off += L) {
             size_t cnt = std::min((size_t)L, G - off);
             Lc.live = cnt;

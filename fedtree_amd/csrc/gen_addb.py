@@ -30,8 +30,10 @@ per wave, 12 waves per workgroup (one workgroup per CU: its LDS holds the key's 
      conditional subtractions of N (dwords from the key's context) make it canonical; rows are stored.
 
 kernarg: 0 u64 x rows, 8 u64 y rows, 16 u64 out rows, 24 u64 kctx, 32 u32 count, 36 u32 workgroups launched
-(persistent: each wave takes batches of 16 ciphertexts wg*12 + wave, + 12 * workgroups, ...).
-kctx: the LDS image (IMG_BYTES: mu copies, N copies, corrections), then N as 128 dwords.
+(persistent: each wave takes batches of 16 ciphertexts wg*12 + wave, + 12 * workgroups, ...), 40 u64 x index
+list, 48 u64 y index list (0: row g is operand row g; else operand row g is row idx[g] of the operand array,
+idx[g] < 0 the integer 1: the gathered products of the histogram scatter / segment sums).
+kctx: the LDS image (IMG_BYTES: mu copies, N copies, corrections), then N as 128 dwords, then the row 1.
 """
 import os
 import sys
@@ -53,7 +55,8 @@ CORR1_OFF = A2_OFF + 16 * COPY
 CORR2_OFF = CORR1_OFF + TILES1 * 64
 IMG_BYTES = CORR2_OFF + TILES2 * 64          # 29,824
 N_OFF = IMG_BYTES                            # N dwords in kctx (not copied to LDS)
-KCTX_BYTES = N_OFF + 512
+ONE_OFF = N_OFF + 512                        # the integer 1 as a row (gathered index < 0)
+KCTX_BYTES = ONE_OFF + 512
 WAVE_AREA = 10496                            # A column (152 x 68) / q staging (16 x 656) / groups (16 x 296)
 LDS_WAVES = IMG_BYTES
 LDS_BYTES = LDS_WAVES + WAVES * WAVE_AREA    # 153,856
@@ -76,7 +79,7 @@ def layout_header():
     vals = dict(kAddbMuShift=MU_SHIFT, kAddbNd1=515, kAddbNd2=513, kAddbKctxBytes=KCTX_BYTES, kAddbA1Off=A1_OFF,
                 kAddbA2Off=A2_OFF, kAddbS1Base=S1_BASE, kAddbKO1=KO1, kAddbKO2=KO2, kAddbCopy=COPY,
                 kAddbTiles1=TILES1, kAddbTiles2=TILES2, kAddbNq1=NQ1, kAddbNq3=NQ3, kAddbBiasCol=BIAS_COL,
-                kAddbBiasDigit=BIAS_DIGIT, kAddbCorr1Off=CORR1_OFF, kAddbCorr2Off=CORR2_OFF, kAddbNOff=N_OFF,
+                kAddbBiasDigit=BIAS_DIGIT, kAddbCorr1Off=CORR1_OFF, kAddbCorr2Off=CORR2_OFF, kAddbNOff=N_OFF, kAddbOneOff=ONE_OFF,
                 kAddbImgBytes=IMG_BYTES, kAddbWaves=WAVES, kAddbPerWg=WAVES * CT_PER_WAVE, kAddbLdsBytes=LDS_BYTES)
     lines = ["// generated by fedtree_amd/build.py from gen_addb.py -- layout of fthe_addb_q152", "#pragma once"]
     lines += [f"constexpr int {k} = {v};" for k, v in vals.items()]
@@ -151,7 +154,8 @@ def gen_addb(name: str) -> str:
     # s[0:1] kernarg, s2 wg id, s[4:5] x rows, s[6:7] y rows, s[8:9] out rows, s[10:11] kctx, s12 count,
     # s13 first ciphertext of this wave, s[14:15] scratch, s[16:17] saved exec, s18 loop counter,
     # lane masks: s[20:21] quad lane 3, s[22:23] lane 0, s[24:25] lane 1, s[26:27] lane 2,
-    # s[28:29] live lanes, s30 = 256, s31 = 65536, s32 = 2^24, s33 = 0x80808080
+    # s[28:29] live lanes, s30 = 256, s31 = 65536, s32 = 2^24, s33 = 0x80808080, s[34:35] x index list,
+    # s[36:37] y index list (0: direct rows), s[38:39] carry scratch of the gathered addresses
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
     LIVE = "s[28:29]"
     NSGPR = 40
@@ -168,6 +172,8 @@ def gen_addb(name: str) -> str:
     e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
     e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
     e('  s_load_dword s12, s[0:1], 0x20')
+    e('  s_load_dwordx2 s[34:35], s[0:1], 0x28')
+    e('  s_load_dwordx2 s[36:37], s[0:1], 0x30')
     for j, pat in ((3, 0x88888888), (0, 0x11111111), (1, 0x22222222), (2, 0x44444444)):
         lo, hi = LANE_MASK[j][2:-1].split(':')
         e(f'  s_mov_b32 s{lo}, {hex(pat)}')
@@ -262,21 +268,57 @@ def gen_addb(name: str) -> str:
     # ---- row I/O helpers (gen_montprog.gen_quad's LOADW / STOREW, for this register plan) ---------------
     W0 = TB                                       # 33 loaded row words (ring area, free outside the product)
 
-    def load_row_limbs(sbase, dst):
+    GA = 146                                      # gathered row address v[146:147], one row v[148:149], t v150
+    #                                               (the group read buffer, free while rows load)
+
+    def load_row_limbs(sbase, dst, sidx):
+        """this lane's quarter of operand row g (or of row idx[g] when the index list sidx is not null; idx < 0:
+        the integer 1 from kctx) -> 38 limbs dst(k)"""
+        lab = f'.Lrow{len(o)}'
         e(f'  s_mov_b64 exec, {LIVE}')
+        e(f'  s_cmp_eq_u64 {sidx}, 0')
+        e(f'  s_cbranch_scc1 {lab}_direct')
+        e(f'  v_lshrrev_b32_e32 v{GA + 4}, 9, v{V_ROW}')               # g
+        e(f'  v_lshlrev_b32_e32 v{GA + 4}, 3, v{GA + 4}')
+        e(f'  global_load_dwordx2 v[{GA}:{GA + 1}], v{GA + 4}, {sidx}')
+        e(f'  v_mov_b32_e32 v{GA + 2}, s10')
+        e(f'  v_mov_b32_e32 v{GA + 3}, s11')
+        e(f'  v_add_co_u32_e32 v{GA + 2}, vcc, {hex(ONE_OFF)}, v{GA + 2}')
+        e(f'  v_addc_co_u32_e32 v{GA + 3}, vcc, 0, v{GA + 3}, vcc')     # kctx + ONE_OFF
+        e('  s_waitcnt vmcnt(0)')
+        e(f'  v_cmp_gt_i64_e64 s[38:39], 0, v[{GA}:{GA + 1}]')          # idx < 0: the row 1
+        e(f'  v_lshlrev_b64 v[{GA}:{GA + 1}], 9, v[{GA}:{GA + 1}]')
+        lo, hi = sbase[2:-1].split(':')
+        e(f'  v_mov_b32_e32 v{GA + 4}, s{hi}')
+        e(f'  v_add_co_u32_e32 v{GA}, vcc, s{lo}, v{GA}')
+        e(f'  v_addc_co_u32_e32 v{GA + 1}, vcc, v{GA + 4}, v{GA + 1}, vcc')
+        e(f'  v_cndmask_b32_e64 v{GA}, v{GA}, v{GA + 2}, s[38:39]')
+        e(f'  v_cndmask_b32_e64 v{GA + 1}, v{GA + 1}, v{GA + 3}, s[38:39]')
+        e(f'  v_and_b32_e32 v{GA + 4}, 0x180, v{V_ROW}')               # + 128 j
+        e(f'  v_add_co_u32_e32 v{GA}, vcc, v{GA}, v{GA + 4}')
+        e(f'  v_addc_co_u32_e32 v{GA + 1}, vcc, 0, v{GA + 1}, vcc')
+        for i in range(8):
+            e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v[{GA}:{GA + 1}], off offset:{16 * i}')
+        e(f'  s_and_b64 exec, {LIVE}, s[20:21]')
+        e(f'  global_load_dword v{W0 + 32}, v[{GA}:{GA + 1}], off offset:0x7c')
+        e(f'  s_andn2_b64 exec, {LIVE}, s[20:21]')
+        e(f'  global_load_dword v{W0 + 32}, v[{GA}:{GA + 1}], off offset:0x80')
+        e(f'  s_mov_b64 exec, {LIVE}')
+        e(f'  s_branch {lab}_loaded')
+        e(f'{lab}_direct:')
         for i in range(8):
             e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v{V_ROW}, {sbase} offset:{16 * i}')
         e(f'  v_add_u32_e32 v{V_TMP}, 0x80, v{V_ROW}')
         e(f'  v_add_u32_e32 v{V_TMP + 1}, 0x7c, v{V_ROW}')
         e(f'  v_cndmask_b32_e64 v{V_TMP}, v{V_TMP}, v{V_TMP + 1}, s[20:21]')
         e(f'  global_load_dword v{W0 + 32}, v{V_TMP}, {sbase}')
+        e(f'{lab}_loaded:')
         e('  s_waitcnt vmcnt(0)')
         e('  s_not_b64 exec, exec')                                      # dead lanes: zero operand
-        lab = f'.Llive{len(o)}'
-        e(f'  s_cbranch_execz {lab}')                                    # (only in a partial batch)
+        e(f'  s_cbranch_execz {lab}_live')                               # (only in a partial batch)
         for i in range(33):
             e(f'  v_mov_b32_e32 v{W0 + i}, 0')
-        e(f'{lab}:')
+        e(f'{lab}_live:')
         e('  s_mov_b64 exec, -1')
         e(f'  v_cndmask_b32_e64 v{W0 + 32}, v{W0 + 32}, 0, s[20:21]')
         for i in range(32):
@@ -335,8 +377,8 @@ def gen_addb(name: str) -> str:
 
     e('// @phase load')
     # ---- 1. x -> X limbs; y -> limbs -> the wave's A column (rows 38j + k of column c) ------------------
-    load_row_limbs('s[4:5]', X)
-    load_row_limbs('s[6:7]', lambda k: f"v{TB + 40 + k}")              # y limbs (ring area above W0)
+    load_row_limbs('s[4:5]', X, 's[34:35]')
+    load_row_limbs('s[6:7]', lambda k: f"v{TB + 40 + k}", 's[36:37]')  # y limbs (ring area above W0)
     for k in range(Q):
         e(f'  ds_write_b32 v{V_ZR}, v{TB + 40 + k} offset:{k * RB}')
     e('  s_waitcnt lgkmcnt(0)')
@@ -635,7 +677,7 @@ def descriptor(name, lds_bytes, nvgpr, nsgpr):
     e(f'.amdhsa_kernel {name}')
     e(f'  .amdhsa_group_segment_fixed_size {lds_bytes}')
     e('  .amdhsa_private_segment_fixed_size 0')
-    e('  .amdhsa_kernarg_size 40')
+    e('  .amdhsa_kernarg_size 56')
     e('  .amdhsa_user_sgpr_count 2')
     e('  .amdhsa_user_sgpr_kernarg_segment_ptr 1')
     e('  .amdhsa_system_sgpr_workgroup_id_x 1')
@@ -653,7 +695,8 @@ def descriptor(name, lds_bytes, nvgpr, nsgpr):
     e('amdhsa.kernels:')
     e('  - .args:')
     for off_, sz, kind in ((0, 8, 'global_buffer'), (8, 8, 'global_buffer'), (16, 8, 'global_buffer'),
-                           (24, 8, 'global_buffer'), (32, 4, 'by_value'), (36, 4, 'by_value')):
+                           (24, 8, 'global_buffer'), (32, 4, 'by_value'), (36, 4, 'by_value'),
+                           (40, 8, 'global_buffer'), (48, 8, 'global_buffer')):
         e(f'      - .offset: {off_}')
         e(f'        .size: {sz}')
         e(f'        .value_kind: {kind}')
@@ -661,7 +704,7 @@ def descriptor(name, lds_bytes, nvgpr, nsgpr):
             e('        .address_space: global')
     e(f'    .group_segment_fixed_size: {lds_bytes}')
     e('    .kernarg_segment_align: 8')
-    e('    .kernarg_segment_size: 40')
+    e('    .kernarg_segment_size: 56')
     e(f'    .max_flat_workgroup_size: {64 * WAVES}')
     e(f'    .name: {name}')
     e('    .private_segment_fixed_size: 0')

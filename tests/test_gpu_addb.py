@@ -90,3 +90,26 @@ def test_addb_full_chunk_aliased_and_host(keys):
     pl.decrypt_u64_dev(x, low)
     dev.sync()
     assert torch.equal(low, m[:cnt] + m[cnt:])
+
+
+def test_addb_beyond_one_launch(keys):
+    """more rows than one launch addresses (4M: row offsets are 32-bit in the kernel): the launches split,
+    and the rows around each split equal the classical product's"""
+    import torch
+    dev, pl, ref = keys
+    cw = 2 * pl.n_words
+    cnt = (1 << 22) + 1000
+    m = torch.randint(0, 2**62, (2 * 8192,), dtype=torch.int64, device="cuda")
+    c = torch.empty((2 * 8192, cw), dtype=torch.int32, device="cuda")
+    pl.encrypt_u64_dev(m, c, seed=11)
+    reps = (cnt + 8191) // 8192
+    a = c[:8192].repeat(reps, 1)[:cnt]
+    b = c[8192:].roll(1, 0).repeat(reps, 1)[:cnt]
+    o = torch.empty_like(a)
+    pl.add_dev(a, b, o)
+    sl = torch.cat([torch.arange(0, 4096), torch.arange((1 << 22) - 4096, cnt)]).cuda()
+    want = torch.empty((len(sl), cw), dtype=torch.int32, device="cuda")
+    ref.add_dev(a[sl].contiguous(), b[sl].contiguous(), want)
+    dev.sync()
+    assert torch.equal(o[sl], want)
+    del a, b, o

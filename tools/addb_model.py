@@ -217,6 +217,7 @@ def addb_image(N):
         for i, c in enumerate(corr):
             img[off + 4 * i:off + 4 * i + 4] = (c & 0xFFFFFFFF).to_bytes(4, "little")
     img[ga.N_OFF:ga.N_OFF + 512] = N.to_bytes(512, "little")
+    img[ga.ONE_OFF] = 1                               # the row 1: a gathered index < 0
     return bytes(img)
 
 

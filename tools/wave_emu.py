@@ -228,6 +228,14 @@ class Wave:
             self.scc = int(g(a[0]) != g(a[1]))
         elif op == 's_cmp_eq_u32':
             self.scc = int(g(a[0]) == g(a[1]))
+        elif op == 's_cmp_eq_u64':
+            self.scc = int(g(a[0], 2) == g(a[1], 2))
+        elif op == 's_and_b64':
+            self.sset(a[0], g(a[1], 2) & g(a[2], 2))
+            self.scc = int(self.sget(a[0], 2) != 0)
+        elif op == 's_andn2_b64':
+            self.sset(a[0], g(a[1], 2) & ~g(a[2], 2) & M64)
+            self.scc = int(self.sget(a[0], 2) != 0)
         else:
             raise NotImplementedError(op)
 
@@ -259,7 +267,8 @@ class Wave:
         return val.to_bytes(4 * n, 'little')
 
     def glob(self, op, a):
-        width = {'global_load_dword': 4, 'global_load_dwordx4': 16, 'global_store_dwordx4': 16}[op]
+        width = {'global_load_dword': 4, 'global_load_dwordx2': 8, 'global_load_dwordx4': 16,
+                 'global_store_dwordx4': 16}[op]
         off = 0
         for t in a[3:]:
             if t.startswith('offset:'):
@@ -267,9 +276,10 @@ class Wave:
         store = op.startswith('global_store')
         vaddr, sbase = a[1] if not store else a[0], a[2]
         data_tok = a[0] if not store else a[1]
-        base = self.sget(sbase, 2)
+        flat = sbase == 'off'                  # 64-bit VGPR address, no SGPR base
+        base = 0 if flat else self.sget(sbase, 2)
         for l in self.lanes():
-            addr = base + self.vget(l, vaddr) + off
+            addr = (self.vget(l, vaddr) if flat else base + self.vget(l, vaddr)) + off
             if store:
                 self.mem.write(addr, width, int.from_bytes(self.vq(l, data_tok), 'little'))
             else:
@@ -322,6 +332,21 @@ class Wave:
                 self.vset(l, a[0], r & M32)
                 nv = (nv | (1 << l)) if r < 0 else (nv & ~(1 << l))
             self.vcc = nv
+            return
+        if op in ('v_add_co_u32_e32', 'v_addc_co_u32_e32'):
+            nv = self.vcc
+            for l in lanes:
+                ci = (self.vcc >> l) & 1 if op == 'v_addc_co_u32_e32' else 0
+                r = g(l, a[2]) + g(l, a[3]) + ci
+                self.vset(l, a[0], r & M32)
+                nv = (nv | (1 << l)) if r >> 32 else (nv & ~(1 << l))
+            self.vcc = nv
+            return
+        if op == 'v_cmp_gt_i64_e64':
+            nv = 0
+            for l in lanes:
+                nv |= int(s64(g(l, a[1], 2)) > s64(g(l, a[2], 2))) << l
+            self.sset(a[0], nv)
             return
         if op == 'v_cmp_gt_u32_e32':
             nv = 0
@@ -385,6 +410,8 @@ class Wave:
                 r = (((g(l, a[1]) << 32) | g(l, a[2])) >> (g(l, a[3]) & 31))
             elif op == 'v_lshl_add_u64':
                 r = (g(l, a[1], 2) << (g(l, a[2]) & 63)) + g(l, a[3], 2)
+            elif op == 'v_lshlrev_b64':
+                r = g(l, a[2], 2) << (g(l, a[1]) & 63)
             elif op == 'v_lshrrev_b64':
                 r = g(l, a[2], 2) >> (g(l, a[1]) & 63)
             elif op == 'v_ashrrev_i64':
@@ -445,7 +472,8 @@ def selftest(ntests=16, count0=None):
     import addb_model as am
     rng = random.Random(5)
     asm = ga.gen_addb('fthe_addb_q152')
-    for trial, n in enumerate((am.rand_n(rng), (1 << 2047) + 1)):
+    for trial, n in enumerate((am.rand_n(rng), (1 << 2047) + 1, am.rand_n(rng))):
+        gather = trial == 2                           # operand rows through index lists (-1: the integer 1)
         N = n * n
         img = am.addb_image(N)
         assert len(img) == ga.KCTX_BYTES
@@ -461,18 +489,31 @@ def selftest(ntests=16, count0=None):
             count = count0 - (3 if trial else 0)
         mem = Mem()
         XB, YB, OB, KB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000, 0x50000000
+        XI, YI = 0x60000000, 0x70000000
+        if gather:                                    # out[g] = xs[xi[g]] ys[yi[g]], index < 0 -> 1
+            xi = [rng.randrange(-1, ntests) for _ in range(ntests)]
+            yi = [rng.randrange(-1, ntests) for _ in range(ntests)]
+            xi[0], yi[1] = -1, -1
+            mem.alloc(b''.join(v.to_bytes(8, 'little', signed=True) for v in xi), XI)
+            mem.alloc(b''.join(v.to_bytes(8, 'little', signed=True) for v in yi), YI)
         mem.alloc(b''.join(x.to_bytes(512, 'little') for x in xs), XB)
         mem.alloc(b''.join(y.to_bytes(512, 'little') for y in ys), YB)
         mem.alloc(bytes(512 * ntests), OB)
         mem.alloc(img, KB)
         karg = XB.to_bytes(8, 'little') + YB.to_bytes(8, 'little') + OB.to_bytes(8, 'little') + \
-            KB.to_bytes(8, 'little') + count.to_bytes(4, 'little') + (1).to_bytes(4, 'little')
+            KB.to_bytes(8, 'little') + count.to_bytes(4, 'little') + (1).to_bytes(4, 'little') + \
+            ((XI.to_bytes(8, 'little') + YI.to_bytes(8, 'little')) if gather else bytes(16))
         mem.alloc(karg, KA)
         steps = run_workgroup(asm, ga.LDS_BYTES, ga.WAVES, mem, KA, 0, 168)
         bad = 0
         for i in range(ntests):
             got = mem.read(OB + 512 * i, 512)
-            want = xs[i] * ys[i] % N if i < count else 0
+            if gather:
+                xv = xs[xi[i]] if xi[i] >= 0 else 1
+                yv = ys[yi[i]] if yi[i] >= 0 else 1
+            else:
+                xv, yv = xs[i], ys[i]
+            want = xv * yv % N if i < count else 0
             if got != want:
                 bad += 1
                 print(f"  ciphertext {i}: mismatch")
