@@ -268,68 +268,67 @@ def gen_addb(name: str) -> str:
     # ---- row I/O helpers (gen_montprog.gen_quad's LOADW / STOREW, for this register plan) ---------------
     W0 = TB                                       # 33 loaded row words (ring area, free outside the product)
 
-    GA = 146                                      # gathered row address v[146:147], one row v[148:149], t v150
-    #                                               (the group read buffer, free while rows load)
+    GA = 146                                      # gathered row addresses v[146:147] (x), v[148:149] (y), the
+    #                                               row 1 v[150:151], t v152 (the group read buffer, free here)
+    WY = TB + 40                                  # y row words v86..v118 (ring area, free outside the product)
 
-    def load_row_limbs(sbase, dst, sidx):
-        """this lane's quarter of operand row g (or of row idx[g] when the index list sidx is not null; idx < 0:
-        the integer 1 from kctx) -> 38 limbs dst(k)"""
+    def issue_row(sbase, sidx, W, ga):
+        """load this lane's 33 words of operand row g (or of row idx[g] when the index list sidx is not null;
+        idx < 0: the integer 1 from kctx) into W(0..32); the caller waits"""
         lab = f'.Lrow{len(o)}'
         e(f'  s_mov_b64 exec, {LIVE}')
         e(f'  s_cmp_eq_u64 {sidx}, 0')
         e(f'  s_cbranch_scc1 {lab}_direct')
-        e(f'  v_lshrrev_b32_e32 v{GA + 4}, 9, v{V_ROW}')               # g
-        e(f'  v_lshlrev_b32_e32 v{GA + 4}, 3, v{GA + 4}')
-        e(f'  global_load_dwordx2 v[{GA}:{GA + 1}], v{GA + 4}, {sidx}')
-        e(f'  v_mov_b32_e32 v{GA + 2}, s10')
-        e(f'  v_mov_b32_e32 v{GA + 3}, s11')
-        e(f'  v_add_co_u32_e32 v{GA + 2}, vcc, {hex(ONE_OFF)}, v{GA + 2}')
-        e(f'  v_addc_co_u32_e32 v{GA + 3}, vcc, 0, v{GA + 3}, vcc')     # kctx + ONE_OFF
+        t = GA + 6
+        e(f'  v_lshrrev_b32_e32 v{t}, 9, v{V_ROW}')                     # g
+        e(f'  v_lshlrev_b32_e32 v{t}, 3, v{t}')
+        e(f'  global_load_dwordx2 v[{ga}:{ga + 1}], v{t}, {sidx}')
+        e(f'  v_mov_b32_e32 v{GA + 4}, s10')
+        e(f'  v_mov_b32_e32 v{GA + 5}, s11')
+        e(f'  v_add_co_u32_e32 v{GA + 4}, vcc, {hex(ONE_OFF)}, v{GA + 4}')
+        e(f'  v_addc_co_u32_e32 v{GA + 5}, vcc, 0, v{GA + 5}, vcc')     # kctx + ONE_OFF
         e('  s_waitcnt vmcnt(0)')
-        e(f'  v_cmp_gt_i64_e64 s[38:39], 0, v[{GA}:{GA + 1}]')          # idx < 0: the row 1
-        e(f'  v_lshlrev_b64 v[{GA}:{GA + 1}], 9, v[{GA}:{GA + 1}]')
+        e(f'  v_cmp_gt_i64_e64 s[38:39], 0, v[{ga}:{ga + 1}]')          # idx < 0: the row 1
+        e(f'  v_lshlrev_b64 v[{ga}:{ga + 1}], 9, v[{ga}:{ga + 1}]')
         lo, hi = sbase[2:-1].split(':')
-        e(f'  v_mov_b32_e32 v{GA + 4}, s{hi}')
-        e(f'  v_add_co_u32_e32 v{GA}, vcc, s{lo}, v{GA}')
-        e(f'  v_addc_co_u32_e32 v{GA + 1}, vcc, v{GA + 4}, v{GA + 1}, vcc')
-        e(f'  v_cndmask_b32_e64 v{GA}, v{GA}, v{GA + 2}, s[38:39]')
-        e(f'  v_cndmask_b32_e64 v{GA + 1}, v{GA + 1}, v{GA + 3}, s[38:39]')
-        e(f'  v_and_b32_e32 v{GA + 4}, 0x180, v{V_ROW}')               # + 128 j
-        e(f'  v_add_co_u32_e32 v{GA}, vcc, v{GA}, v{GA + 4}')
-        e(f'  v_addc_co_u32_e32 v{GA + 1}, vcc, 0, v{GA + 1}, vcc')
+        e(f'  v_mov_b32_e32 v{t}, s{hi}')
+        e(f'  v_add_co_u32_e32 v{ga}, vcc, s{lo}, v{ga}')
+        e(f'  v_addc_co_u32_e32 v{ga + 1}, vcc, v{t}, v{ga + 1}, vcc')
+        e(f'  v_cndmask_b32_e64 v{ga}, v{ga}, v{GA + 4}, s[38:39]')
+        e(f'  v_cndmask_b32_e64 v{ga + 1}, v{ga + 1}, v{GA + 5}, s[38:39]')
+        e(f'  v_and_b32_e32 v{t}, 0x180, v{V_ROW}')                    # + 128 j
+        e(f'  v_add_co_u32_e32 v{ga}, vcc, v{ga}, v{t}')
+        e(f'  v_addc_co_u32_e32 v{ga + 1}, vcc, 0, v{ga + 1}, vcc')
         for i in range(8):
-            e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v[{GA}:{GA + 1}], off offset:{16 * i}')
+            e(f'  global_load_dwordx4 v[{W + 4 * i}:{W + 4 * i + 3}], v[{ga}:{ga + 1}], off offset:{16 * i}')
         e(f'  s_and_b64 exec, {LIVE}, s[20:21]')
-        e(f'  global_load_dword v{W0 + 32}, v[{GA}:{GA + 1}], off offset:0x7c')
+        e(f'  global_load_dword v{W + 32}, v[{ga}:{ga + 1}], off offset:0x7c')
         e(f'  s_andn2_b64 exec, {LIVE}, s[20:21]')
-        e(f'  global_load_dword v{W0 + 32}, v[{GA}:{GA + 1}], off offset:0x80')
+        e(f'  global_load_dword v{W + 32}, v[{ga}:{ga + 1}], off offset:0x80')
         e(f'  s_mov_b64 exec, {LIVE}')
-        e(f'  s_branch {lab}_loaded')
+        e(f'  s_branch {lab}_issued')
         e(f'{lab}_direct:')
         for i in range(8):
-            e(f'  global_load_dwordx4 v[{W0 + 4 * i}:{W0 + 4 * i + 3}], v{V_ROW}, {sbase} offset:{16 * i}')
+            e(f'  global_load_dwordx4 v[{W + 4 * i}:{W + 4 * i + 3}], v{V_ROW}, {sbase} offset:{16 * i}')
         e(f'  v_add_u32_e32 v{V_TMP}, 0x80, v{V_ROW}')
         e(f'  v_add_u32_e32 v{V_TMP + 1}, 0x7c, v{V_ROW}')
         e(f'  v_cndmask_b32_e64 v{V_TMP}, v{V_TMP}, v{V_TMP + 1}, s[20:21]')
-        e(f'  global_load_dword v{W0 + 32}, v{V_TMP}, {sbase}')
-        e(f'{lab}_loaded:')
-        e('  s_waitcnt vmcnt(0)')
-        e('  s_not_b64 exec, exec')                                      # dead lanes: zero operand
-        e(f'  s_cbranch_execz {lab}_live')                               # (only in a partial batch)
-        for i in range(33):
-            e(f'  v_mov_b32_e32 v{W0 + i}, 0')
-        e(f'{lab}_live:')
-        e('  s_mov_b64 exec, -1')
-        e(f'  v_cndmask_b32_e64 v{W0 + 32}, v{W0 + 32}, 0, s[20:21]')
+        e(f'  global_load_dword v{W + 32}, v{V_TMP}, {sbase}')
+        e(f'{lab}_issued:')
+
+    def convert_row(W, dst):
+        """W(0..32) (this lane's words of the row, dead lanes zero) -> 38 limbs dst(k): the 2j-bit funnel
+        shift of the lane's quarter, then 27-bit fields (the row I/O of gen_montprog.gen_quad)"""
+        e(f'  v_cndmask_b32_e64 v{W + 32}, v{W + 32}, 0, s[20:21]')
         for i in range(32):
-            e(f'  v_alignbit_b32 v{W0 + i}, v{W0 + i + 1}, v{W0 + i}, v{V_SH}')
-        e(f'  v_lshrrev_b32_e32 v{W0 + 32}, v{V_SH}, v{W0 + 32}')
+            e(f'  v_alignbit_b32 v{W + i}, v{W + i + 1}, v{W + i}, v{V_SH}')
+        e(f'  v_lshrrev_b32_e32 v{W + 32}, v{V_SH}, v{W + 32}')
         for jj in range(Q):
             a, sh = (B * jj) >> 5, (B * jj) & 31
             if sh + B <= 32:
-                e(f'  v_bfe_u32 {dst(jj)}, v{W0 + a}, {sh}, {B}')
+                e(f'  v_bfe_u32 {dst(jj)}, v{W + a}, {sh}, {B}')
             else:
-                e(f'  v_alignbit_b32 {dst(jj)}, v{W0 + a + 1}, v{W0 + a}, {sh}')
+                e(f'  v_alignbit_b32 {dst(jj)}, v{W + a + 1}, v{W + a}, {sh}')
                 e(f'  v_and_b32_e32 {dst(jj)}, {hex(MASK)}, {dst(jj)}')
 
     def limbs_to_words(src, U, t1, bo):
@@ -377,10 +376,21 @@ def gen_addb(name: str) -> str:
 
     e('// @phase load')
     # ---- 1. x -> X limbs; y -> limbs -> the wave's A column (rows 38j + k of column c) ------------------
-    load_row_limbs('s[4:5]', X, 's[34:35]')
-    load_row_limbs('s[6:7]', lambda k: f"v{TB + 40 + k}", 's[36:37]')  # y limbs (ring area above W0)
+    # both rows in flight at once (one memory latency per batch), then y's limbs (via X) to the A column
+    issue_row('s[4:5]', 's[34:35]', W0, GA)
+    issue_row('s[6:7]', 's[36:37]', WY, GA + 2)
+    e('  s_waitcnt vmcnt(0)')
+    e('  s_not_b64 exec, exec')                                          # dead lanes: zero operands
+    e('  s_cbranch_execz .Lrows_live')                                   # (only in a partial batch)
+    for i in range(33):
+        e(f'  v_mov_b32_e32 v{W0 + i}, 0')
+        e(f'  v_mov_b32_e32 v{WY + i}, 0')
+    e('.Lrows_live:')
+    e('  s_mov_b64 exec, -1')
+    convert_row(WY, X)
     for k in range(Q):
-        e(f'  ds_write_b32 v{V_ZR}, v{TB + 40 + k} offset:{k * RB}')
+        e(f'  ds_write_b32 v{V_ZR}, {X(k)} offset:{k * RB}')
+    convert_row(W0, X)
     e('  s_waitcnt lgkmcnt(0)')
 
     e('// @phase product')
