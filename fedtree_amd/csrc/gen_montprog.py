@@ -463,7 +463,7 @@ def gen(S: int, B: int, U: int, name: str, sqr_unrolled: bool = True) -> str:
 
 
 
-def _descriptor(name, lds_bytes, NVGPR, NSGPR):
+def _descriptor(name, lds_bytes, NVGPR, NSGPR, max_wg=256):
     o = []
     e = o.append
     # ---- kernel descriptor ------------------------------------------------
@@ -502,7 +502,7 @@ def _descriptor(name, lds_bytes, NVGPR, NSGPR):
     e(f'    .group_segment_fixed_size: {lds_bytes}')
     e('    .kernarg_segment_align: 8')
     e('    .kernarg_segment_size: 168')
-    e('    .max_flat_workgroup_size: 256')
+    e(f'    .max_flat_workgroup_size: {max_wg}')
     e(f'    .name: {name}')
     e('    .private_segment_fixed_size: 0')
     e(f'    .sgpr_count: {NSGPR + 2}')

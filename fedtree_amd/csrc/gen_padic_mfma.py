@@ -42,6 +42,7 @@ TILE_OFF = 512                  # byte offset of the tile image in ctx
 TILE_BYTES = 20 * 1024          # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
 SPILL_BYTES = 10 * 1024         # per wave: V[37..73] while Barrett 1 runs (9 x dwordx4 + 1 dword per lane)
 SPILL = "spill" in AB           # measured: no gain (profiles/r02zzi_spill_ab.jsonl), so off
+PP = "pingpong" in AB
 LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
 QBIT = 28 * 38                  # q3 = floor(N / 2^1064)
@@ -61,8 +62,11 @@ def gen_padic_mfma(name: str) -> str:
     # ---- VGPR plan ---------------------------------------------------------
     V_TID, V_GOFF = 0, 1
     VA = (2, 6, 10)                              # A-tile buffers v[2:5], v[6:9], v[10:13] (ACC is free)
-    ACC0 = 10                                    # product columns: 2 column sets x 2 chains x 64-bit
-    CARRY = 18
+    # product columns: NCOL adjacent columns side by side (one 64-bit accumulator chain each), two column
+    # sets (the tails of one set run inside the next set's multiply-adds)
+    NCOL = next((int(t[3:]) for t in AB.split(',') if t in ('col3', 'col4')), 2)
+    ACC0 = 10 if NCOL == 2 else 2                # v[ACC0 .. ACC0 + 4 NCOL); below v20 either way
+    CARRY = ACC0 + 4 * NCOL
     XA = 20                                      # x0 digit (v20..v56); Barrett: accumulators v20..v51
     G0, G1 = XA, XA + 16
     # Barrett scratch in XA above the accumulators: chunk sums v[52:55], clamp mask v56, chunk carry v[58:59]
@@ -91,11 +95,11 @@ def gen_padic_mfma(name: str) -> str:
         return f"v[{n}:{n + 1}]"
 
     def acc(s, ch):
-        n = ACC0 + 2 * (2 * s + ch)
+        n = ACC0 + 2 * (NCOL * s + ch)
         return f"v[{n}:{n + 1}]"
 
     def acclo(s, ch):
-        return f"v{ACC0 + 2 * (2 * s + ch)}"
+        return f"v{ACC0 + 2 * (NCOL * s + ch)}"
 
     carry = pair(CARRY)
     o = []
@@ -103,6 +107,10 @@ def gen_padic_mfma(name: str) -> str:
 
     def e(line):
         sink[-1].append(line)
+
+    def phase():
+        if PP:
+            e('  s_barrier')
 
     def capture(fn):
         sink.append([])
@@ -143,9 +151,9 @@ def gen_padic_mfma(name: str) -> str:
                 t.append(f'  {shr} {carry}, {B}, {a0}')
             return t
 
-        for gi in range(0, len(cols), 2):
-            s = (gi // 2) % 2
-            members = list(range(gi, min(gi + 2, len(cols))))
+        for gi in range(0, len(cols), NCOL):
+            s = (gi // NCOL) % 2
+            members = list(range(gi, min(gi + NCOL, len(cols))))
             seqs = [(acc(s, m), cols[ci]['terms']) for m, ci in enumerate(members)]
             used = [False] * len(seqs)
             n = 0
@@ -540,11 +548,24 @@ def gen_padic_mfma(name: str) -> str:
     for i in range(7):
         e(f'  s_mov_b32 s{SNEG + i}, {hex((-(1 << (4 * i))) & 0xFFFFFFFF)}')
     e(f'  s_mov_b32 s35, {hex(MASK)}')
-    e('  s_lshl_b32 s14, s2, 10')
+    # PP (ping-pong): 512-thread workgroups, the two waves of a SIMD are waves w and w + 4 of one workgroup;
+    # half 1 runs one phase behind half 0 (s_barrier between the products and the reduction of every
+    # SQR / MUL / LOADP), so one wave's matrix phases meet the other wave's product phase
+    e(f'  s_lshl_b32 s14, s2, {11 if PP else 10}')
+    if PP:
+        e(f'  v_readfirstlane_b32 s18, v{V_TID}')
+        if "ppodd" in AB:                          # s18 = half (odd waves: 1)
+            e('  s_bfe_u32 s18, s18, 0x10006')
+        else:                                      # s18 = half (waves 0-3: 0, waves 4-7: 1)
+            e('  s_lshr_b32 s18, s18, 8')
     e(f'  v_lshlrev_b32_e32 v{V_GOFF}, 2, v{V_TID}')
     e(f'  v_add_u32_e32 v{V_GOFF}, s14, v{V_GOFF}')
     # LDS tile image: 5 x 4 KB, each thread one dwordx4 per 4 KB
-    e(f'  v_lshlrev_b32_e32 v10, 4, v{V_TID}')
+    if PP:                                       # threads t and t + 256 write the same image words
+        e(f'  v_and_b32_e32 v10, 0xff, v{V_TID}')
+        e('  v_lshlrev_b32_e32 v10, 4, v10')
+    else:
+        e(f'  v_lshlrev_b32_e32 v10, 4, v{V_TID}')
     for it in range(TILE_BYTES // 4096):
         e(f'  global_load_dwordx4 v[2:5], v10, s[8:9] offset:{TILE_OFF}')
         e('  s_waitcnt vmcnt(0)')
@@ -560,7 +581,12 @@ def gen_padic_mfma(name: str) -> str:
         e(f'  v_add_u32_e32 v{V_SPILL}, v{V_SPILL}, v{V_LDS}')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
-    if "nodesync" not in AB:
+    if PP:
+        e('  s_cmp_eq_u32 s18, 1')                  # half 1: one barrier ahead = one phase behind
+        e('  s_cbranch_scc0 .Lpp_start')
+        e('  s_barrier')
+        e('.Lpp_start:')
+    elif "nodesync" not in AB:
         # odd workgroups start ~8K cycles late: the two waves of a SIMD then reach their matrix-core
         # phases at different times (s_sleep spends no issue slots); 1.5% (profiles/r02zt_desync_ab.jsonl)
         e('  s_bitcmp1_b32 s2, 0')
@@ -646,7 +672,9 @@ def gen_padic_mfma(name: str) -> str:
             col['terms'] = [(sq, sq)]
         cols.append(col)
     columns(cols)
+    phase()
     call('.Lreduce')
+    phase()
     e('  s_sub_u32 s19, s19, 1')
     e('  s_branch .Lsqr_loop')
 
@@ -658,14 +686,18 @@ def gen_padic_mfma(name: str) -> str:
     TM = X1 + T[K:]                              # x1, y1 dead
     columns(product_cols(X0, Y0, 2 * K, TM))
     move(T[:K], X1)
+    phase()
     call('.Lreduce')
+    phase()
     e('  s_branch .Lprog')
 
     # LOADP slot: plain X -> T -> (q3 = x1, r = x0)
     e('.Lloadp:')
     load_limbs(T)
+    phase()
     q3 = mfma_barrett(T, T[K:], clamp=True)
     mfma_remainder(T, q3, T[:K], nxt_p1=False)
+    phase()
     move(X0, T[:K])
     move(X1, T[K:2 * K])
     e('  s_branch .Lprog')
@@ -685,10 +717,18 @@ def gen_padic_mfma(name: str) -> str:
     e('  s_branch .Lprog')
 
     e('.Lend:')
+    if PP:                                       # half 0 pays back half 1's extra barrier
+        e('  s_cmp_eq_u32 s18, 0')
+        e('  s_cbranch_scc0 .Lpp_end')
+        e('  s_barrier')
+        e('.Lpp_end:')
     e('  s_endpgm')
 
     # reduce (SQR, MUL): T (x0^2 or x0 y0), V (cross terms) -> x0 = T mod P, x1 = (V + T div P) mod P
     e('.Lreduce:')
+    PRIO = next((int(t[4:]) for t in AB.split(',') if t.startswith('prio') and t[4:].isdigit()), 0)
+    if PRIO:
+        e(f'  s_setprio {PRIO}')                # the latency-bound matrix phases win the SIMD's VALU issue
     dbuf = "nodbuf" not in AB
     spill = dbuf and SPILL
     if spill:
@@ -710,12 +750,14 @@ def gen_padic_mfma(name: str) -> str:
     mfma_remainder(V, q3b, V[:K], nxt_p1=False, dbuf=dbuf)
     move(X0, T[:K])
     move(X1, V[:K])
+    if PRIO:
+        e('  s_setprio 0')
     e('  s_setpc_b64 s[12:13]')
 
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
     e('')
-    o.extend(_descriptor(name, LDS_BYTES, NVGPR, NSGPR).splitlines())
+    o.extend(_descriptor(name, LDS_BYTES, NVGPR, NSGPR, max_wg=512 if PP else 256).splitlines())
     return "\n".join(o) + "\n"
 
 

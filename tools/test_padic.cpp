@@ -1,6 +1,6 @@
 // Standalone bring-up test + timing of the P-adic exponentiation kernel (fedtree_amd/csrc/gen_padic.py).
 // Build: hipcc --offload-arch=gfx950 -O2 -idirafter /opt/conda/include tools/test_padic.cpp -l:libgmp.so.10 -o tools/bin/test_padic
-// Run:   tools/bin/test_padic <hsaco> [lanes] [mode] [kernel]   mode 0: y^P, y < P (encrypt); 1: c^(P-1), c < P^2;
+// Run:   [M37_BLOCK=512] tools/bin/test_padic <hsaco> [lanes] [mode] [kernel]   mode 0: y^P, y < P (encrypt); 1: c^(P-1), c < P^2;
 //        bring-up programs: 2: LOADP; STOREP (c < P^2), 3: LOADP; SQR 1; STOREP, 4: LOADP; SQR 1; MUL IN; STOREP
 //        kernel: fthe_padic_k37 (default) or fthe_padic_m37 (gen_padic_mfma.py: ctx carries the LDS tile image)
 // Checks sampled lanes against GMP's mpz_powm and prints the launch time and products per second.
@@ -72,7 +72,8 @@ int main(int argc, char **argv) {
     int L = argc > 2 ? atoi(argv[2]) : 65536;
     int mode = argc > 3 ? atoi(argv[3]) : 0;
     std::string kname = argc > 4 ? argv[4] : "fthe_padic_k37";
-    if (L % 256) { printf("lanes must be a multiple of 256\n"); return 2; }
+    const int BLK = getenv("M37_BLOCK") ? atoi(getenv("M37_BLOCK")) : 256;   // 512: ping-pong m37 variants
+    if (BLK <= 0 || BLK % 256 || L % BLK) { printf("lanes must be a multiple of the block (%d)\n", BLK); return 2; }
     std::ifstream f(path, std::ios::binary);
     std::vector<char> blob((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
     if (blob.empty()) { printf("no code object at %s\n", path); return 2; }
@@ -144,7 +145,7 @@ int main(int argc, char **argv) {
     float best = 1e30f;
     for (int rep = 0; rep < 3; rep++) {
         CHECK(hipEventRecord(e0));
-        CHECK(hipModuleLaunchKernel(fn, L / 256, 1, 1, 256, 1, 1, 0, 0, nullptr, cfg));
+        CHECK(hipModuleLaunchKernel(fn, L / BLK, 1, 1, BLK, 1, 1, 0, 0, nullptr, cfg));
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
