@@ -43,6 +43,10 @@ TILE_BYTES = 20 * 1024          # 19 tiles of 1 KB, padded to 5 dwordx4 per thre
 SPILL_BYTES = 10 * 1024         # per wave: V[37..73] while Barrett 1 runs (9 x dwordx4 + 1 dword per lane)
 SPILL = "spill" in AB           # measured: no gain (profiles/r02zzi_spill_ab.jsonl), so off
 PP = "pingpong" in AB
+# PREXOR: the limbs that only ever reach the matrix cores (the upper product halves and q3) leave the
+# column tails / chunk folds with bit 7 of every byte already flipped (v_bitop3_b32 (x & mask) ^ pattern
+# in place of the mask), so packing them into the b ^ 0x80 operand bytes needs no v_xor per dword
+PREXOR = "noprexor" not in AB   # default: 128 fewer VALU per squaring, 72.5 vs 73.3 ms (profiles/r03y_m37_prexor_ab.jsonl)
 LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
 QBIT = 28 * 38                  # q3 = floor(N / 2^1064)
@@ -75,7 +79,14 @@ def gen_padic_mfma(name: str) -> str:
     VV = 174                                     # V limbs v174..v247
     V_LDS = 248                                  # (lane & 63) * 16
     V_SPILL = 249                                # this wave's spill area + (lane & 63) * 16 (SPILL only)
-    NVGPR = 250 if SPILL else 249
+    PATV = (249, 250)                            # PREXOR: byte-flip patterns of even / odd limbs
+    assert not (SPILL and PREXOR)
+    NVGPR = 250 if SPILL else 251 if PREXOR else 249
+
+    def pat(t):
+        """flip pattern of limb t of a packed number (limb t at bit 28 t): bits j with 28 t + j = 7 mod 8"""
+        return f"v{PATV[t % 2]}"
+    PATVAL = (0x00808080, 0x08080808)
     X0 = [f"v{XA + i}" for i in range(K)]
     X1 = [f"v{XB + i}" for i in range(K)]
     T = [f"v{TT + i}" for i in range(2 * K)]
@@ -143,8 +154,14 @@ def gen_padic_mfma(name: str) -> str:
                 x = col['sq']
                 t.append(f'  {mad} {a0}, vcc, {x}, {x}, {a0}')
             if col.get('out') is not None:
+                px = col.get('px')
                 if col.get('last'):
-                    t.append(f'  v_mov_b32_e32 {col["out"]}, {lo0}')
+                    if px:
+                        t.append(f'  v_xor_b32_e32 {col["out"]}, {px}, {lo0}')
+                    else:
+                        t.append(f'  v_mov_b32_e32 {col["out"]}, {lo0}')
+                elif px:                                     # (lo & mask) ^ pattern
+                    t.append(f'  v_bitop3_b32 {col["out"]}, {lo0}, {SMASK}, {px} bitop3:0x6a')
                 else:
                     t.append(f'  v_and_b32_e32 {col["out"]}, {hex(MASK)}, {lo0}')
             if not col.get('last') and not col.get('nocarry'):
@@ -184,6 +201,8 @@ def gen_padic_mfma(name: str) -> str:
                     if a2 is not None:
                         terms.append((a2[i], b2[j]))
             cols.append({'terms': terms, 'out': outs[c], 'last': c == n_out - 1})
+            if PREXOR and c >= K:                      # the upper half only feeds Barrett's q1 bytes
+                cols[-1]['px'] = pat(c - (K - 1))
         return cols
 
     def move(dst, src):
@@ -202,11 +221,26 @@ def gen_padic_mfma(name: str) -> str:
     CCARRY = pair(XA + 38)                      # chunk carry v[58:59]
     SMASK = "s35"                               # 0x0fffffff (v_bfi_b32 operand)
 
-    def orpack(limbs, shift_bits, ndw, xor_masks, lead_one=False, norm0=False):
+    def orpack(limbs, shift_bits, ndw, xor_masks, lead_one=False, norm0=False, pre=()):
         """normalised 28-bit limbs (limb t at bit 28 t + shift_bits) -> dwords D[0..ndw-1] XOR xor_masks[w],
         each dword from the (at most two) limbs it overlaps: no carry chain.  lead_one: byte 0 is the
-        constant digit 1 (shift_bits = 8).  norm0: limb 0 may hold a bit 28 (masked off here)."""
+        constant digit 1 (shift_bits = 8).  norm0: limb 0 may hold a bit 28 (masked off here).  pre: the
+        limbs already XORed with pat(t) (PREXOR); only the flips they do not carry are applied here."""
         n = len(limbs)
+        pre = set(pre)
+
+        def carried(w):
+            """bits of dword w already flipped by pre-XORed limbs"""
+            m = 0
+            for b in range(32):
+                q = 32 * w - shift_bits + b                   # bit of the packed number
+                if q < 0 or (lead_one and w == 0 and b < 8):
+                    continue
+                t, j = q // B, q % B
+                if t in pre and t < n and (PATVAL[t % 2] >> j) & 1:
+                    m |= 1 << b
+            return m
+        xor_masks = [xor_masks[w] ^ carried(w) for w in range(ndw)]
         for w in range(ndw):
             d = D[w]
             if lead_one and w == 0:
@@ -394,9 +428,9 @@ def gen_padic_mfma(name: str) -> str:
         own accumulator (two, alternating), independent of the carry; its tail (+ carry, mask, carry out)
         is deferred into the next chunk's multiply-adds, so the carry chain never stalls the wave."""
 
-        def __init__(self, base_bits, t0, t_last, outs, neg, inits=None, nocarry_last=False):
+        def __init__(self, base_bits, t0, t_last, outs, neg, inits=None, nocarry_last=False, px=False):
             self.base, self.t, self.t0, self.t_last, self.outs, self.neg = base_bits, t0, t0, t_last, outs, neg
-            self.inits, self.nocarry_last = inits, nocarry_last
+            self.inits, self.nocarry_last, self.px = inits, nocarry_last, px
             self.pending = []
             self.fresh = True
             self.begun = False
@@ -422,7 +456,11 @@ def gen_padic_mfma(name: str) -> str:
             if self.t != self.t0:
                 tail.append(f'  v_lshl_add_u64 {a}, {a}, 0, {CCARRY}')
             if 0 <= self.t < len(self.outs):
-                tail.append(f'  v_and_b32_e32 {self.outs[self.t]}, {hex(MASK)}, v{a[2:a.index(":")]}')
+                if self.px:                              # q3 limbs leave pre-flipped (PREXOR)
+                    tail.append(f'  v_bitop3_b32 {self.outs[self.t]}, v{a[2:a.index(":")]}, {SMASK}, '
+                                f'{pat(self.t)} bitop3:0x6a')
+                else:
+                    tail.append(f'  v_and_b32_e32 {self.outs[self.t]}, {hex(MASK)}, v{a[2:a.index(":")]}')
             if not (self.nocarry_last and self.t == self.t_last):
                 tail.append(f'  v_ashrrev_i64 {CCARRY}, {B}, {a}')
             self.pending = tail
@@ -475,19 +513,22 @@ def gen_padic_mfma(name: str) -> str:
     P1_TILES = [(1, m, [k for k in range(5) if m - k <= 1]) for m in range(5)]
     P2_TILES = [(2, m, [k for k in range(5) if m >= k]) for m in range(5)]
 
-    def mfma_barrett(Tl, q3out, clamp, prefetched=False, dbuf=False, setb=None):
+    def mfma_barrett(Tl, q3out, clamp, prefetched=False, dbuf=False, setb=None, pre_in=None):
         """product 1: q3 = Barrett's quotient of T (Tl: 2K limbs, Tl[K-1] < 2^29 allowed) -> q3out (K regs,
         may be Tl[K:]); clamp: q3 = -1 (q1 = 0) -> 0; prefetched: its first A-tile reads are in flight;
-        dbuf: double-buffered accumulators (T[38..69] free)"""
+        dbuf: double-buffered accumulators (T[38..69] free); pre_in: Tl[K..2K-1] arrive pre-flipped
+        (PREXOR, default); q3out leaves pre-flipped under PREXOR"""
+        if pre_in is None:
+            pre_in = PREXOR
         if not prefetched:
             prefetch(*P1_TILES[0])
-        orpack(Tl[K - 1:2 * K], 0, 34, [0x80808080] * 34, norm0=True)
+        orpack(Tl[K - 1:2 * K], 0, 34, [0x80808080] * 34, norm0=True, pre=range(1, K + 1) if pre_in else ())
         e(f'  v_bfe_u32 {D[34]}, {Tl[K - 1]}, 28, 1')              # c = bit 28 of q1[0] -> digit 16 c at byte 137
         e(f'  v_lshl_or_b32 {D[34]}, {D[34]}, 12, 1')               # and the constant digit 1 at byte 136
         for w in range(35, 40):
             e(f'  v_mov_b32_e32 {D[w]}, 0')
         swap_operands()
-        ch = Chunks(QBIT, (8 * S1_LO - QBIT) // B, 39, q3out, neg=False)
+        ch = Chunks(QBIT, (8 * S1_LO - QBIT) // B, 39, q3out, neg=False, px=PREXOR)
 
         def consume(m, creg):
             fold_columns(ch, tile_cols(1, m, lambda rho: S1_LO + 32 * m + rho, creg))
@@ -495,15 +536,18 @@ def gen_padic_mfma(name: str) -> str:
         ch.finish()
         if clamp:                                  # final carry = 0, or -1 when q1 = 0 (q3 = -1 -> 0)
             e(f'  v_not_b32_e32 v{XA + 36}, v{XA + 38}')
-            for r in q3out:
-                e(f'  v_and_b32_e32 {r}, {r}, v{XA + 36}')
+            for t, r in enumerate(q3out):
+                if PREXOR:                         # ((r ^ pat) & m) ^ pat
+                    e(f'  v_bitop3_b32 {r}, {r}, v{XA + 36}, {pat(t)} bitop3:0xe2')
+                else:
+                    e(f'  v_and_b32_e32 {r}, {r}, v{XA + 36}')
         return q3out
 
     def mfma_remainder(Tl, q3, rout, nxt_p1, dbuf=False, after_pack=None):
         """product 2: r = (T - q3 P) mod b^K -> rout (may be Tl[:K]); the product-2 tile-0 reads are already
         in flight; nxt_p1: prefetch product 1's first tiles at the end (the next Barrett); after_pack: the
         caller's last use of the q3 limbs (dbuf may then take their registers)"""
-        orpack(q3, 8, 33, [0x80808000] + [0x80808080] * 32, lead_one=True)
+        orpack(q3, 8, 33, [0x80808000] + [0x80808080] * 32, lead_one=True, pre=range(K) if PREXOR else ())
         if after_pack and not dbuf:
             after_pack()
         e(f'  v_mov_b32_e32 {D[33]}, 0x80')          # q3 byte 131 (zero, offset) at byte 132; pads 0
@@ -548,6 +592,9 @@ def gen_padic_mfma(name: str) -> str:
     for i in range(7):
         e(f'  s_mov_b32 s{SNEG + i}, {hex((-(1 << (4 * i))) & 0xFFFFFFFF)}')
     e(f'  s_mov_b32 s35, {hex(MASK)}')
+    if PREXOR:
+        for v_, val in zip(PATV, PATVAL):
+            e(f'  v_mov_b32_e32 v{v_}, {hex(val)}')
     # PP (ping-pong): 512-thread workgroups, the two waves of a SIMD are waves w and w + 4 of one workgroup;
     # half 1 runs one phase behind half 0 (s_barrier between the products and the reduction of every
     # SQR / MUL / LOADP), so one wave's matrix phases meet the other wave's product phase
@@ -658,12 +705,16 @@ def gen_padic_mfma(name: str) -> str:
     for c in range(2 * K):
         terms = [(X0[i], X1[c - i]) for i in range(K) if 0 <= c - i < K]
         cols.append({'terms': terms, 'dbl': True, 'out': V[c], 'last': c == 2 * K - 1})
+        if PREXOR and c >= K:
+            cols[-1]['px'] = pat(c - (K - 1))
     columns(cols)
     cols = []
     for c in range(2 * K):
         terms = [(X0[i], X0[c - i]) for i in range(K) if i < c - i < K]
         sq = X0[c // 2] if c % 2 == 0 and c // 2 < K else None
         col = {'terms': terms, 'out': T[c], 'last': c == 2 * K - 1}
+        if PREXOR and c >= K:
+            col['px'] = pat(c - (K - 1))
         if terms:
             col['dbl'] = True
             if sq:
@@ -695,11 +746,15 @@ def gen_padic_mfma(name: str) -> str:
     e('.Lloadp:')
     load_limbs(T)
     phase()
-    q3 = mfma_barrett(T, T[K:], clamp=True)
+    q3 = mfma_barrett(T, T[K:], clamp=True, pre_in=False)
     mfma_remainder(T, q3, T[:K], nxt_p1=False)
     phase()
     move(X0, T[:K])
-    move(X1, T[K:2 * K])
+    if PREXOR:
+        for i in range(K):
+            e(f'  v_xor_b32_e32 {X1[i]}, {pat(i)}, {T[K + i]}')
+    else:
+        move(X1, T[K:2 * K])
     e('  s_branch .Lprog')
 
     # STOREP slot: x0 + x1 P with -P in SGPRs (scratch -x1 in T[0..K-1]; out V)
@@ -726,7 +781,9 @@ def gen_padic_mfma(name: str) -> str:
 
     # reduce (SQR, MUL): T (x0^2 or x0 y0), V (cross terms) -> x0 = T mod P, x1 = (V + T div P) mod P
     e('.Lreduce:')
-    PRIO = next((int(t[4:]) for t in AB.split(',') if t.startswith('prio') and t[4:].isdigit()), 0)
+    # default s_setprio 3 over the reduction (noprio: none): -0.5..1% (profiles/r03s_m37_prio_ab.jsonl)
+    PRIO = next((int(t[4:]) for t in AB.split(',') if t.startswith('prio') and t[4:].isdigit()),
+                0 if "noprio" in AB else 3)
     if PRIO:
         e(f'  s_setprio {PRIO}')                # the latency-bound matrix phases win the SIMD's VALU issue
     dbuf = "nodbuf" not in AB
@@ -740,7 +797,10 @@ def gen_padic_mfma(name: str) -> str:
 
     def add_u1():
         for i in range(K):
-            e(f'  v_add_u32_e32 {V[i]}, {V[i]}, {q3[i]}')  # V += u1 (limbs < 2^29); u1 dies here
+            if PREXOR:                                      # V += u1 ^ pat (u1 arrives pre-flipped)
+                e(f'  v_xad_u32 {V[i]}, {q3[i]}, {pat(i)}, {V[i]}')
+            else:
+                e(f'  v_add_u32_e32 {V[i]}, {V[i]}, {q3[i]}')  # V += u1 (limbs < 2^29); u1 dies here
         if spill:                                           # V[37..73] back (older than every tile read)
             for j in range(9):
                 e(f'  ds_read_b128 v[{VV + 38 + 4 * j}:{VV + 41 + 4 * j}], v{V_SPILL} offset:{1024 * j}')
