@@ -46,6 +46,9 @@ PP = "pingpong" in AB
 # PREXOR: the limbs that only ever reach the matrix cores (the upper product halves and q3) leave the
 # column tails / chunk folds with bit 7 of every byte already flipped (v_bitop3_b32 (x & mask) ^ pattern
 # in place of the mask), so packing them into the b ^ 0x80 operand bytes needs no v_xor per dword
+# chunk carry enters the next chunk's first multiply-add (no carry add): 162 fewer VALU per squaring,
+# 69.8-70.5 vs 71.7-72.9 ms (profiles/r03za_m37_cmerge_ab.jsonl); nocmerge restores the deferred carry add
+CMERGE = "nocmerge" not in AB
 PREXOR = "noprexor" not in AB   # default: 128 fewer VALU per squaring, 72.5 vs 73.3 ms (profiles/r03y_m37_prexor_ab.jsonl)
 LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
@@ -443,9 +446,13 @@ def gen_padic_mfma(name: str) -> str:
             if self.pending:
                 e(self.pending.pop(0))
 
+        def addend0(self):
+            """addend of a chunk's first multiply-add: the previous chunk's carry under CMERGE"""
+            return CCARRY if CMERGE and self.t != self.t0 else "0"
+
         def start(self):
             if self.inits is not None and 0 <= self.t < len(self.inits):
-                self.emit(f'  v_mad_u64_u32 {self.acc()}, vcc, {self.inits[self.t]}, 1, 0')
+                self.emit(f'  v_mad_u64_u32 {self.acc()}, vcc, {self.inits[self.t]}, 1, {self.addend0()}')
                 self.fresh = False
 
         def close(self):
@@ -453,7 +460,7 @@ def gen_padic_mfma(name: str) -> str:
                 e(ins)
             a = self.acc()
             tail = []
-            if self.t != self.t0:
+            if self.t != self.t0 and not CMERGE:
                 tail.append(f'  v_lshl_add_u64 {a}, {a}, 0, {CCARRY}')
             if 0 <= self.t < len(self.outs):
                 if self.px:                              # q3 limbs leave pre-flipped (PREXOR)
@@ -462,7 +469,10 @@ def gen_padic_mfma(name: str) -> str:
                 else:
                     tail.append(f'  v_and_b32_e32 {self.outs[self.t]}, {hex(MASK)}, v{a[2:a.index(":")]}')
             if not (self.nocarry_last and self.t == self.t_last):
-                tail.append(f'  v_ashrrev_i64 {CCARRY}, {B}, {a}')
+                if CMERGE:                               # the next chunk's first multiply-add reads it
+                    e(f'  v_ashrrev_i64 {CCARRY}, {B}, {a}')
+                else:
+                    tail.append(f'  v_ashrrev_i64 {CCARRY}, {B}, {a}')
             self.pending = tail
             self.t += 1
             self.fresh = True
@@ -479,7 +489,7 @@ def gen_padic_mfma(name: str) -> str:
             sh = 8 * s - self.base - B * t
             mul = NEG(sh) if self.neg else POW(sh)
             a = self.acc()
-            self.emit(f'  v_mad_i64_i32 {a}, vcc, {reg}, {mul}, {"0" if self.fresh else a}')
+            self.emit(f'  v_mad_i64_i32 {a}, vcc, {reg}, {mul}, {self.addend0() if self.fresh else a}')
             self.fresh = False
 
         def finish(self):
