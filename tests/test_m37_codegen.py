@@ -7,11 +7,14 @@
   one lane, on pre-flipped limbs, and must give exactly the dwords of the unflipped limbs with bit 7 of every
   byte flipped (what the i8 matrix product expects: b ^ 0x80 = b - 128);
 * the v_bitop3_b32 truth tables the generator uses, under the operand order the compiler's own output shows
-  (bit index = src0 << 2 | src1 << 1 | src2)."""
+  (bit index = src0 << 2 | src1 << 1 | src2);
+* the whole kernel, one wave on the CPU emulator (tools/wave_emu.py), against Python integers."""
 import os
 import random
 import re
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fedtree_amd", "csrc"))
@@ -131,3 +134,13 @@ def test_bitop3_tables():
         assert _bitop3(m, p, x, 0x6C) == (x & m) ^ p               # hipcc's own encoding of (a & b) ^ c
     src = open(os.path.join(ROOT, "fedtree_amd", "csrc", "gen_padic_mfma.py")).read()
     assert "bitop3:0x6a" in src and "bitop3:0xe2" in src
+
+
+@pytest.mark.parametrize("bits", [1009, 1030])
+def test_wave_emulation_of_the_kernel(bits):
+    """one wave of the generated fthe_padic_m37 on the CPU (tools/wave_emu.py: the MFMA and permlane32 lane
+    maps measured on the GPU): LOADP, STOREX, SQR, MUL, STOREP = x^3 mod P^2 on 64 lanes, P at the ends of the
+    kernel's range, x incl. 0, 1, P - 1, P and P^2 - 1"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import wave_emu
+    assert wave_emu.m37_selftest(seed=bits, bits=bits) == 0

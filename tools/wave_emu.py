@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
-"""Emulator of whole wavefronts (64 lanes) for the instruction subset of the matrix-core Barrett add kernel
-(fedtree_amd/csrc/gen_addb.py): per-lane VGPRs, SGPRs, EXEC / VCC / SCC, DPP quad_perm, LDS, global
-memory, v_mfma_i32_16x16x64_i8 (lane map measured on the GPU: profiles/r03c_mfma16_probe.txt) -- so that
-register plans, lane layouts, LDS offsets and control flow are checked on the CPU before the kernel
-runs on a GPU.  A workgroup is emulated wave by wave: every wave up to its s_barrier, then each wave to
-its end (the kernel's waves share only what they wrote before the barrier).
+"""Emulator of whole wavefronts (64 lanes) for the instruction subsets of the matrix-core kernels: the
+Barrett add (fedtree_amd/csrc/gen_addb.py) and the P-adic exponentiation fthe_padic_m37 (gen_padic_mfma.py):
+per-lane VGPRs, SGPRs, EXEC / VCC / SCC, DPP quad_perm, LDS, global memory, v_mfma_i32_16x16x64_i8 and
+v_mfma_i32_32x32x32_i8 and v_permlane32_swap (lane maps measured on the GPU: profiles/r03c_mfma16_probe.txt,
+profiles/r02zh_mfma_probe.txt), the s_getpc / s_swappc call of m37's shared reduction -- so that register
+plans, lane layouts, LDS offsets and control flow are checked on the CPU before the kernel runs on a GPU.  A
+workgroup is emulated wave by wave: every wave up to its s_barrier, then each wave to its end (the kernels'
+waves share only what they wrote before the barrier).
 
   python tools/wave_emu.py         (self-test: 16 random adds mod n^2 and edge cases vs Python integers)
+  python tools/wave_emu.py m37     (one wave of fthe_padic_m37: LOADP, STOREX, SQR, MUL, STOREP = x^3 mod P^2)
 """
 import os
 import random
@@ -88,6 +91,9 @@ class Wave:
             return self.exec
         r = self.rr(tok)
         if r is None:
+            m = re.fullmatch(r'(\.L\w+)-(\.L\w+)', tok)          # label difference (s_getpc-relative call)
+            if m:
+                return (self.labels[m.group(1)] - self.labels[m.group(2)]) & M32
             return int(tok, 0) & (M64 if width == 2 else M32)
         kind, b, n = r
         assert kind == 's', tok
@@ -148,7 +154,29 @@ class Wave:
         if op == 's_barrier':
             self.at_barrier = True
             return
-        if op in ('s_nop', 's_waitcnt'):
+        if op in ('s_nop', 's_waitcnt', 's_setprio', 's_sleep'):
+            return
+        if op == 's_cbranch_scc0':
+            if not self.scc:
+                self.pc = self.labels[a[0]]
+            return
+        if op == 's_getpc_b64':                    # pc = index of the next instruction
+            self.sset(a[0], self.pc)
+            return
+        if op == 's_swappc_b64':
+            ret = self.pc
+            self.pc = self.sget(a[1], 2)
+            self.sset(a[0], ret)
+            return
+        if op == 's_setpc_b64':
+            self.pc = self.sget(a[0], 2)
+            return
+        if op == 'v_mfma_i32_32x32x32_i8':
+            return self.mfma32(a)
+        if op == 'v_permlane32_swap_b32_e32':      # the upper half of vdst <-> the lower half of vsrc
+            x, y = self.rr(a[0])[1], self.rr(a[1])[1]
+            for l in range(32):
+                self.v[x][l + 32], self.v[y][l] = self.v[y][l], self.v[x][l + 32]
             return
         if op == 's_branch':
             self.pc = self.labels[a[0]]
@@ -191,9 +219,18 @@ class Wave:
 
     def salu(self, op, a):
         g = self.sget
-        if op == 's_load_dwordx2':
+        if op in ('s_load_dwordx2', 's_load_dwordx4', 's_load_dwordx8', 's_load_dwordx16'):
+            n = int(op[len('s_load_dwordx'):])
             addr = g(a[1], 2) + int(a[2], 0)
-            self.sset(a[0], self.mem.read(addr, 8))
+            self.sset(a[0], self.mem.read(addr, 4 * n))
+        elif op == 's_bitcmp1_b32':
+            self.scc = (g(a[0]) >> (g(a[1]) & 31)) & 1
+        elif op == 's_mul_hi_u32':
+            self.sset(a[0], (g(a[1]) * g(a[2])) >> 32)
+        elif op == 's_addc_u32':
+            r = g(a[1]) + g(a[2]) + self.scc
+            self.sset(a[0], r)
+            self.scc = r >> 32
         elif op == 's_load_dword':
             addr = g(a[1], 2) + int(a[2], 0)
             self.sset(a[0], self.mem.read(addr, 4))
@@ -268,7 +305,7 @@ class Wave:
 
     def glob(self, op, a):
         width = {'global_load_dword': 4, 'global_load_dwordx2': 8, 'global_load_dwordx4': 16,
-                 'global_store_dwordx4': 16}[op]
+                 'global_store_dword': 4, 'global_store_dwordx4': 16}[op]
         off = 0
         for t in a[3:]:
             if t.startswith('offset:'):
@@ -309,9 +346,52 @@ class Wave:
         for (g, l), val in newd.items():
             self.v[D[1] + g][l] = val
 
+    def mfma32(self, a):
+        """v_mfma_i32_32x32x32_i8 D, A, B, C (C may be 0): lane l (r = l & 31, h = l >> 5) holds A[r][16h + j]
+        and B[16h + j][r] in byte j of its 16-byte fragment; register g of D / C is row (g & 3) + 8 (g >> 2) + 4h,
+        column r (profiles/r02zh_mfma_probe.txt)"""
+        D, A, Bt = (self.rr(t) for t in a[:3])
+        C = self.rr(a[3])
+        Am = [[0] * 32 for _ in range(32)]
+        Bm = [[0] * 32 for _ in range(32)]
+        for l in range(64):
+            r, h = l & 31, l >> 5
+            ab = b''.join(self.v[A[1] + i][l].to_bytes(4, 'little') for i in range(4))
+            bb = b''.join(self.v[Bt[1] + i][l].to_bytes(4, 'little') for i in range(4))
+            for j in range(16):
+                Am[r][16 * h + j] = ab[j] - 256 if ab[j] > 127 else ab[j]
+                Bm[16 * h + j][r] = bb[j] - 256 if bb[j] > 127 else bb[j]
+        cols = [[sum(Am[i][k] * Bm[k][n] for k in range(32)) for n in range(32)] for i in range(32)]
+        newd = {}
+        for l in range(64):
+            h, col = l >> 5, l & 31
+            for gi in range(16):
+                row = (gi & 3) + 8 * (gi >> 2) + 4 * h
+                c = s32(self.v[C[1] + gi][l]) if C is not None else 0
+                newd[(gi, l)] = (cols[row][col] + c) & M32
+        for (gi, l), val in newd.items():
+            self.v[D[1] + gi][l] = val
+
     def valu(self, op, a):
         lanes = self.lanes()
         g = self.vget
+        if op == 'v_pk_mov_b32':                   # op_sel:[a,b]: lo from src0's half a, hi from src1's half b
+            sel = [int(x) for x in re.search(r'op_sel:\[([01]),([01])\]', ' '.join(a)).groups()]
+            for l in lanes:
+                s0, s1 = g(l, a[1]), g(l, a[2])
+                lo = (s0 >> (32 * sel[0])) & M32
+                hi = (s1 >> (32 * sel[1])) & M32
+                self.vset(l, a[0], lo | hi << 32)
+            return
+        if op == 'v_bitop3_b32':                   # bit i = table[src0_i << 2 | src1_i << 1 | src2_i]
+            tbl = int(a[4].split(':')[1], 0)
+            for l in lanes:
+                x, y, z = g(l, a[1]), g(l, a[2]), g(l, a[3])
+                r = 0
+                for i in range(32):
+                    r |= ((tbl >> ((x >> i & 1) << 2 | (y >> i & 1) << 1 | (z >> i & 1))) & 1) << i
+                self.vset(l, a[0], r)
+            return
         if op in ('v_mad_u64_u32', 'v_mad_i64_i32'):
             newvcc = self.vcc
             for l in lanes:
@@ -420,6 +500,12 @@ class Wave:
                 r = g(l, a[2]) if (self.sget(a[3], 2) >> l) & 1 else g(l, a[1])
             elif op == 'v_cndmask_b32_e32':
                 r = g(l, a[2]) if (self.vcc >> l) & 1 else g(l, a[1])
+            elif op == 'v_bfi_b32':
+                r = (g(l, a[1]) & g(l, a[2])) | (~g(l, a[1]) & g(l, a[3]))
+            elif op == 'v_xad_u32':
+                r = (g(l, a[1]) ^ g(l, a[2])) + g(l, a[3])
+            elif op == 'v_not_b32_e32':
+                r = ~g(l, a[1])
             else:
                 raise NotImplementedError(op)
             self.vset(l, a[0], r & (M64 if self.rr(a[0])[2] == 2 else M32))
@@ -451,16 +537,18 @@ def parse(asm):
     return prog, labels
 
 
-def run_workgroup(asm, lds_bytes, waves, mem, kernarg_addr, wg, nvgpr):
+def run_workgroup(asm, lds_bytes, waves, mem, kernarg_addr, wg, nvgpr, finish=None):
+    """finish: the waves to run past their first barrier (default all)"""
     prog, labels = parse(asm)
     lds = bytearray(lds_bytes)
     ws = [Wave(prog, labels, lds, mem, {0: kernarg_addr & M32, 1: kernarg_addr >> 32, 2: wg}, 64 * w, nvgpr)
           for w in range(waves)]
     for w in ws:
         w.run()
-    for w in ws:
-        w.at_barrier = False
-        w.run()
+    for i, w in enumerate(ws):
+        if finish is None or i in finish:
+            w.at_barrier = False
+            w.run()
     return sum(w.count for w in ws)
 
 
@@ -522,8 +610,66 @@ def selftest(ntests=16, count0=None):
     print("wave_emu selftest OK")
 
 
+def m37_selftest(seed=1, ab=None, bits=1024):
+    """wave 0 of fthe_padic_m37 (one workgroup of 256 lanes, 4 waves fill the LDS tile image, wave 0 runs on):
+    LOADP x; STOREX t; SQR 1; MUL t; STOREP -> x^3 mod P^2 (< 6 P^2), against Python integers on its 64 lanes
+    (x < P^2: 0, 1, P - 1, P, P^2 - 1 and random).  ab: a generator switch string (FTHE_GEN_M37_AB)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
+    sys.path.insert(0, here)
+    if ab is not None:
+        os.environ["FTHE_GEN_M37_AB"] = ab
+    import importlib
+    import gen_padic_mfma as gm
+    gm = importlib.reload(gm)
+    import padic_mfma_model as mm
+    rng = random.Random(seed)
+    P = rng.getrandbits(bits) | (1 << (bits - 1)) | (1 << (bits - 2)) | 1
+    P2 = P * P
+    K, S, L, B = 37, 74, 256, 28
+    asm = gm.gen_padic_mfma('fthe_padic_m37')
+    nv = int(re.search(r'\.amdhsa_next_free_vgpr (\d+)', asm).group(1))
+    lds_bytes = int(re.search(r'\.amdhsa_group_segment_fixed_size (\d+)', asm).group(1))
+    ctx = bytearray(gm.TILE_OFF + gm.TILE_BYTES)
+    for j in range(K):                                           # -P limbs (int32)
+        ctx[4 * j:4 * j + 4] = ((-((P >> (B * j)) & ((1 << B) - 1))) & M32).to_bytes(4, 'little')
+    img = mm.MfmaKey(P).tile_image()
+    ctx[gm.TILE_OFF:gm.TILE_OFF + len(img)] = img
+    xs = [rng.randrange(P2) for _ in range(L)]
+    xs[:5] = [0, 1, P - 1, P, P2 - 1]
+    IN, TAB, OUT = 0, 1, 2
+    slots = bytearray(3 * S * L * 4)
+    for g_, x in enumerate(xs):
+        for k in range(S):
+            off = (IN * S + k) * L * 4 + 4 * g_
+            slots[off:off + 4] = ((x >> (B * k)) & ((1 << B) - 1)).to_bytes(4, 'little')
+    prog = [22, IN, 2, TAB, 3, 1, 4, TAB, 23, OUT, 0, 0]
+    mem = Mem()
+    SB, PB, CB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000
+    mem.alloc(slots, SB)
+    mem.alloc(b''.join(w.to_bytes(4, 'little') for w in prog), PB)
+    mem.alloc(bytes(ctx), CB)
+    karg = SB.to_bytes(8, 'little') + PB.to_bytes(8, 'little') + CB.to_bytes(8, 'little') + \
+        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + bytes(4 + 128)
+    mem.alloc(karg, KA)
+    steps = run_workgroup(asm, lds_bytes, 4, mem, KA, 0, nv, finish=(0,))
+    bad = 0
+    for g_ in range(64):
+        got = 0
+        for k in reversed(range(S)):
+            got = (got << B) + mem.read(SB + (OUT * S + k) * L * 4 + 4 * g_, 4)
+        if not (got < 6 * P2 and got % P2 == pow(xs[g_], 3, P2)):
+            bad += 1
+            if bad <= 3:
+                print(f"  lane {g_}: got {got:#x}\n   want {pow(xs[g_], 3, P2):#x}")
+    print(f"m37 ({ab or 'default'}): 64 lanes, {bad} mismatches, {steps} wave-instructions emulated")
+    return bad
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 1:                     # e.g. 211: wave 0 takes a second batch (the grid-stride loop)
+    if len(sys.argv) > 1 and sys.argv[1] == 'm37':
+        sys.exit(1 if m37_selftest(ab=sys.argv[2] if len(sys.argv) > 2 else None) else 0)
+    elif len(sys.argv) > 1:                   # e.g. 211: wave 0 takes a second batch (the grid-stride loop)
         selftest(ntests=int(sys.argv[1]), count0=int(sys.argv[1]))
     else:
         selftest()
