@@ -377,6 +377,27 @@ def gen_nadic(S: int, B: int, name: str) -> str:
 
         def est_list(tb, u, qreg, dacc):
             acc = f"v[{dacc}:{dacc + 1}]"
+            ab = os.environ.get("FTHE_GEN_NADIC_AB", "")
+            if "noest" in ab:                                        # timing only: q = 0 (wrong results)
+                return [f'  v_mov_b32_e32 v{qreg}, 0', None, None,
+                        f'  v_mov_b32_dpp v{qreg}, v{qreg} quad_perm:[3,3,3,3] {DPP}']
+            if "fold" in ab.split(","):
+                # y = col[Q-1] + (col[Q-2] >> 27) with two 64-bit integer instructions (v[6:7] is free inside
+                # the product), then -q = trunc(bias - y 2^27 invN) through a two-term fma chain: one
+                # conversion and one fma fewer than the chain over col[Q-1] and hi32(col[Q-2]).  Bit-exact
+                # (tools/nadic_model.py, the GPU tests) but 1.2% slower: 453k vs 459k public-key encrypts/s
+                # (profiles/r03zh_nadic_fold_ab.jsonl) -- the chain becomes serial; so opt-in, not the default
+                return [
+                    f'  v_ashrrev_i64 {tmp}, {B}, {R(tb, Q - 2, u)}',
+                    f'  v_lshl_add_u64 {tmp}, {R(tb, Q - 1, u)}, 0, {tmp}',
+                    f'  v_cvt_f64_i32_e32 {d0}, v{V_TMP + 1}',
+                    f'  v_fma_f64 {acc}, {d0}, s[40:41], {bias}',
+                    f'  v_cvt_f64_u32_e32 {d0}, v{V_TMP}',
+                    f'  v_fma_f64 {acc}, {d0}, s[38:39], {acc}',
+                    f'  v_cvt_i32_f64_e32 v{qreg}, {acc}',
+                    None, None,                                   # DPP read-after-VALU-write spacing
+                    f'  v_mov_b32_dpp v{qreg}, v{qreg} quad_perm:[3,3,3,3] {DPP}',
+                ]
             return [
                 # -q = trunc(bias - V invN) with the constants negated on the host (as MULWC)
                 f'  v_cvt_f64_i32_e32 {d0}, {Rhi(tb, Q - 2, u)}',
