@@ -1,3 +1,6 @@
+#!/bin/bash
+# PMC (GRBM / SQ cycles, VALU instructions) with the kernel trace on three m37 code objects in the standalone
+# harness: the clock and the cycles of the default schedule, of the timing-only variant without MFMAs and of prio3.
 set -e
 export TMPDIR=/tmp
 for v in base nomfma prio3; do
