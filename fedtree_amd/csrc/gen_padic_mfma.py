@@ -43,6 +43,10 @@ TILE_BYTES = 20 * 1024          # 19 tiles of 1 KB, padded to 5 dwordx4 per thre
 SPILL_BYTES = 10 * 1024         # per wave: V[37..73] while Barrett 1 runs (9 x dwordx4 + 1 dword per lane)
 SPILL = "spill" in AB           # measured: no gain (profiles/r02zzi_spill_ab.jsonl), so off
 PP = "pingpong" in AB
+# VALU instructions kept between a tile's last MFMA and the lane exchange that reads its results (>= 24: the
+# 8-pass XDL -> VALU hazard then needs no s_nop); A/B knob marginN
+MARGIN = next((int(t[6:]) for t in AB.split(',') if t.startswith('margin') and t[6:].isdigit()), 30)
+assert MARGIN >= 24
 # PREXOR: the limbs that only ever reach the matrix cores (the upper product halves and q3) leave the
 # column tails / chunk folds with bit 7 of every byte already flipped (v_bitop3_b32 (x & mask) ^ pattern
 # in place of the mask), so packing them into the b ^ 0x80 operand bytes needs no v_xor per dword
@@ -387,7 +391,7 @@ def gen_padic_mfma(name: str) -> str:
             work = capture(after_issue0)
             for ins in work:
                 e(ins)
-            separated = len(work) >= 30
+            separated = len(work) >= MARGIN
         for m in range(5):
             if m < 4:
                 nxt_issue = capture(lambda: issue_tile(*tiles[m + 1], *sets[(m + 1) % 2], prefetched=False))
@@ -412,9 +416,9 @@ def gen_padic_mfma(name: str) -> str:
                     grp = []
             if grp:
                 items.append(grp)
-            room = len(fold) - 30                  # the MFMAs go before the last 30 instructions of the fold
+            room = len(fold) - MARGIN              # the MFMAs go before the last MARGIN instructions of the fold
             gap = max(1, room // (len(items) + 1)) if items else 0
-            separated = items != [] and len(fold) - gap * len(items) >= 30
+            separated = items != [] and len(fold) - gap * len(items) >= MARGIN
             k = 0
             for i, ins in enumerate(fold):
                 if items and k < len(items) and i % gap == 0:
