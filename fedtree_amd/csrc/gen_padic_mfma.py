@@ -15,10 +15,13 @@ multiply-adds of fthe_padic_k37, and both of their products have a constant oper
   * the A operand is a 32 x 32 tile of the constant's Toeplitz matrix in balanced base-256 digits, read
     from LDS (19 tiles, 19 KB, filled once per workgroup from the key's context; the correction for the
     -128 offset and the truncation bias ride in one extra digit column, tools/padic_mfma_model.py);
-  * each M-tile (32 output columns) accumulates its K-tiles in int32 (16 VGPRs per group), the two groups'
-    accumulators are exchanged with 16 v_permlane32_swap so that every lane holds its own 32 column sums,
-    and the lane folds them into 28-bit limbs: one v_mad_i64_i32 per column (x 2^sh), one mask and one
-    arithmetic shift per limb.
+  * each M-tile (32 output columns) accumulates its K-tiles in int32 (16 VGPRs per group); adjacent rows are
+    paired in 32-bit, the two groups' accumulators exchanged with v_permlane32_swap (only the registers the
+    fold reads) so that every lane holds its own 32 column sums, and the lane folds them into 28-bit limbs:
+    one v_mad_i64_i32 per (paired) column (x 2^sh), one mask and one arithmetic shift per limb, the carry
+    entering the next limb's first multiply-add;
+  * the limbs that only feed the matrix cores (the upper product halves, q3) are produced with their operand
+    bytes already XORed with 0x80 (v_bitop3_b32), so packing them costs no XOR.
 
 Product 1 forms columns 112..271 of q1 mu and yields q3 = Barrett's quotient estimate or one less (q3 is
 clamped to 0 when q1 = 0); product 2 forms columns 0..129 of q3 P (as matrix columns 1..130, the constant
@@ -36,24 +39,29 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gen_montprog import _descriptor  # noqa: E402
 
 # A/B variants for tools/build_m37_ab.sh only (fedtree_amd/build.py clears the switch): the timing-only ones
-# give wrong results (noswap, nonop, nomfma); nodbuf / nointerleave / nopair / nodesync are correct schedules
+# give wrong results (noswap, nonop, nomfma); the others are correct schedules: nodbuf, nointerleave, nopair,
+# noprepair, nodesync, spill, pingpong[,ppodd], col3 / col4, marginN, prioN / noprio, noprexor, nocmerge
 AB = os.environ.get("FTHE_GEN_M37_AB", "")
 TILE_OFF = 512                  # byte offset of the tile image in ctx
 TILE_BYTES = 20 * 1024          # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
 SPILL_BYTES = 10 * 1024         # per wave: V[37..73] while Barrett 1 runs (9 x dwordx4 + 1 dword per lane)
 SPILL = "spill" in AB           # measured: no gain (profiles/r02zzi_spill_ab.jsonl), so off
+# ping-pong halves in 512-thread workgroups (s_barrier between products and reduction): no gain
+# (profiles/r03t_m37_pingpong_ab.jsonl), so off
 PP = "pingpong" in AB
 # VALU instructions kept between a tile's last MFMA and the lane exchange that reads its results (>= 24: the
-# 8-pass XDL -> VALU hazard then needs no s_nop); A/B knob marginN
+# 8-pass XDL -> VALU hazard then needs no s_nop); A/B knob marginN (24..90 within noise,
+# profiles/r03zj_m37_margin_ab.jsonl)
 MARGIN = next((int(t[6:]) for t in AB.split(',') if t.startswith('margin') and t[6:].isdigit()), 30)
 assert MARGIN >= 24
-# PREXOR: the limbs that only ever reach the matrix cores (the upper product halves and q3) leave the
-# column tails / chunk folds with bit 7 of every byte already flipped (v_bitop3_b32 (x & mask) ^ pattern
-# in place of the mask), so packing them into the b ^ 0x80 operand bytes needs no v_xor per dword
-# chunk carry enters the next chunk's first multiply-add (no carry add): 162 fewer VALU per squaring,
-# 69.8-70.5 vs 71.7-72.9 ms (profiles/r03za_m37_cmerge_ab.jsonl); nocmerge restores the deferred carry add
+# the limbs that only ever reach the matrix cores (the upper product halves and q3) leave the column tails /
+# chunk folds with bit 7 of every byte already flipped (v_bitop3_b32 (x & mask) ^ pattern in place of the
+# mask), so packing them into the b ^ 0x80 operand bytes needs no v_xor per dword: 128 fewer VALU per
+# squaring, 71.7-72.2 vs 73.0-73.5 ms (profiles/r03y_m37_prexor_ab.jsonl)
+PREXOR = "noprexor" not in AB
+# a chunk's carry enters the next chunk's first multiply-add (no carry add in its tail): 162 fewer VALU per
+# squaring, 69.8-70.5 vs 71.7-72.9 ms (profiles/r03za_m37_cmerge_ab.jsonl)
 CMERGE = "nocmerge" not in AB
-PREXOR = "noprexor" not in AB   # default: 128 fewer VALU per squaring, 72.5 vs 73.3 ms (profiles/r03y_m37_prexor_ab.jsonl)
 LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
 QBIT = 28 * 38                  # q3 = floor(N / 2^1064)
@@ -101,7 +109,7 @@ def gen_padic_mfma(name: str) -> str:
     D = [f"v{XB + i}" for i in range(40)]
     # ---- SGPR plan ---------------------------------------------------------
     # s[0:1] kernarg, s2 wg id, s[2:3] call target, s[4:5] slots, s[6:7] prog, s[8:9] ctx, s10 limb
-    # stride, s11 slot stride, s[12:13] return address, s[14:15] op/arg, s[16:17] addr, s19 counter;
+    # stride, s11 slot stride, s[12:13] return address, s[14:15] op/arg, s[16:17] addr, s18 half (PP), s19 counter;
     # s20..s27 = 2^0, 2^4, .., 2^28; s28..s34 = -2^0, .., -2^24; -P limbs from s36
     SPOW, SNEG, SNP = 20, 28, 36                   # s35 = 0x0fffffff
     NSGPR = SNP + K
