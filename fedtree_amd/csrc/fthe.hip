@@ -1490,8 +1490,9 @@ int end_call(fthe_ctx *c, Launch &Lc) {
 }
 
 // Host-resident calls: chunked, double-buffered transfers through pinned
-// staging on the context's copy stream.  Chunk i+1's input is staged and
-// chunk i's output drained while the kernels of the neighbouring chunk run,
+// staging on the context's copy stream.  Chunk i+1's input is staged (ahead of
+// chunk i's output on the copy stream) and chunk i's output drained while the
+// kernels of the neighbouring chunk run,
 // so a host-to-host call costs ~max(compute, PCIe + host memcpy) rather than
 // their sum.  Caller buffers that are already page-locked are DMA'd directly.
 // Large host copies (pageable caller buffer <-> pinned staging) on several cores.
@@ -1582,6 +1583,11 @@ struct HostPipe {
     int after(size_t off, size_t cnt) {
         int rc;
         const int sl = (int)((off / L) & 1);
+        // the next chunk's input first: on the copy stream it must not queue behind this chunk's output
+        // drain, which waits for this chunk's kernels -- the next chunk's kernels wait for their input, so
+        // the other order serialised every D2H with the compute (3.5 ms of idle GPU per 393,216-row chunk,
+        // profiles/r03zl_e2e_timeline.txt)
+        if ((rc = stage(off + L))) return rc;
         if (nout) {
             HIPOK(hipEventRecord(c->ev_done[sl], c->stream));
             HIPOK(hipStreamWaitEvent(c->copy, c->ev_done[sl], 0));
@@ -1597,7 +1603,6 @@ struct HostPipe {
             }
             HIPOK(hipEventRecord(c->ev_copied[sl], c->copy));
         }
-        if ((rc = stage(off + L))) return rc;       // next chunk's input, behind this chunk's compute
         if ((rc = finish_pending())) return rc;      // previous chunk's output -> caller
         if (nout) { pend = true; pend_slot = sl; pend_off = off; pend_cnt = cnt; }
         return FTHE_OK;
