@@ -1518,6 +1518,11 @@ struct HostPipe {
     Out out[2]; int nout = 0;
     size_t L = 0, count = 0;
     bool pend = false; int pend_slot = 0; size_t pend_off = 0, pend_cnt = 0;
+    // compute-bound calls (encrypt, decrypt): the next chunk's input goes on the copy stream ahead of this
+    // chunk's output drain, so the next kernels never wait behind a D2H.  Copy-bound calls (add / sub:
+    // 1.5 KB of PCIe per product) keep the drain first, so the DMA engine works while the host copies the
+    // next chunk into pinned staging.
+    bool input_first = true;
     static bool is_pinned(const void *p) {
         hipPointerAttribute_t a;
         if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
@@ -1587,7 +1592,7 @@ struct HostPipe {
         // drain, which waits for this chunk's kernels -- the next chunk's kernels wait for their input, so
         // the other order serialised every D2H with the compute (3.5 ms of idle GPU per 393,216-row chunk,
         // profiles/r03zl_e2e_timeline.txt)
-        if ((rc = stage(off + L))) return rc;
+        if (input_first && (rc = stage(off + L))) return rc;
         if (nout) {
             HIPOK(hipEventRecord(c->ev_done[sl], c->stream));
             HIPOK(hipStreamWaitEvent(c->copy, c->ev_done[sl], 0));
@@ -1603,6 +1608,7 @@ struct HostPipe {
             }
             HIPOK(hipEventRecord(c->ev_copied[sl], c->copy));
         }
+        if (!input_first && (rc = stage(off + L))) return rc;
         if ((rc = finish_pending())) return rc;      // previous chunk's output -> caller
         if (nout) { pend = true; pend_slot = sl; pend_off = off; pend_cnt = cnt; }
         return FTHE_OK;
@@ -3905,6 +3911,7 @@ static int pair_host(fthe_key *k, fthe_ctx *c, const uint32_t *a, const uint32_t
     }
     for (int i = 0; i < 3; i++) if ((rc = c->io[i].ensure(std::max<size_t>(4, count * row)))) return rc;
     HostPipe pipe{c};
+    pipe.input_first = false;                    // PCIe-bound: keep the DMA engine busy during host copies
     pipe.add_in(a, c->io[0].p, row);
     pipe.add_in(b, c->io[1].p, row);
     pipe.add_out(out, c->io[2].p, row);
