@@ -1,6 +1,7 @@
 """Driver for a timeline of the host-resident encrypt (bench.py's e2e_host_encrypt_pinned_per_s): one warm
-call, then fthe_encrypt_u64 of N gradient plaintexts from page-locked host memory into page-locked host rows.
-    rocprofv3 --kernel-trace --memory-copy-trace --stats -d DIR -- python3 tools/e2e_trace.py [N]"""
+call, then fthe_encrypt_u64 of N gradient plaintexts from page-locked host memory into page-locked host rows,
+then the device-resident encrypt and (mode dec) three device-resident CRT decrypts of the same N ciphertexts.
+    rocprofv3 --kernel-trace --memory-copy-trace --stats -d DIR -- python3 tools/e2e_trace.py [N] [dec]"""
 import ctypes
 import json
 import os
@@ -39,6 +40,15 @@ def main():
         dev.sync()
         res[f"device_s_{rep}"] = round(time.perf_counter() - t0, 4)
     res["same"] = bool(torch.equal(cd.cpu(), cp))
+    if len(sys.argv) > 2 and sys.argv[2] == "dec":
+        low = torch.empty(ne, dtype=torch.int64, device="cuda")
+        for rep in range(3):
+            dev.sync()
+            t0 = time.perf_counter()
+            pl.decrypt_u64_dev(cd, low)
+            dev.sync()
+            res[f"decrypt_device_s_{rep}"] = round(time.perf_counter() - t0, 4)
+        res["decrypt_ok"] = bool(torch.equal(low.cpu(), torch.from_numpy(mh.view(np.int64))))
     print(json.dumps(res), flush=True)
 
 
