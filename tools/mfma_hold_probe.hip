@@ -119,6 +119,43 @@ __global__ __launch_bounds__(256) void chains(unsigned long long *out, int iters
     if (s == 7) out[0] = 0;
 }
 
+
+// one wave per SIMD: MFMA + 6 fillers per gap, dependent (one register) or independent (six registers)
+#define IND6(a, b, c, d, e, f) a "\n" b "\n" c "\n" d "\n" e "\n" f "\n"
+#define DEP_KERNEL(NAME, FILL)                                                                           \
+__global__ __launch_bounds__(256) void NAME(unsigned long long *out, int iters, int seed) {              \
+    v4i a = {seed, seed + 1, seed + 2, (int)threadIdx.x}, b = a;                                          \
+    v16i c0 = {}, c1 = {};                                                                               \
+    unsigned long long m0 = threadIdx.x, m1 = 1, m2 = 2, m3 = 3, m4 = 4, m5 = 5;                        \
+    unsigned x = seed * 3 + 1, y = threadIdx.x ^ 5;     /* not the MFMA operands */                                                                  \
+    unsigned long long t0 = __builtin_readcyclecounter();                                              \
+    for (int i = 0; i < iters; i++) {                                                                     \
+        asm volatile("v_mfma_i32_32x32x32_i8 %[c0], %[a], %[b], %[c0]\n" FILL                           \
+                     "v_mfma_i32_32x32x32_i8 %[c1], %[a], %[b], %[c1]\n" FILL                           \
+                     "v_mfma_i32_32x32x32_i8 %[c0], %[a], %[b], %[c0]\n" FILL                           \
+                     "v_mfma_i32_32x32x32_i8 %[c1], %[a], %[b], %[c1]\n" FILL                           \
+                     : [c0] "+v"(c0), [c1] "+v"(c1), [m0] "+v"(m0), [m1] "+v"(m1), [m2] "+v"(m2),        \
+                       [m3] "+v"(m3), [m4] "+v"(m4), [m5] "+v"(m5)                                       \
+                     : [a] "v"(a), [b] "v"(b), [x] "v"(x), [y] "v"(y) : "vcc");                           \
+    }                                                                                                     \
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");                                            \
+    unsigned long long t1 = __builtin_readcyclecounter();                                              \
+    int s = 0;                                                                                           \
+    for (int k = 0; k < 16; k++) s += c0[k] + c1[k];                                                     \
+    if ((threadIdx.x & 63) == 0) out[blockIdx.x * 4 + threadIdx.x / 64] = t1 - t0;                       \
+    if (s == 0x12345 && m0 + m1 + m2 + m3 + m4 + m5 == 7) out[0] = 0;                                    \
+}
+#define MADR(r) "v_mad_u64_u32 %[" #r "], vcc, %[x], %[y], %[" #r "]"
+DEP_KERNEL(d_mad6_dep, IND6(MADR(m0), MADR(m0), MADR(m0), MADR(m0), MADR(m0), MADR(m0)))
+DEP_KERNEL(d_mad6_ind, IND6(MADR(m0), MADR(m1), MADR(m2), MADR(m3), MADR(m4), MADR(m5)))
+DEP_KERNEL(d_mad6_two, IND6(MADR(m0), MADR(m1), MADR(m0), MADR(m1), MADR(m0), MADR(m1)))
+DEP_KERNEL(d_mad12_dep, IND6(MADR(m0), MADR(m0), MADR(m0), MADR(m0), MADR(m0), MADR(m0))
+                        IND6(MADR(m0), MADR(m0), MADR(m0), MADR(m0), MADR(m0), MADR(m0)))
+DEP_KERNEL(d_mad12_two, IND6(MADR(m0), MADR(m1), MADR(m0), MADR(m1), MADR(m0), MADR(m1))
+                        IND6(MADR(m0), MADR(m1), MADR(m0), MADR(m1), MADR(m0), MADR(m1)))
+DEP_KERNEL(d_mad12_ind, IND6(MADR(m0), MADR(m1), MADR(m2), MADR(m3), MADR(m4), MADR(m5))
+                        IND6(MADR(m0), MADR(m1), MADR(m2), MADR(m3), MADR(m4), MADR(m5)))
+
 static double mean_cycles(const std::vector<unsigned long long> &v, int stride, int lo, int hi) {
     double s = 0; int n = 0;
     for (size_t i = 0; i < v.size(); i++) if ((int)(i % stride) >= lo && (int)(i % stride) < hi) { s += (double)v[i]; n++; }
@@ -169,5 +206,15 @@ int main() {
                mean_cycles(v, 4, 0, 4) / (64.0 * (iters / 4)));
     };
     runc(chains<1>, 1); runc(chains<2>, 2); runc(chains<3>, 3); runc(chains<4>, 4); runc(chains<8>, 8);
+    auto rund = [&](auto kern, const char *name) {
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 96 * 1024, 0, d, iters / 2, 3);
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 96 * 1024, 0, d, iters / 2, 3);
+        if (hipMemcpy(h.data(), d, nb * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) exit(1);
+        std::vector<unsigned long long> v(h.begin(), h.begin() + nb * 4);
+        printf("{\"test\": \"chain_shape\", \"kind\": \"%s\", \"cycles_per_mfma_gap\": %.2f}\n", name,
+               mean_cycles(v, 4, 0, 4) / (4.0 * (iters / 2)));
+    };
+    rund(d_mad6_dep, "6 mads, one chain"); rund(d_mad6_two, "6 mads, two chains"); rund(d_mad6_ind, "6 mads, six chains");
+    rund(d_mad12_dep, "12 mads, one chain"); rund(d_mad12_two, "12 mads, two chains"); rund(d_mad12_ind, "12 mads, six chains");
     return 0;
 }
