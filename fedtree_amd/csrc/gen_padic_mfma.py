@@ -40,7 +40,8 @@ from gen_montprog import _descriptor  # noqa: E402
 
 # A/B variants for tools/build_m37_ab.sh only (fedtree_amd/build.py clears the switch): the timing-only ones
 # give wrong results (noswap, nonop, nomfma); the others are correct schedules: nodbuf, nointerleave, nopair,
-# noprepair, nodesync, spill, pingpong[,ppodd], col3 / col4, marginN, prioN / noprio, noprexor, nocmerge
+# noprepair, nodesync, spill, pingpong[,ppodd], col3 / col4, marginN, prioN / noprio, noprexor, nocmerge,
+# ldsx[,ldsxa]
 AB = os.environ.get("FTHE_GEN_M37_AB", "")
 TILE_OFF = 512                  # byte offset of the tile image in ctx
 TILE_BYTES = 20 * 1024          # 19 tiles of 1 KB, padded to 5 dwordx4 per thread
@@ -62,7 +63,18 @@ PREXOR = "noprexor" not in AB
 # a chunk's carry enters the next chunk's first multiply-add (no carry add in its tail): 162 fewer VALU per
 # squaring, 69.8-70.5 vs 71.7-72.9 ms (profiles/r03za_m37_cmerge_ab.jsonl)
 CMERGE = "nocmerge" not in AB
-LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0)
+# ldsx: the B operands' lane-half exchange through LDS (each half writes the 4 dwords per K-block the other half
+# needs under a half EXEC mask and reads the partner's back) instead of 20 v_permlane32_swap per product, which
+# cost 8 issue cycles each (profiles/r03zr_mfma_hold_probe.jsonl).  Measured slower: 72.1-72.4 vs 70.9-71.0 ms,
+# with ldsxa 74.6-75.3 (profiles/r03zs_m37_ldsx_ab.jsonl): the stores' VGPR transfer and the round trip the
+# wave waits out cost more than the swaps, so off
+LDSX = "ldsx" in AB
+# ldsxa (with ldsx): also the accumulator exchange of every fully paired M-tile (8 of a Barrett's 10): the 8
+# pairs packed into the tile's first 8 accumulator registers, 2 dwordx4 per half through LDS for 8 swaps
+LDSXA = LDSX and "ldsxa" in AB
+LDSX_BYTES = 5 * 1024           # per wave: 5 K-blocks x 64 lanes x 16 B
+assert not (LDSX and (PP or SPILL))
+LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0) + (4 * LDSX_BYTES if LDSX else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
 QBIT = 28 * 38                  # q3 = floor(N / 2^1064)
 TILE_D1 = (-3, -2, -1, 0, 1)    # product-1 Toeplitz tiles (k <= 3) by m - k; then k = 4 for m = 0..4
@@ -97,6 +109,9 @@ def gen_padic_mfma(name: str) -> str:
     PATV = (249, 250)                            # PREXOR: byte-flip patterns of even / odd limbs
     assert not (SPILL and PREXOR)
     NVGPR = 250 if SPILL else 251 if PREXOR else 249
+    V_XW, V_XR = NVGPR, NVGPR + 1                # LDSX: this wave's exchange area + lane * 16, and ^ 512
+    if LDSX:
+        NVGPR += 2
 
     def pat(t):
         """flip pattern of limb t of a packed number (limb t at bit 28 t): bits j with 28 t + j = 7 mod 8"""
@@ -113,6 +128,9 @@ def gen_padic_mfma(name: str) -> str:
     # s20..s27 = 2^0, 2^4, .., 2^28; s28..s34 = -2^0, .., -2^24; -P limbs from s36
     SPOW, SNEG, SNP = 20, 28, 36                   # s35 = 0x0fffffff
     NSGPR = SNP + K
+    SLO, SHI = 74, 76                            # LDSX: EXEC masks of lanes 0-31 / 32-63
+    if LDSX:
+        NSGPR = SHI + 2
     POW = lambda sh: f"s{SPOW + sh // 4}"
     NEG = lambda sh: f"s{SNEG + sh // 4}"
     NP = lambda j: f"s{SNP + j}"
@@ -279,6 +297,24 @@ def gen_padic_mfma(name: str) -> str:
                 e(f'  v_xor_b32_e32 {d}, {hex(xor_masks[w])}, {d}')
 
     def swap_operands():
+        if LDSX:
+            # lane r + 32's D[8k + j] <-> lane r's D[8k + 4 + j], as the swaps below; LDS executes one wave's
+            # operations in order, and the last one (K-block 4) is never the first tile's first K-block, which
+            # issue_tile's lgkmcnt counts then leave the only exchange operation possibly still in flight
+            lo, hi = f"s[{SLO}:{SLO + 1}]", f"s[{SHI}:{SHI + 1}]"
+            e(f'  s_mov_b64 exec, {lo}')
+            for k in range(5):
+                e(f'  ds_write_b128 v{V_XW}, v[{XB + 8 * k + 4}:{XB + 8 * k + 7}] offset:{1024 * k}')
+            e(f'  s_mov_b64 exec, {hi}')
+            for k in range(5):
+                e(f'  ds_write_b128 v{V_XW}, v[{XB + 8 * k}:{XB + 8 * k + 3}] offset:{1024 * k}')
+            for k in range(5):
+                e(f'  ds_read_b128 v[{XB + 8 * k}:{XB + 8 * k + 3}], v{V_XR} offset:{1024 * k}')
+            e(f'  s_mov_b64 exec, {lo}')
+            for k in range(5):
+                e(f'  ds_read_b128 v[{XB + 8 * k + 4}:{XB + 8 * k + 7}], v{V_XR} offset:{1024 * k}')
+            e('  s_mov_b64 exec, -1')
+            return
         e('  s_nop 1')
         for k in range(5):
             for j in range(4):
@@ -341,6 +377,10 @@ def gen_padic_mfma(name: str) -> str:
                 swaps.append(rr)
         return paired, swaps
 
+    def compact(tile):
+        """LDSXA: all 8 even rr paired, the pairs then sit in rr / 2 and move through LDS"""
+        return LDSXA and plan(consumed(*tile))[0] == set(range(0, 16, 2))
+
     def exchange(G0x, G1x, waited=False, tile=None):
         """results -> VALU: wait out the last MFMA writing them (8-pass XDL: 11 wait states on gfx950), pair
         adjacent rows (plan), then exchange the halves of the registers still needed; waited: at least 30
@@ -350,6 +390,27 @@ def gen_padic_mfma(name: str) -> str:
             e('  s_nop 7')
             e('  s_nop 7')
         paired, swaps = plan(consumed(*tile))
+        if compact(tile):
+            for rr in range(0, 16, 2):
+                for G in (G0x, G1x):
+                    e(f'  v_lshl_add_u32 v{G + rr // 2}, v{G + rr + 1}, 8, v{G + rr}')
+            # lanes 0-31 send the group-1 pairs and receive the partner's group-0 pairs into them, lanes
+            # 32-63 the other way round (the permlane32_swap of every pair register, as below)
+            lo, hi = f"s[{SLO}:{SLO + 1}]", f"s[{SHI}:{SHI + 1}]"
+            e(f'  s_mov_b64 exec, {lo}')
+            for j in range(2):
+                e(f'  ds_write_b128 v{V_XW}, v[{G1x + 4 * j}:{G1x + 4 * j + 3}] offset:{1024 * j}')
+            e(f'  s_mov_b64 exec, {hi}')
+            for j in range(2):
+                e(f'  ds_write_b128 v{V_XW}, v[{G0x + 4 * j}:{G0x + 4 * j + 3}] offset:{1024 * j}')
+            for j in range(2):
+                e(f'  ds_read_b128 v[{G0x + 4 * j}:{G0x + 4 * j + 3}], v{V_XR} offset:{1024 * j}')
+            e(f'  s_mov_b64 exec, {lo}')
+            for j in range(2):
+                e(f'  ds_read_b128 v[{G1x + 4 * j}:{G1x + 4 * j + 3}], v{V_XR} offset:{1024 * j}')
+            e('  s_mov_b64 exec, -1')
+            e('  s_waitcnt lgkmcnt(0)')
+            return
         for rr in sorted(paired):
             for G in (G0x, G1x):
                 e(f'  v_lshl_add_u32 v{G + rr}, v{G + rr + 1}, 8, v{G + rr}')
@@ -363,12 +424,16 @@ def gen_padic_mfma(name: str) -> str:
         """(output column, register, pre-paired) of M-tile m in column order, after exchange()"""
         C = consumed(prod, m)
         paired, _ = plan(C)
+        cp = compact((prod, m))
         out = []
         for rho in sorted(C):
             rr = (rho & 3) + 4 * (rho >> 3)
             if rho % 2 and rr - 1 in paired:
                 continue                              # folded into rho - 1 before the exchange
-            out.append((s_of(rho), creg(rho), rho % 2 == 0 and rr in paired))
+            src = rho
+            if cp:                                    # the pair of rr sits in rr / 2 of the same group
+                src = (rr // 2 & 3) + 8 * (rr // 2 >> 2) + 4 * (rho >> 2 & 1)
+            out.append((s_of(rho), creg(src), rho % 2 == 0 and rr in paired))
         return out
 
     def mtile_mfmas(prod, m, ks, nxt=None):
@@ -534,6 +599,7 @@ def gen_padic_mfma(name: str) -> str:
 
     P1_TILES = [(1, m, [k for k in range(5) if m - k <= 1]) for m in range(5)]
     P2_TILES = [(2, m, [k for k in range(5) if m >= k]) for m in range(5)]
+    assert P1_TILES[0][2][0] != 4 and P2_TILES[0][2][0] != 4      # LDSX: see swap_operands
 
     def mfma_barrett(Tl, q3out, clamp, prefetched=False, dbuf=False, setb=None, pre_in=None):
         """product 1: q3 = Barrett's quotient of T (Tl: 2K limbs, Tl[K-1] < 2^29 allowed) -> q3out (K regs,
@@ -648,6 +714,16 @@ def gen_padic_mfma(name: str) -> str:
         e(f'  v_mul_u32_u24_e32 v{V_SPILL}, {hex(SPILL_BYTES)}, v{V_SPILL}')
         e(f'  v_add_u32_e32 v{V_SPILL}, {hex(TILE_BYTES)}, v{V_SPILL}')
         e(f'  v_add_u32_e32 v{V_SPILL}, v{V_SPILL}, v{V_LDS}')
+    if LDSX:
+        e(f'  v_lshrrev_b32_e32 v{V_XW}, 6, v{V_TID}')                # wave in the workgroup
+        e(f'  v_mul_u32_u24_e32 v{V_XW}, {hex(LDSX_BYTES)}, v{V_XW}')
+        e(f'  v_add_u32_e32 v{V_XW}, {hex(TILE_BYTES)}, v{V_XW}')
+        e(f'  v_add_u32_e32 v{V_XW}, v{V_XW}, v{V_LDS}')
+        e(f'  v_xor_b32_e32 v{V_XR}, 0x200, v{V_XW}')                # lane ^ 32
+        e(f'  s_mov_b32 s{SLO}, -1')
+        e(f'  s_mov_b32 s{SLO + 1}, 0')
+        e(f'  s_mov_b32 s{SHI}, 0')
+        e(f'  s_mov_b32 s{SHI + 1}, -1')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
     if PP:
