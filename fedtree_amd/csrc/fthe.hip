@@ -43,18 +43,20 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 8;
+constexpr int MAX_VARIANTS = 9;
 // s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency);
 // 1000 + K: the P-adic exponentiation kernels mod P^2 (gen_padic.py, digits of K limbs, slots of 2K
 // limbs; the "S" here only names the variant): K = 37 runs on the s74 slots of Paillier-2048,
 // K = 19 on slots of its own (38 limbs) for Paillier-1024;
 // 1137: the K = 37 P-adic kernel with matrix-core (MFMA) Barrett reductions (gen_padic_mfma.py), same
 // slots and programs, no fixed-base table ops;
-// 2000 + 76: the n-adic four-lane kernel (gen_nadic.py, base-n digits of 76 limbs) on the s152 slots
-constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19, kNadicS = 2076, kPadicMfmaS = 1137;
+// 2000 + 76: the n-adic four-lane kernel (gen_nadic.py, base-n digits of 76 limbs) on the s152 slots;
+// 2100 + 76: its Montgomery form (gen_nadic.py mont: LSB-first reductions, no quotient estimates)
+constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19, kNadicS = 2076, kPadicMfmaS = 1137,
+              kNadicMontS = 2176;
 const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4},
                                        {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}, {kNadicS, 27, 4},
-                                       {kPadicMfmaS, 28, 1}};
+                                       {kPadicMfmaS, 28, 1}, {kNadicMontS, 27, 4}};
 constexpr Shape kLatShape{80, 27, 4};
 constexpr int kAddbBlob = 3152;           // fthe_addb_q152's code object in gen/montprog_blobs.h
 
@@ -316,6 +318,11 @@ struct fthe_key {
     bool nadic = false;
     DevMod mnA;                     // m: n^2 on the s152 slot shape; ctx: n on 76 limbs of 27 bits
     int c_n76 = -1;                 // n in 76 limbs (the output c = x0 + x1 n)
+    // the Montgomery form of the n-adic kernel (default; FTHE_NADIC_CLASSICAL=1 keeps the classical one):
+    // ctx as mnA's (n limbs, n' at word 76); K = R^(n+1) mod n^2 as digits (K mod n, K div n), R = 2^2052
+    bool nadic_mont = false;
+    DevMod mnM;
+    int c_Kn = -1;
     // Paillier-1024 public-key encrypt (n of 1009..1030 bits) on the P-adic kernel with P = n
     bool padic_pub = false;
     DevMod mnP;
@@ -335,7 +342,7 @@ struct fthe_key {
     int pq_w = 0;
     ~fthe_key() {
         co.reset();
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA, &mnP})
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA, &mnP, &mnM})
             if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
@@ -382,6 +389,7 @@ struct fthe_key {
     PH prP_enc_p, prP_enc_q, prP_encB_p, prP_encB_q, prP_encB_p_nt;
     PH prP_dec_pre_p, prP_dec_pre_q, prP_dec_p, prP_dec_q, prP_dec_post_p, prP_dec_post_q;
     PH prN_enc_pub;                  // n-adic form of the public-key encrypt
+    PH prM_enc_pub;                  // its Montgomery form (fthe_nadic_m76)
     PH prP_enc_pub;                  // P-adic form (P = n) of the Paillier-1024 public-key encrypt
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
@@ -500,7 +508,8 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         if (!blob) return FTHE_ERR_HIP;
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
-        if (kVariants[i].S > 2000) snprintf(name, sizeof name, "fthe_nadic_q%d", kVariants[i].S - 2000);
+        if (kVariants[i].S > 2100) snprintf(name, sizeof name, "fthe_nadic_m%d", kVariants[i].S - 2100);
+        else if (kVariants[i].S > 2000) snprintf(name, sizeof name, "fthe_nadic_q%d", kVariants[i].S - 2000);
         else if (kVariants[i].S > 1100) snprintf(name, sizeof name, "fthe_padic_m%d", kVariants[i].S - 1100);
         else if (kVariants[i].S > 1000) snprintf(name, sizeof name, "fthe_padic_k%d", kVariants[i].S - 1000);
         else snprintf(name, sizeof name, "fthe_montprog_s%d", kVariants[i].S);
@@ -766,6 +775,31 @@ static int key_finish(fthe_key *k) {
             h.alg = nadic_alg(x, k->n);
             h.exec = nadic_exec(x);
             k->prN_enc_pub = h;
+            // Montgomery form (tools/nadic_mont_model.py): the raw r is a Montgomery residue (value r R^-1),
+            // pow(n) gives r^n R^(1-n), MUL (1, m) and MUL K (slot C2) give (1 + m n) r^n; digits < 2n
+            // between products, CANON at the end
+            k->nadic_mont = !getenv("FTHE_NADIC_CLASSICAL");
+            if (k->nadic_mont) {
+                if ((rc = upload_nadic(k->mnM, k->n, k->n2, k->sn2))) return rc;
+                k->mnM.kernel_S = kNadicMontS;
+                Mpz Kc, R, e1, q0, q1;
+                mpz_set_ui(R, 1); mpz_mul_2exp(R, R, (mp_bitcnt_t)kNadicDigit.B * kNadicDigit.S);
+                mpz_add_ui(e1, k->n, 1);
+                mpz_powm(Kc, R, e1, k->n2);
+                mpz_fdiv_qr(q1, q0, Kc, k->n);
+                std::vector<uint32_t> kl = to_limbs(q0, kNadicDigit.S, kNadicDigit.B);
+                std::vector<uint32_t> kh = to_limbs(q1, kNadicDigit.S, kNadicDigit.B);
+                kl.insert(kl.end(), kh.begin(), kh.end());
+                k->c_Kn = k->add_const(kl);
+                Prog y;
+                y.loadx(SL_IN0); y.canon();
+                y.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
+                y.mul(SL_C1); y.mul(SL_C2); y.canon(); y.storex(SL_OUTP); y.end();
+                fthe_key::PH hm = k->add_prog(y);
+                hm.alg = nadic_alg(y, k->n);
+                hm.exec = nadic_exec(y);
+                k->prM_enc_pub = hm;
+            }
         }
         // Paillier-1024 (n of 1009..1030 bits, n^2 on the s74 slots): the P-adic kernel with P = n -- the
         // base-n digit arithmetic needs no factorisation.  X = r -> digits (LOADP), X^n, X (1 + m n) with the
@@ -1863,7 +1897,10 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             pack_rows(c->stream, rw, rwn, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
             Lc.fill(SL_C1, k->c_one_n2);
             m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_C1) + (size_t)D * L, D, L, Lc.B);
-            if ((rc = Lc.prog(k->prN_enc_pub, k->mnA))) return rc;
+            if (k->nadic_mont) {
+                Lc.fill(SL_C2, k->c_Kn);
+                if ((rc = Lc.prog(k->prM_enc_pub, k->mnM))) return rc;
+            } else if ((rc = Lc.prog(k->prN_enc_pub, k->mnA))) return rc;
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTP), D, k->cst(k->c_n76), D,
                         Lc.slot(SL_OUTP) + (size_t)D * L, D, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
         } else if (k->padic_pub) {

@@ -44,7 +44,11 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from gen_montprog import QUAD_ROWB, _descriptor  # noqa: E402
 
 
-def gen_nadic(S: int, B: int, name: str) -> str:
+def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
+    """mont: the Montgomery form (fthe_nadic_m76, tools/nadic_mont_model.py) -- each product
+    Mont(X, Y) = X Y R^-1 mod n^2 (R = 2^(B S)) as two interleaved LSB-first Montgomery reductions mod n,
+    q = col0 n' mod 2^B on lane 0 instead of the classical form's f64 quotient estimates and overflow
+    folds; digits stay in [0, 2n) between products (no conditional subtraction), CANON reduces them."""
     assert S % 4 == 0
     Q = S // 4
     MASK = (1 << B) - 1
@@ -106,6 +110,8 @@ def gen_nadic(S: int, B: int, name: str) -> str:
     e('  s_mov_b32 s23, 0x11111111')
     e('  s_waitcnt lgkmcnt(0)')
     e(f'  s_load_dwordx8 s[36:43], s[8:9], {hex(4 * (S + 1))}')   # -k1, -k2, -k3, bias (doubles)
+    if mont:
+        e(f'  s_load_dword s44, s[8:9], {hex(4 * S)}')                # n' = -n^-1 mod 2^B
     # ROW = g*512 + k*128 = wg*32768 + tid*128 (g = wg*64 + tid>>2, k = tid & 3)
     e('  s_lshl_b32 s14, s2, 15')
     e(f'  v_lshlrev_b32_e32 v{V_ROW}, 7, v{V_TID}')
@@ -266,6 +272,8 @@ def gen_nadic(S: int, B: int, name: str) -> str:
         ripple_quad(X1)
     carry_into_x1_col(add_x1_limb0)
     canon_once(X1, 'cx1')
+    if mont:                                     # x1 < 2n + 1 after the carry: a second round
+        canon_once(X1, 'cx1b')
     e('  s_branch .Lprog')
 
     # ---- A operand -> LDS ------------------------------------------------------------
@@ -338,12 +346,19 @@ def gen_nadic(S: int, B: int, name: str) -> str:
         e('  s_mov_b32 s19, 0')
         e('  s_branch .Lprod_mul')
 
+    # FTHE_GEN_NADIC_AB=dbl (Montgomery form): a squaring also writes 2 x0 into rows S.. and window 2 reads its
+    # multiplier limb from there (one LDS read per step instead of a VALU doubling)
+    dbl = mont and "dbl" in os.environ.get("FTHE_GEN_NADIC_AB", "").split(",")
     e('.Lsqr:')
     e('  s_mov_b32 s19, s15')
     e('.Lsqr_loop:')
     e('  s_cmp_eq_u32 s19, 0')
     e('  s_cbranch_scc1 .Lprog')
     write_rows(X0, 0)
+    if dbl:
+        for j in range(Q):                       # the rings are free between products
+            e(f'  v_lshlrev_b32_e32 v{TB1 + j}, 1, {X0(j)}')
+        write_rows(lambda j: f"v{TB1 + j}", S)
     e('  s_branch .Lprod_sq')
 
     # ---- the fused product ------------------------------------------------------------
@@ -528,8 +543,122 @@ def gen_nadic(S: int, B: int, name: str) -> str:
         e('  s_sub_u32 s19, s19, 1')
         e('  s_branch .Lsqr_loop')
 
-    emit_product(True)
-    emit_product(False)
+    # ---- the Montgomery fused product (mont) -------------------------------------------------
+    def emit_product_mont(sq):
+        """LSB-first: step i takes multiplier limb i (rows i, S + i), per window 19 + 19 multiply-adds per
+        lane, q from lane 0's lowest column (v_mul_lo_u32 by n', mask, DPP broadcast), then every lane
+        splits its lowest column, keeps hi in its next column and hands lo to the lane below as that
+        lane's new top column (gen_montprog.py gen_quad's step; lane 0's lo is 0).  Window 2 takes -q1
+        into its lowest column (lane 0) and its columns are signed (arithmetic split).  Rings of NTC
+        pairs per window: position k at step u in pair (u + k) mod NTC."""
+        lab = '.Lprod_sq' if sq else '.Lprod_mul'
+        NT = NTC
+        assert NT % 2 == 0 and NT >= Q + 1
+
+        def T(tb, k):
+            k %= NT
+            return f"v[{tb + 2 * k}:{tb + 2 * k + 1}]"
+
+        def Tlo(tb, k):
+            return f"v{tb + 2 * (k % NT)}"
+
+        def Thi(tb, k):
+            return f"v{tb + 2 * (k % NT) + 1}"
+
+        tmp2 = f"v[{DF0}:{DF0 + 1}]"
+
+        def reduce_split(tb, qreg, t, shr):
+            for j in range(Q):
+                e(f'  v_mad_u64_u32 {T(tb, u_[0] + j)}, vcc, v{qreg}, {NV(j)}, {T(tb, u_[0] + j)}')
+                if j == 3:
+                    e(f'  {shr} {t}, {B}, {T(tb, u_[0])}')
+                if j == 9:
+                    e(f'  v_lshl_add_u64 {T(tb, u_[0] + 1)}, {t}, 0, {T(tb, u_[0] + 1)}')
+                if j == 12:
+                    e(f'  v_and_b32_e32 {Tlo(tb, u_[0])}, {hex(MASK)}, {Tlo(tb, u_[0])}')
+            e(f'  v_mov_b32_dpp {Tlo(tb, u_[0] + Q)}, {Tlo(tb, u_[0])} quad_perm:[1,2,3,0] {DPP}')
+            e(f'  v_mov_b32_e32 {Thi(tb, u_[0] + Q)}, 0')
+
+        def qstep(j, tb, qreg):
+            if j == 3:
+                e(f'  v_mul_lo_u32 v{qreg}, {Tlo(tb, u_[0])}, s44')
+            if j == 6:
+                e(f'  v_and_b32_e32 v{qreg}, {hex(MASK)}, v{qreg}')
+            if j == 9:
+                e(f'  v_mov_b32_dpp v{qreg}, v{qreg} quad_perm:[0,0,0,0] {DPP}')
+
+        u_ = [0]
+
+        def step(u, last):
+            u_[0] = u
+            ai = f"v{V_AI[u % 2]}"
+            nai = f"v{V_AI[(u + 1) % 2]}"
+            bi = f"v{V_BI[u % 2]}"
+            nbi = f"v{V_BI[(u + 1) % 2]}"
+            if sq and not dbl:
+                e(f'  v_lshlrev_b32_e32 v{V_A2}, 1, {ai}')
+            a2 = bi if dbl else f"v{V_A2}"
+            # window 1: + a_i X0, q1, + q1 N, split
+            for j in range(Q):
+                e(f'  v_mad_u64_u32 {T(TB1, u + j)}, vcc, {ai}, {X0(j)}, {T(TB1, u + j)}')
+                qstep(j, TB1, V_Q)
+                if j == 11 and not last:
+                    e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * RB_}')
+                    if not sq or dbl:
+                        e(f'  ds_read_b32 {nbi}, v{V_LDSI} offset:{(S + u + 1) * RB_}')
+            reduce_split(TB1, V_Q, tmp, 'v_lshrrev_b64')
+            # window 2: + 2 a_i X1 (SQR) / a_i X1 + b_i X0 (MUL), - q1 at position 0, q2, + q2 N, split
+            for j in range(Q):
+                if sq:
+                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {a2}, {X1(j)}, {T(TB2, u + j)}')
+                else:
+                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {ai}, {X1(j)}, {T(TB2, u + j)}')
+                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {bi}, {X0(j)}, {T(TB2, u + j)}')
+                if j == 0:       # lane 0: += q1 (-1); the other lanes add 0
+                    e(f'  v_mad_i64_i32 {T(TB2, u)}, vcc, v{V_Q}, v{V_L0N}, {T(TB2, u)}')
+                qstep(j, TB2, V_Q2)
+            reduce_split(TB2, V_Q2, tmp2, 'v_ashrrev_i64')
+            e('  s_waitcnt lgkmcnt(0)')
+
+        e(f'{lab}:')
+        for k in range(NT):
+            e(f'  v_mov_b64_e32 v[{TB1 + 2 * k}:{TB1 + 2 * k + 1}], 0')
+            e(f'  v_mov_b64_e32 v[{TB2 + 2 * k}:{TB2 + 2 * k + 1}], 0')
+        e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
+        if not sq or dbl:
+            e(f'  ds_read_b32 v{V_BI[0]}, v{V_LDSI} offset:{S * RB_}')
+        e('  s_waitcnt lgkmcnt(0)')
+        NTRIP, TL = S // NT, S % NT
+        assert NTRIP > 0 and TL > 0
+        e(f'  s_mov_b32 s18, {NTRIP}')
+        e(f'{lab}_trip:')
+        for u in range(NT):
+            step(u, False)
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(NT * RB_)}, v{V_LDSI}')
+        e('  s_sub_u32 s18, s18, 1')
+        e('  s_cmp_lg_u32 s18, 0')
+        e(f'  s_cbranch_scc1 {lab}_trip')
+        for u in range(TL):
+            step(u, u == TL - 1)
+        e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB_)}, v{V_LDSI}')   # back to the column base
+
+        def normalise(tb, X):
+            e(f'  v_mov_b64_e32 {tmp}, 0')
+            for k in range(Q):
+                e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(tb, TL + k)}')
+                e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+                e(f'  v_ashrrev_i64 {tmp}, {B}, {tmp}')
+            ripple_quad(X, signed=True)
+
+        normalise(TB1, X0)                       # digits in [0, 2n): no conditional subtraction
+        normalise(TB2, X1)
+        e('  s_cmp_eq_u32 s19, 0')
+        e('  s_cbranch_scc1 .Lprog')
+        e('  s_sub_u32 s19, s19, 1')
+        e('  s_branch .Lsqr_loop')
+
+    for sq in (True, False):
+        (emit_product_mont if mont else emit_product)(sq)
     e('.Lend:')
     e('  s_endpgm')
     e(f'.Lfunc_end_{name}:')

@@ -37,11 +37,57 @@ def _nadic_launches(dev, fn):
         out = fn()
         vals = [ctypes.c_double() for _ in range(7)]
         assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
+        launches = 0.0
+        for variant in (2076, 2176):            # the classical and the Montgomery form (default)
+            ms, nl = ctypes.c_double(), ctypes.c_double()
+            assert lib.fthe_prof_variant(dev.ctx, variant, ctypes.byref(ms), ctypes.byref(nl)) == 0
+            launches += nl.value
+    finally:
+        lib.fthe_prof_enable(dev.ctx, 0)
+    return out, launches
+
+
+def _variant_launches(dev, fn, variant):
+    lib = dev.lib
+    lib.fthe_prof_enable(dev.ctx, 1)
+    try:
+        out = fn()
+        vals = [ctypes.c_double() for _ in range(7)]
+        assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
         ms, nl = ctypes.c_double(), ctypes.c_double()
-        assert lib.fthe_prof_variant(dev.ctx, 2076, ctypes.byref(ms), ctypes.byref(nl)) == 0
+        assert lib.fthe_prof_variant(dev.ctx, variant, ctypes.byref(ms), ctypes.byref(nl)) == 0
     finally:
         lib.fthe_prof_enable(dev.ctx, 0)
     return out, nl.value
+
+
+def test_montgomery_form_same_ciphertexts_as_classical(keys):
+    """fthe_nadic_m76 (Montgomery n-adic, default; tools/nadic_mont_model.py) against fthe_nadic_q76
+    (FTHE_NADIC_CLASSICAL=1) and the oracle's formula: injected r at the extremes (r >= n included) and
+    random, plaintexts up to 2^64 - 1, across a chunk boundary; each form's launches are its own kernel."""
+    dev, pa, pm = keys
+    from fedtree_amd.paillier import Paillier
+    os.environ["FTHE_NADIC_CLASSICAL"] = "1"
+    try:
+        pc = Paillier.from_primes(pa.p, pa.q, dev)
+    finally:
+        del os.environ["FTHE_NADIC_CLASSICAL"]
+    rng = np.random.default_rng(SEED + 5)
+    n = pa.modulus
+    cnt = 98304 + 1000                          # one launch's 98,304 ciphertexts + a partial one
+    rs = [1, 2, n - 1, n - 2, n + 5, 2**2048 - 1, 2 * n - 1 if 2 * n < 2**2048 else n + 7] + \
+        [int.from_bytes(rng.bytes(256), "little") % n for _ in range(cnt - 7)]
+    m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    m[:3] = [0, 2**64 - 1, 1]
+    rw = pyoracle.ints_to_words(rs, pa.n_words)
+    ca, la = _variant_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True), 2176)
+    cc, lc = _variant_launches(dev, lambda: pc.encrypt_u64(m, r=rw, public=True), 2076)
+    assert la == lc and la >= 2
+    assert np.array_equal(ca, cc)
+    got = pyoracle.words_to_ints(ca[:64])
+    n2 = n * n
+    for i in range(64):
+        assert got[i] == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
 
 
 def test_injected_r_same_ciphertexts_as_montgomery(keys):

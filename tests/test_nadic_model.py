@@ -63,3 +63,40 @@ def test_gathered_digit_entries_on_quad_emulator():
         quad_emu.selftest_gather(True)
     finally:
         os.chdir(cwd)
+
+
+def test_montgomery_model_bounds_and_encrypt():
+    """tools/nadic_mont_model.py: the Montgomery n-adic product (fthe_nadic_m76) at digits up to 2n - 1
+    (the chained bound), squarings, and the encrypt program pow / MUL (1, m) / MUL K / CANON vs pow()"""
+    import nadic_mont_model as mm
+    rng = random.Random(5)
+    st = {}
+    for nb in (2042, 2048):
+        n = rng.getrandbits(nb) | (1 << (nb - 1)) | 1
+        n2 = n * n
+        rinv = pow(mm.R, -1, n2)
+        for xs in ([2 * n - 1] * 4, [rng.randrange(2 * n) for _ in range(4)], [0, 2 * n - 1, 1, 0]):
+            x0, x1, y0, y1 = xs
+            z0, z1 = mm.mont(y0, y1, x0, x1, n, stats=st)
+            assert (z0 + z1 * n) % n2 == (x0 + x1 * n) * (y0 + y1 * n) * rinv % n2
+            z0, z1 = mm.mont(x0, x1, x0, x1, n, sq=True, stats=st)
+            assert (z0 + z1 * n) % n2 == (x0 + x1 * n) ** 2 * rinv % n2
+    assert st['col'] < 1 << 62
+    n = rng.getrandbits(2048) | (1 << 2047) | 1
+    e = rng.getrandbits(40) | (1 << 39)
+    m = rng.getrandbits(64)
+    for r in (2 * n - 1, rng.randrange(1, n)):
+        z0, z1 = mm.encrypt(m, r, n, e)
+        assert z0 + z1 * n == pow(r, e, n * n) * (1 + m * n) % (n * n)
+
+
+def test_montgomery_assembly_on_quad_emulator():
+    """the generated fthe_nadic_m76 (gen_nadic.py mont=True) on the emulated quad: LOADX of a raw r,
+    CANON, pow, MUL (1, m), MUL K, CANON, STOREX against pow(r, e, n^2) (1 + m n)"""
+    import quad_emu
+    cwd = os.getcwd()
+    os.chdir(ROOT)
+    try:
+        quad_emu.selftest(trials=2, ebits=6, mont=True)
+    finally:
+        os.chdir(cwd)

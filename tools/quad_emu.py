@@ -232,6 +232,9 @@ class QuadEmu:
             if op == 's_cmp_eq_u32':
                 self.scc = int((self.sread(args[0]) & M32) == (self.sread(args[1]) & M32))
                 continue
+            if op == 's_cmp_lg_u32':
+                self.scc = int((self.sread(args[0]) & M32) != (self.sread(args[1]) & M32))
+                continue
             # ---- vector (per active lane) ----
             if op == 'v_mov_b32_dpp':
                 m = re.search(r'quad_perm:\[(\d),(\d),(\d),(\d)\]', ins)
@@ -426,13 +429,16 @@ def pow_ops(e, tbl0, sq_slot, w, op):
         op(3, pend)
 
 
-def selftest(trials=2, ebits=24):
+def selftest(trials=2, ebits=24, mont=False):
+    """mont: the Montgomery form fthe_nadic_m76 (tools/nadic_mont_model.py) and its encrypt program
+    LOADX, CANON, pow(e), MUL (1, m), MUL K (K = R^(e+1) mod n^2), CANON, STOREX"""
     sys.path.insert(0, 'fedtree_amd/csrc')
     sys.path.insert(0, 'tools')
     from gen_nadic import gen_nadic
     import nadic_model as nm
     S, B, SS = 76, 27, 152
-    asm = gen_nadic(S, B, 'fthe_nadic_q76')
+    kname = 'fthe_nadic_m76' if mont else 'fthe_nadic_q76'
+    asm = gen_nadic(S, B, kname, mont=mont)
     lds_bytes = 4 * 2 * S * 68
     rng = random.Random(11)
     for trial in range(trials):
@@ -444,7 +450,7 @@ def selftest(trials=2, ebits=24):
         for i, v in enumerate([SLOTS & M32, SLOTS >> 32, PROG, 0, CTX, 0, L * 4, SS * L * 4, L, 0]):
             em.mem[KA + 4 * i] = v
         k1, k2, k3, bias = nm.consts(n)
-        ctxw = nm.limbs(n) + [0]
+        ctxw = nm.limbs(n) + [(-pow(n, -1, 1 << B)) % (1 << B)]
         for d in (k1, k2, k3, bias):
             b_ = f2b(d)
             ctxw += [b_ & M32, b_ >> 32]
@@ -460,6 +466,8 @@ def selftest(trials=2, ebits=24):
         op(20, 0)
         pow_ops(e, 16, 9, 3, op)
         op(4, 3)
+        if mont:
+            op(4, 4)
         op(20, 0)
         op(2, 6)
         op(0, 0)
@@ -471,10 +479,13 @@ def selftest(trials=2, ebits=24):
                 em.mem[SLOTS + s * SS * L * 4 + k_ * L * 4] = limb          # ciphertext 0
         put_slot(0, [(r >> (B * k_)) & ((1 << B) - 1) for k_ in range(SS)])
         put_slot(3, nm.limbs(1) + nm.limbs(m))
+        if mont:
+            K = pow(1 << (B * S), e + 1, n2)
+            put_slot(4, nm.limbs(K % n) + nm.limbs(K // n))
         em.s[0], em.s[1], em.s[2] = KA, 0, 0
         for ln in range(NL):
             em.v[ln][0] = ln                                  # tid
-        em.run('fthe_nadic_q76')
+        em.run(kname)
         out = [em.mem.get(SLOTS + 6 * SS * L * 4 + k_ * L * 4, 0) for k_ in range(SS)]
         x0 = sum(out[k_] << (B * k_) for k_ in range(S))
         x1 = sum(out[S + k_] << (B * k_) for k_ in range(S))
