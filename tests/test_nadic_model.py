@@ -71,7 +71,7 @@ def test_montgomery_model_bounds_and_encrypt():
     import nadic_mont_model as mm
     rng = random.Random(5)
     st = {}
-    for nb in (2042, 2048):
+    for nb in (1033, 1536, 2042, 2048):
         n = rng.getrandbits(nb) | (1 << (nb - 1)) | 1
         n2 = n * n
         rinv = pow(mm.R, -1, n2)
