@@ -708,11 +708,17 @@ static bool nadic_ok(const fthe_key *k) {
     return !getenv("FTHE_NO_NADIC") && k->sn2.S == 152 && k->sn2.B == 27 && k->sn2.lanes == 4 &&
            b >= 2042 && b <= 2050;
 }
-static int upload_nadic(DevMod &d, const mpz_t n, const mpz_t n2, Shape slots) {
+// its Montgomery form (fthe_nadic_m76, the default) needs only an odd n with 8 n < R = 2^2052 and n^2 on the
+// s152 slots: every n of 1033..2048 bits (no quotient estimate, so no lower bound of its own)
+static bool nadic_mont_ok(const fthe_key *k) {
+    return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_CLASSICAL") && k->sn2.S == 152 && k->sn2.B == 27 &&
+           k->sn2.lanes == 4 && mpz_sizeinbase(k->n, 2) <= 2048;
+}
+static int upload_nadic(DevMod &d, const mpz_t n, const mpz_t n2, Shape slots, bool classical = true) {
     d.m.init(n2, slots);
     MontMod dm;
     dm.init(n, kNadicDigit);
-    if (!dm.classical_ok()) return FTHE_ERR_UNSUPPORTED;
+    if (classical && !dm.classical_ok()) return FTHE_ERR_UNSUPPORTED;
     if (hipMalloc(&d.d_ctx, dm.ctx.size() * 4) != hipSuccess) return FTHE_ERR_NOMEM;
     HIPOK(hipMemcpy(d.d_ctx, dm.ctx.data(), dm.ctx.size() * 4, hipMemcpyHostToDevice));
     d.kernel_S = kNadicS;
@@ -764,9 +770,10 @@ static int key_finish(fthe_key *k) {
         // n-adic form (n of 2048 bits): X = r as base-n digits (r, 0); X^n; X (1 + m n) with the digits
         // (1, m) of slot C1; canonical digits -> c = x0 + x1 n by the output kernel (mul_add_out)
         k->nadic = nadic_ok(k);
+        k->nadic_mont = nadic_mont_ok(k);
+        if (k->nadic || k->nadic_mont) k->c_n76 = k->add_const(to_limbs(k->n, kNadicDigit.S, kNadicDigit.B));
         if (k->nadic) {
             if ((rc = upload_nadic(k->mnA, k->n, k->n2, k->sn2))) return rc;
-            k->c_n76 = k->add_const(to_limbs(k->n, kNadicDigit.S, kNadicDigit.B));
             Prog x;
             x.loadx(SL_IN0); x.canon();
             x.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
@@ -775,12 +782,13 @@ static int key_finish(fthe_key *k) {
             h.alg = nadic_alg(x, k->n);
             h.exec = nadic_exec(x);
             k->prN_enc_pub = h;
+        }
+        {
             // Montgomery form (tools/nadic_mont_model.py): the raw r is a Montgomery residue (value r R^-1),
             // pow(n) gives r^n R^(1-n), MUL (1, m) and MUL K (slot C2) give (1 + m n) r^n; digits < 2n
             // between products, CANON at the end
-            k->nadic_mont = !getenv("FTHE_NADIC_CLASSICAL");
             if (k->nadic_mont) {
-                if ((rc = upload_nadic(k->mnM, k->n, k->n2, k->sn2))) return rc;
+                if ((rc = upload_nadic(k->mnM, k->n, k->n2, k->sn2, false))) return rc;
                 k->mnM.kernel_S = kNadicMontS;
                 Mpz Kc, R, e1, q0, q1;
                 mpz_set_ui(R, 1); mpz_mul_2exp(R, R, (mp_bitcnt_t)kNadicDigit.B * kNadicDigit.S);
@@ -1891,7 +1899,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
                         k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
-        } else if (k->nadic) {
+        } else if (k->nadic || k->nadic_mont) {
             // n-adic kernel: digits (r, 0) in IN0, (1, m) in C1; out = x0 + x1 n (x0, x1 < n: c < n^2)
             const int D = kNadicDigit.S;
             pack_rows(c->stream, rw, rwn, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);

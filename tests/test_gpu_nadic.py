@@ -154,9 +154,10 @@ def _prime_of_bits(rng, bits):
             return p
 
 
-# n of 2042..2048 bits runs on the n-adic kernel (the quotient estimate needs n >= 2^(27*76 - 10); n^2 of
-# more than 4096 bits has no kernel shape at all); one bit below, on the Montgomery s152 program
-@pytest.mark.parametrize("nbits,nadic", [(2042, True), (2045, True), (2041, False), (2030, False)])
+# the Montgomery form (default) runs every n of 1033..2048 bits (n^2 on the s152 slots); the classical form
+# needs n >= 2^(27*76 - 10) for its quotient estimate (n of 2042..2048), below that FTHE_NADIC_CLASSICAL=1
+# keys fall back to the Montgomery s152 program (tests/test_gpu_nadic.py::test_classical_form_range)
+@pytest.mark.parametrize("nbits,nadic", [(2042, True), (2045, True), (2041, True), (2030, True), (1536, True)])
 def test_modulus_range_edges(nbits, nadic):
     from fedtree_amd.paillier import Device, Paillier
     dev = Device(0)
@@ -179,3 +180,31 @@ def test_modulus_range_edges(nbits, nadic):
         assert pyoracle.from_words(c[i]) == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
     full = Paillier.from_primes(p, q, dev)
     assert np.array_equal(full.decrypt_u64(c), m)
+
+
+@pytest.mark.parametrize("nbits,classical", [(2042, True), (2041, False)])
+def test_classical_form_range(nbits, classical):
+    """FTHE_NADIC_CLASSICAL=1: fthe_nadic_q76 from n of 2042 bits, the Montgomery s152 program one bit below"""
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    rng = np.random.default_rng(nbits + 7)
+    while True:
+        p = _prime_of_bits(rng, nbits // 2)
+        q = _prime_of_bits(rng, nbits - nbits // 2)
+        n = p * q
+        if n.bit_length() == nbits:
+            break
+    os.environ["FTHE_NADIC_CLASSICAL"] = "1"
+    try:
+        pl = Paillier.from_public(n, dev)
+    finally:
+        del os.environ["FTHE_NADIC_CLASSICAL"]
+    cnt = 300
+    rs = [1, n - 1] + [int.from_bytes(rng.bytes(260), "little") % (n - 1) + 1 for _ in range(cnt - 2)]
+    m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    rw = pyoracle.ints_to_words(rs, pl.n_words)
+    c, launches = _variant_launches(dev, lambda: pl.encrypt_u64(m, r=rw), 2076)
+    assert launches == (1 if classical else 0)
+    n2 = n * n
+    for i in (0, 1, 2, cnt - 1):
+        assert pyoracle.from_words(c[i]) == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
