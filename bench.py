@@ -657,11 +657,15 @@ def run(a, world):
                       "GHPair::operator+ on the USE_HIP key (2 host adds x y mod n^2 per operator; empty bins "
                       "promoted from the key's GPU-filled randomizer pool), every bin checked by decryption; "
                       "reference_add_same_threads_per_s: the reference's Paillier_GMP::add (mpz_mul + mpz_mod) on "
-                      "the same threads and operands in the same run; compare cpu_baseline.ops.p2048_add too"}
+                      "the same threads and operands in the same run; compare cpu_baseline.ops.p2048_add too. "
+                      "sub: the sibling subtraction (hist_tree_builder.cpp:672-680), OpenMP over 4,096 bins, "
+                      "`dest[i] = father[i] - child[i]` through GHPair::operator- (2 x mul(x, 2^64-1) + 2 adds; a "
+                      "single-element mul is a host mpz_powm, as paillier_gpu.cu:65-67), every bin decrypted; "
+                      "reference_sub_same_threads_per_s: mpz_powm + mpz_mul/mpz_mod on the same threads and operands"}
         for thr in (16, 64):
             try:
-                r = subprocess.run([exe, str(KEY_BITS), str(thr), "8192", "16"], capture_output=True, text=True,
-                                   timeout=180)
+                r = subprocess.run([exe, str(KEY_BITS), str(thr), "8192", "16", "4096"], capture_output=True,
+                                   text=True, timeout=180)
                 hl[f"threads_{thr}"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                     {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
             except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:

@@ -393,7 +393,7 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
         def est_list(tb, u, qreg, dacc):
             acc = f"v[{dacc}:{dacc + 1}]"
             ab = os.environ.get("FTHE_GEN_NADIC_AB", "")
-            if "noest" in ab:                                        # timing only: q = 0 (wrong results)
+            if "noest" in ab.split(","):                             # timing only: q = 0 (wrong results)
                 return [f'  v_mov_b32_e32 v{qreg}, 0', None, None,
                         f'  v_mov_b32_dpp v{qreg}, v{qreg} quad_perm:[3,3,3,3] {DPP}']
             if "fold" in ab.split(","):

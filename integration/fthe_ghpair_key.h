@@ -37,6 +37,12 @@
 // so the operator bodies compile unchanged.
 #pragma once
 #include <gmp.h>
+// The key fields are read-only views (mpz_roinit_n, alloc 0) of the cell's limbs.  A caller that writes one
+// relies on GMP allocating afresh for an alloc-0 destination, which GMP guarantees from 6.2 on; older
+// releases realloc the view's pointer (the cell's std::vector storage) and corrupt the heap.
+#if (__GNU_MP_VERSION * 100 + __GNU_MP_VERSION_MINOR) < 602
+#error "fthe_ghpair_key.h needs GMP >= 6.2 (writes to mpz_roinit_n views)"
+#endif
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -436,13 +442,26 @@ public:
         mpz_init(r);
         mul_into(r, x, y);
     }
-    // The same into an initialised r (Paillier_GPU::mul's contract, paillier_gpu.cu:65-67).
+    // The same into an initialised r (Paillier_GPU::mul's contract, paillier_gpu.cu:65-67).  One element with
+    // an exponent of at most 64 bits -- operator-'s 2^64 - 1 (common.h:253-337) from the sibling subtraction
+    // and missing_gh loops (hist_tree_builder.cpp:672-680, 715-726) -- is a host mpz_powm, as in the
+    // reference's GPU build: 64 squarings of 4096 bits take ~0.2 ms on one core, and a GPU queue round trip per
+    // element costs more than that and serialises the OpenMP callers (bench
+    // secondary.histogram_loop_unchanged_callers.*.sub).  FTHE_SHIM_MUL_ENGINE=1 sends them to the engine's
+    // coalescing queue instead (the round-3 behaviour, kept for the A/B).  Batches of subtractions go to the
+    // engine through Paillier_HIP::subtract (fthe_sub).  Larger exponents run on the engine.
     void mul_into(mpz_ptr r, const mpz_t &x, const mpz_t &y) const {
         fthe_shim::KeyCell *c = need();
         const int cw = 2 * c->nw;
         if (mpz_sgn(y) < 0) throw std::runtime_error("mul: negative exponent");
-        std::vector<uint32_t> a(cw), o(cw);
+        static const bool on_engine = [] { const char *e = std::getenv("FTHE_SHIM_MUL_ENGINE"); return e && *e == '1'; }();
         fthe_shim::Scratch &s = fthe_shim::scratch();
+        if (!on_engine && mpz_sizeinbase(y, 2) <= 64) {
+            mpz_powm(s.v, x, y, c->n2);                             // x reduced mod n^2 first, as the reference's
+            mpz_set(r, s.v);
+            return;
+        }
+        std::vector<uint32_t> a(cw), o(cw);
         mpz_mod(s.v, x, c->n2);                                     // the reference's powm reduces x first
         fthe_shim::to_words(s.v, a.data(), cw);
         auto k = c->engine();

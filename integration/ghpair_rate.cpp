@@ -5,7 +5,12 @@
 // empty bin promotes it with homo_encrypt (two pooled encryptions, Q10).  Checked: every populated bin
 // decrypts to the codec sum of its members.  The same run times the reference's own per-element add
 // (Paillier_GMP::add = mpz_mul + mpz_mod, paillier_gmp.cpp:16-21) on the same threads and operands.
-//   ghpair_rate [bits] [threads = features] [instances] [bins]      -> one JSON line
+// Then the sibling subtraction (hist_tree_builder.cpp:672-680, and missing_gh :715-726): an OpenMP loop over
+// bins, `dest[i] = father[i] - child[i]` through GHPair::operator- (common.h:253-337: two mul(x, 2^64 - 1)
+// and two adds per operator), timed beside the reference GPU build's own per-element work on the same threads
+// and operands (Paillier_GPU::mul = mpz_powm(x, 2^64 - 1, n^2), paillier_gpu.cu:65-67, then
+// Paillier_GPU::add = mpz_mul + mpz_mod, :57-61).  Checked: every difference decrypts to the codec difference.
+//   ghpair_rate [bits] [threads = features] [instances] [bins] [sub_bins]    -> one JSON line
 #include <omp.h>
 
 #include <chrono>
@@ -13,6 +18,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -23,7 +29,8 @@ int main(int argc, char **argv) {
     const int F = argc > 2 ? std::atoi(argv[2]) : 32;
     const int N = argc > 3 ? std::atoi(argv[3]) : 512;
     const int B = argc > 4 ? std::atoi(argv[4]) : 16;
-    if (bits <= 0 || F <= 0 || N <= 0 || B <= 0) return 2;
+    const int SB = argc > 5 ? std::atoi(argv[5]) : 4096;
+    if (bits <= 0 || F <= 0 || N <= 0 || B <= 0 || SB < 0) return 2;
     Paillier_HIP server;
     server.keygen(bits);
     SyncArray<GHPair> gh(N);
@@ -114,14 +121,95 @@ int main(int argc, char **argv) {
             std::fabs(out.host_data()[b].h - eh) > 1e-5 + 1e-6 * std::fabs(eh))
             bad++;
     }
+    // -- sibling subtraction: father - child per bin (both encrypted: the encrypted-rhs branch) --
+    double sub_s = 1e30, sub_ref_s = 1e30;
+    std::vector<double> sub_all, sub_ref_all;
+    int sub_bad = 0;
+    if (SB > 0) {
+        std::vector<GHPair> father(SB), child(SB), diff(SB);
+        std::vector<float> fg(SB), fh(SB), cg(SB), ch(SB);
+        {
+            SyncArray<GHPair> fc(2 * (size_t)SB);
+            for (int i = 0; i < SB; i++) {
+                fg[i] = 0.002f * (float)(i % 97) - 0.09f;   fh[i] = 1.5f + 0.003f * (float)(i % 41);
+                cg[i] = 0.001f * (float)(i % 89) - 0.04f;   ch[i] = 0.5f + 0.002f * (float)(i % 37);
+                fc.host_data()[i] = GHPair(fg[i], fh[i]);
+                fc.host_data()[SB + i] = GHPair(cg[i], ch[i]);
+            }
+            server.encrypt(fc);
+            for (int i = 0; i < 2 * SB; i++) {
+                fc.host_data()[i].encrypted = true;
+                fc.host_data()[i].paillier = server.paillier_cpu;
+            }
+            for (int i = 0; i < SB; i++) { father[i] = fc.host_data()[i]; child[i] = fc.host_data()[SB + i]; }
+        }
+        const int T = F;
+        auto sub_round = [&]() {
+            const auto t0 = std::chrono::steady_clock::now();
+#pragma omp parallel for num_threads(T) schedule(static)
+            for (int i = 0; i < SB; i++) diff[i] = father[i] - child[i];
+            return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        };
+        // the reference GPU build's per-element work for one operator-: mpz_powm(x, 2^64 - 1, n^2) and a
+        // product mod n^2, for g and h
+        auto sub_ref_round = [&]() {
+            const auto t0 = std::chrono::steady_clock::now();
+#pragma omp parallel num_threads(T)
+            {
+                mpz_t mo, r, t;
+                mpz_init(r); mpz_init(t); mpz_init(mo);
+                const long m1 = -1;
+                mpz_import(mo, 1, -1, sizeof(m1), 0, 0, &m1);
+#pragma omp for schedule(static)
+                for (int i = 0; i < SB; i++) {
+                    mpz_powm(t, child[i].g_enc, mo, server.paillier_cpu.n_square);
+                    mpz_mul(r, father[i].g_enc, t);
+                    mpz_mod(r, r, server.paillier_cpu.n_square);
+                    mpz_powm(t, child[i].h_enc, mo, server.paillier_cpu.n_square);
+                    mpz_mul(r, father[i].h_enc, t);
+                    mpz_mod(r, r, server.paillier_cpu.n_square);
+                }
+                mpz_clear(r); mpz_clear(t); mpz_clear(mo);
+            }
+            return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        };
+        for (int rep = 0; rep < 3; rep++) {
+            sub_ref_all.push_back(sub_ref_round());
+            sub_all.push_back(sub_round());
+            sub_ref_s = std::min(sub_ref_s, sub_ref_all.back());
+            sub_s = std::min(sub_s, sub_all.back());
+        }
+        SyncArray<GHPair> dd(SB);
+        for (int i = 0; i < SB; i++) dd.host_data()[i] = diff[i];
+        server.decrypt(dd);
+        for (int i = 0; i < SB; i++) {
+            // decrypt_gh_pairs decodes the low 64 bits as a signed fixed-point value (Q6, Q9)
+            const double eg = (double)((long)(fg[i] * 1e6) - (long)(cg[i] * 1e6)) / 1e6;
+            const double eh = (double)((long)(fh[i] * 1e6) - (long)(ch[i] * 1e6)) / 1e6;
+            if (!diff[i].encrypted || std::fabs(dd.host_data()[i].g - eg) > 1e-5 + 1e-6 * std::fabs(eg) ||
+                std::fabs(dd.host_data()[i].h - eh) > 1e-5 + 1e-6 * std::fabs(eh))
+                sub_bad++;
+        }
+    }
+    auto arr3 = [](const std::vector<double> &v) {
+        char b[96];
+        if (v.size() < 3) return std::string("[]");
+        std::snprintf(b, sizeof b, "[%.4f, %.4f, %.4f]", v[0], v[1], v[2]);
+        return std::string(b);
+    };
+    const double sops = 2.0 * SB;   // ciphertext subtractions (g and h)
     const double ops = (double)F * N;
     std::printf("{\"bits\": %d, \"threads\": %d, \"instances\": %d, \"bins\": %d, \"operators\": %.0f, "
                 "\"ciphertext_adds\": %.0f, \"promotions\": %d, \"s\": %.4f, \"operators_per_s\": %.0f, "
                 "\"ciphertext_adds_per_s\": %.0f, \"reference_add_same_threads_per_s\": %.0f, "
                 "\"vs_reference_add\": %.3f, \"rounds_s\": [%.4f, %.4f, %.4f], \"reference_rounds_s\": [%.4f, %.4f, %.4f], "
-                "\"bad_bins\": %d, \"ok\": %s}\n",
+                "\"bad_bins\": %d, \"sub\": {\"bins\": %d, \"ciphertext_subs\": %.0f, \"s\": %.5f, "
+                "\"ciphertext_subs_per_s\": %.0f, \"reference_sub_same_threads_per_s\": %.0f, \"vs_reference_sub\": %.3f, "
+                "\"rounds_s\": %s, \"reference_rounds_s\": %s, \"bad_bins\": %d}, \"ok\": %s}\n",
                 bits, F, N, B, ops, 2 * ops, 2 * populated, s, ops / s, 2 * ops / s, 2 * ops / ref_s,
                 (2 * ops / s) / (2 * ops / ref_s), op_all[0], op_all[1], op_all[2], ref_all[0], ref_all[1], ref_all[2],
-                bad, bad ? "false" : "true");
-    return bad ? 1 : 0;
+                bad, SB, sops, SB ? sub_s : 0.0, SB ? sops / sub_s : 0.0, SB ? sops / sub_ref_s : 0.0,
+                SB ? sub_ref_s / sub_s : 0.0, arr3(sub_all).c_str(), arr3(sub_ref_all).c_str(), sub_bad,
+                (bad || sub_bad) ? "false" : "true");
+    return (bad || sub_bad) ? 1 : 0;
 }

@@ -17,6 +17,7 @@
 #   opstrace       kernel trace of tools/prof_ops.py add,kway (the add / merge launch durations for pmc:add)
 #   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo)
 #   ghpair         tools/bin/ghpair_rate at 16 and 64 threads, tools/bin/ghpair_e2e
+#   ghsub          the operator- A/B: tools/bin/ghpair_rate at 16 threads, host powm vs FTHE_SHIM_MUL_ENGINE=1
 #   py:SCRIPT[,ARGS]  python SCRIPT ARGS (a tools/ measurement), appended to TAG_SCRIPT.jsonl
 R=${1:?tag}
 shift
@@ -84,12 +85,19 @@ for step in "$@"; do
       cut -c1-600 ${O}_rehearse_2rank_1gpu.json;;
     ghpair)
       for t in 16 64; do
-        timeout -k 10 300 tools/bin/ghpair_rate 2048 $t 8192 16 >> ${O}_ghpair_rate.jsonl 2>> ${O}_ghpair.err \
+        timeout -k 10 300 tools/bin/ghpair_rate 2048 $t 8192 16 4096 >> ${O}_ghpair_rate.jsonl 2>> ${O}_ghpair.err \
           || fail ghpair_rate $? ${O}_ghpair.err
       done
       timeout -k 10 300 tools/bin/ghpair_e2e 2048 2000000 2 >> ${O}_ghpair_e2e.jsonl 2>> ${O}_ghpair.err \
         || fail ghpair_e2e $? ${O}_ghpair.err
       cat ${O}_ghpair_rate.jsonl ${O}_ghpair_e2e.jsonl;;
+    ghsub)
+      for v in 0 1 0 1; do
+        FTHE_SHIM_MUL_ENGINE=$v timeout -k 10 300 tools/bin/ghpair_rate 2048 16 8192 16 4096 > ${O}_one.json 2>> ${O}_ghsub.err \
+          || fail ghsub $? ${O}_ghsub.err
+        echo "{\"mul_engine\": $v, \"res\": $(tail -1 ${O}_one.json)}" >> ${O}_ghsub_ab.jsonl
+      done
+      cat ${O}_ghsub_ab.jsonl;;
     py:*)
       spec=${step#py:}
       script=${spec%%,*}
