@@ -684,6 +684,19 @@ def run(a, world):
                       "mpz_t fields (host in and out, PCIe, mpz import/export per ciphertext); compare "
                       "e2e_host_encrypt_per_s (numpy rows) and the device-resident value")
         secondary["ghpair_e2e"] = ge
+        # the host side of an N-GPU server: the same mpz_t <-> row marshalling for 1, 2, 4, 8 concurrent
+        # shards of 1,048,576 pairs, no kernels (integration/marshal_rate.cpp) -- can one host feed 8 GPUs?
+        try:
+            r = subprocess.run([os.path.join(ROOT, "tools", "bin", "marshal_rate"), str(KEY_BITS), "1048576", "3",
+                                "1,2,4,8"], capture_output=True, text=True, timeout=240)
+            mr = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+        except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
+            mr = {"error": repr(ex)[:300]}
+        mr["note"] = ("Paillier_HIP::encrypt/decrypt(SyncArray<GHPair>&)'s host marshalling alone (codec + rows <-> mpz "
+                      "limbs, up to 16 threads per shard, one host thread per shard), aggregated ciphertexts/s; the "
+                      "8-GPU feed needs 8 x the device rate (value) on the encrypt side")
+        secondary["host_marshalling_shards"] = mr
         # key generation (homo_init; re-run every round in the vertical simulation, FLtrainer.cpp:556):
         # host prime search on up to 16 threads + device key set-up
         t0 = time.perf_counter()

@@ -86,15 +86,42 @@ inline fthe_ctx *thread_ctx() {
     }
     return c;
 }
-// mpz <-> little-endian u32 words (paillier_gpu.cu:7,18 order)
+// mpz <-> little-endian u32 words (paillier_gpu.cu:7,18 order: mpz_export / mpz_import with order -1, size 4).
+// On a little-endian host with 64-bit limbs and no nails those words ARE the limbs' bytes, so the batch
+// marshalling copies limbs directly (memcpy + size) instead of GMP's generic word loop, which runs ~1.2M
+// ciphertexts/s per core at 4096 bits -- short of feeding 8 GPUs from one host (integration/marshal_rate.cpp,
+// DESIGN 6).  Same values either way (tests: integration/host_ops_test.cpp round trips).
+#if defined(__BYTE_ORDER__) && __BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__ && GMP_LIMB_BITS == 64 && GMP_NAIL_BITS == 0
+#define FTHE_SHIM_LIMB_COPY 1
+#endif
 inline void to_words(const mpz_t x, uint32_t *w, int nw) {
-    size_t cnt = 0;
-    for (int i = 0; i < nw; i++) w[i] = 0;
     if (mpz_sgn(x) < 0) throw std::runtime_error("negative operand");
     if (mpz_sizeinbase(x, 2) > (size_t)nw * 32) throw std::runtime_error("operand does not fit");
+#ifdef FTHE_SHIM_LIMB_COPY
+    const size_t nb = mpz_size(x) * sizeof(mp_limb_t), cap = (size_t)nw * 4;
+    const size_t cp = std::min(nb, cap);                 // the top limb may hold only the row's last word
+    if (cp) std::memcpy(w, mpz_limbs_read(x), cp);
+    if (cp < cap) std::memset(reinterpret_cast<char *>(w) + cp, 0, cap - cp);
+#else
+    size_t cnt = 0;
+    for (int i = 0; i < nw; i++) w[i] = 0;
     mpz_export(w, &cnt, -1, 4, 0, 0, x);
+#endif
 }
-inline void from_words(mpz_t x, const uint32_t *w, int nw) { mpz_import(x, (size_t)nw, -1, 4, 0, 0, w); }
+inline void from_words(mpz_t x, const uint32_t *w, int nw) {
+#ifdef FTHE_SHIM_LIMB_COPY
+    int top = nw;
+    while (top > 0 && w[top - 1] == 0) top--;
+    const mp_size_t nl = (top + 1) / 2;
+    if (nl == 0) { mpz_set_ui(x, 0); return; }
+    mp_limb_t *d = mpz_limbs_write(x, nl);
+    d[nl - 1] = 0;                                      // an odd word count leaves the top limb's high half 0
+    std::memcpy(d, w, (size_t)top * 4);
+    mpz_limbs_finish(x, nl);
+#else
+    mpz_import(x, (size_t)nw, -1, 4, 0, 0, w);
+#endif
+}
 inline size_t words_of(const mpz_t x) { return (mpz_sizeinbase(x, 2) + 31) / 32; }
 
 // Scratch integers of the calling thread (the operators run from OpenMP workers).

@@ -24,6 +24,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -55,28 +57,83 @@ inline void parallel_for(size_t n, F f) {
     for (auto &x : th) x.join();
     for (auto &e : err) if (e) std::rethrow_exception(e);
 }
-// Page-locked row buffers of the calling thread (fthe_host_alloc), grown on demand and kept across calls:
-// the batch calls then DMA straight from / into them (no pinned staging copy, no page faults on a fresh
-// multi-GB vector), and pinning is paid once per thread, not per encrypt_gh_pairs.
-template <class T>
-inline T *pinned(int slot, size_t count) {
-    struct Buf {
-        void *p = nullptr;
-        size_t cap = 0;
-        ~Buf() { fthe_host_free(p); }
-    };
-    static thread_local Buf bufs[2];
-    Buf &b = bufs[slot];
-    const size_t bytes = std::max<size_t>(1, count) * sizeof(T);
-    if (b.cap < bytes) {
-        fthe_host_free(b.p);
-        b.p = nullptr;
-        b.cap = 0;
-        check(fthe_host_alloc(bytes, &b.p), "host_alloc");
-        b.cap = bytes;
+// Page-locked row buffers (fthe_host_alloc) for the batch calls, which then DMA straight from / into them (no
+// pinned staging copy, no page faults on a fresh multi-GB vector).  A process-wide pool, not per thread: a
+// lease takes the smallest free buffer that fits (or pins a new one) and returns it when the call ends; free
+// buffers beyond FTHE_SHIM_PINNED_CACHE_MB (default 4096) are unpinned at once, so many OpenMP or server
+// threads cannot accumulate page-locked memory, and pinning is still paid once for a steady batch size.  The
+// pool is emptied by an atexit handler registered at the first pin -- after the HIP runtime's own
+// initialisation, so it runs before the runtime tears down.
+class PinnedPool {
+public:
+    static PinnedPool &get() {
+        static PinnedPool *p = new PinnedPool();          // never destroyed: the atexit handler empties it
+        return *p;
     }
-    return static_cast<T *>(b.p);
-}
+    void *acquire(size_t bytes) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            auto best = free_.end();
+            for (auto it = free_.begin(); it != free_.end(); ++it)
+                if (it->second >= bytes && (best == free_.end() || it->second < best->second)) best = it;
+            if (best != free_.end()) {
+                void *q = best->first;
+                cached_ -= best->second;
+                size_[q] = best->second;
+                free_.erase(best);
+                return q;
+            }
+        }
+        void *q = nullptr;
+        check(fthe_host_alloc(bytes, &q), "host_alloc");
+        std::lock_guard<std::mutex> lk(m_);
+        if (!hooked_) { hooked_ = true; std::atexit([] { PinnedPool::get().drain(0); }); }
+        size_[q] = bytes;
+        return q;
+    }
+    void release(void *q) {
+        if (!q) return;
+        std::lock_guard<std::mutex> lk(m_);
+        auto it = size_.find(q);
+        if (it == size_.end()) return;
+        free_.emplace_back(q, it->second);
+        cached_ += it->second;
+        size_.erase(it);
+        trim(cap_);
+    }
+    void drain(size_t keep) { std::lock_guard<std::mutex> lk(m_); trim(keep); }
+    size_t cached_bytes() { std::lock_guard<std::mutex> lk(m_); return cached_; }
+
+private:
+    PinnedPool() {
+        const char *e = std::getenv("FTHE_SHIM_PINNED_CACHE_MB");
+        cap_ = (size_t)(e ? std::atoll(e) : 4096) << 20;
+    }
+    void trim(size_t keep) {                              // unpin the largest free buffers first
+        while (cached_ > keep && !free_.empty()) {
+            auto big = std::max_element(free_.begin(), free_.end(),
+                                        [](const auto &a, const auto &b) { return a.second < b.second; });
+            fthe_host_free(big->first);
+            cached_ -= big->second;
+            free_.erase(big);
+        }
+    }
+    std::mutex m_;
+    std::vector<std::pair<void *, size_t>> free_;
+    std::map<void *, size_t> size_;
+    size_t cached_ = 0, cap_ = 0;
+    bool hooked_ = false;
+};
+// One call's page-locked buffer of count T (returned to the pool when the lease ends).
+template <class T>
+struct Pinned {
+    explicit Pinned(size_t count) : p(static_cast<T *>(PinnedPool::get().acquire(std::max<size_t>(1, count) * sizeof(T)))) {}
+    ~Pinned() { PinnedPool::get().release(p); }
+    Pinned(const Pinned &) = delete;
+    Pinned &operator=(const Pinned &) = delete;
+    T *get() const { return p; }
+    T *p;
+};
 // codec of common.h:81-86 and paillier_gpu.cu:487
 inline uint64_t encode(float_type v) { long l = (long)(v * 1e6); return (uint64_t)l; }
 inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 1e6; }
@@ -175,13 +232,26 @@ public:
         size_t n = message.size();
         if (n == 0) return;
         int nw = fthe_key_n_words(key()), cw = 2 * nw;
-        uint64_t *m = fthe_shim::pinned<uint64_t>(0, 2 * n);
+        fthe_shim::Pinned<uint64_t> mb(2 * n);
+        uint64_t *m = mb.get();
+        encode_pairs(d, n, m);
+        fthe_shim::Pinned<uint32_t> cb(2 * n * (size_t)cw);
+        uint32_t *c = cb.get();
+        fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m, 2 * n, nullptr, 0, 0, c,
+                                          eff_flags()), "encrypt");
+        rows_to_pairs(d, n, c, cw);
+    }
+
+    // The host marshalling of the batch calls, on up to 16 threads (integration/marshal_rate.cpp times it
+    // alone, for 1..8 concurrent shards: the host side of a multi-GPU server).
+    // encrypt: the codec of common.h:81-86 into plaintext words; the 2n result rows (g rows, then h rows)
+    // into the pairs' mpz fields (mpz_import, as paillier_gpu.cu:18).
+    static void encode_pairs(const GHPair *d, size_t n, uint64_t *m) {
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
         });
-        uint32_t *c = fthe_shim::pinned<uint32_t>(1, 2 * n * (size_t)cw);
-        fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m, 2 * n, nullptr, 0, 0, c,
-                                          eff_flags()), "encrypt");
+    }
+    static void rows_to_pairs(GHPair *d, size_t n, const uint32_t *c, int cw) {
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) {
                 fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
@@ -189,14 +259,9 @@ public:
             }
         });
     }
-
-    // Paillier_GPU::decrypt(SyncArray<GHPair>&) (paillier_gpu.cu:448-494)
-    void decrypt(SyncArray<GHPair> &message) {
-        auto *d = message.host_data();
-        size_t n = message.size();
-        if (n == 0) return;
-        int nw = fthe_key_n_words(key()), cw = 2 * nw;
-        uint32_t *c = fthe_shim::pinned<uint32_t>(1, 2 * n * (size_t)cw);
+    // decrypt: the pairs' mpz fields into rows (mpz_export, paillier_gpu.cu:7; unencrypted pairs: zero rows),
+    // then the plaintexts' codec back into g, h
+    static void pairs_to_rows(const GHPair *d, size_t n, uint32_t *c, int cw) {
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {      // to_words throws only on oversize input
             for (size_t i = b; i < e; i++) {
                 if (!d[i].encrypted) {                               // rows of unencrypted pairs: zeros
@@ -208,13 +273,28 @@ public:
                 fthe_shim::to_words(d[i].h_enc, &c[(n + i) * cw], cw);
             }
         });
-        uint64_t *m = fthe_shim::pinned<uint64_t>(0, 2 * n);
-        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key(), fthe_shim::thread_ctx(), c,
-                                                                         2 * n, m, nullptr), "decrypt");
+    }
+    static void decode_pairs(GHPair *d, size_t n, const uint64_t *m) {
         fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++)
                 if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }
         });
+    }
+
+    // Paillier_GPU::decrypt(SyncArray<GHPair>&) (paillier_gpu.cu:448-494)
+    void decrypt(SyncArray<GHPair> &message) {
+        auto *d = message.host_data();
+        size_t n = message.size();
+        if (n == 0) return;
+        int nw = fthe_key_n_words(key()), cw = 2 * nw;
+        fthe_shim::Pinned<uint32_t> cb(2 * n * (size_t)cw);
+        uint32_t *c = cb.get();
+        pairs_to_rows(d, n, c, cw);
+        fthe_shim::Pinned<uint64_t> mb(2 * n);
+        uint64_t *m = mb.get();
+        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key(), fthe_shim::thread_ctx(), c,
+                                                                         2 * n, m, nullptr), "decrypt");
+        decode_pairs(d, n, m);
     }
 
     // Paillier_GPU::decrypt(GHPair&) (paillier_gpu.cu:497-542)

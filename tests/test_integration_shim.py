@@ -282,3 +282,19 @@ def test_pooled_promotions_from_threads(tmp_path):
     _build(exe, "pool_test.cpp", extra=("-fopenmp",))
     r = subprocess.run([exe, "threads", f"{p:x}", f"{q:x}", "16", "300"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "pool OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_marshalling_round_trip_and_shards(tmp_path):
+    """The batch calls' host marshalling (Paillier_HIP::encode_pairs / rows_to_pairs / pairs_to_rows /
+    decode_pairs; the limb-copy fast path of fthe_ghpair_key.h) is lossless for 1 and 2 concurrent shards
+    (integration/marshal_rate.cpp, no kernels; the bench runs it at 1M pairs per shard)."""
+    import json
+    exe = str(tmp_path / "marshal_rate")
+    _build(exe, "marshal_rate.cpp", extra=("-fopenmp",))
+    r = subprocess.run([exe, "2048", "3000", "1", "1,2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["round_trip_ok"] and [s["shards"] for s in out["shards"]] == [1, 2]
+    for bits in ("1024", "2016"):                                  # other row widths (edge rows self-checked)
+        r = subprocess.run([exe, bits, "777", "1", "1"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and json.loads(r.stdout.strip().splitlines()[-1])["round_trip_ok"], r.stderr

@@ -17,6 +17,7 @@
 #   opstrace       kernel trace of tools/prof_ops.py add,kway (the add / merge launch durations for pmc:add)
 #   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo)
 #   ghpair         tools/bin/ghpair_rate at 16 and 64 threads, tools/bin/ghpair_e2e
+#   marshal        tools/bin/marshal_rate: host mpz <-> row marshalling of 1, 2, 4, 8 concurrent shards (no kernels)
 #   ghsub          the operator- A/B: tools/bin/ghpair_rate at 16 threads, host powm vs FTHE_SHIM_MUL_ENGINE=1
 #   py:SCRIPT[,ARGS]  python SCRIPT ARGS (a tools/ measurement), appended to TAG_SCRIPT.jsonl
 R=${1:?tag}
@@ -91,6 +92,10 @@ for step in "$@"; do
       timeout -k 10 300 tools/bin/ghpair_e2e 2048 2000000 2 >> ${O}_ghpair_e2e.jsonl 2>> ${O}_ghpair.err \
         || fail ghpair_e2e $? ${O}_ghpair.err
       cat ${O}_ghpair_rate.jsonl ${O}_ghpair_e2e.jsonl;;
+    marshal)
+      timeout -k 10 300 tools/bin/marshal_rate 2048 1048576 3 1,2,4,8 >> ${O}_marshal.jsonl 2>> ${O}_marshal.err \
+        || fail marshal $? ${O}_marshal.err
+      cat ${O}_marshal.jsonl;;
     ghsub)
       for v in 0 1 0 1; do
         FTHE_SHIM_MUL_ENGINE=$v timeout -k 10 300 tools/bin/ghpair_rate 2048 16 8192 16 4096 > ${O}_one.json 2>> ${O}_ghsub.err \
