@@ -34,6 +34,7 @@
 #include "bn_host.hpp"
 #include "padic_tiles.hpp"
 #include "addb_image.hpp"
+#include "nadicb_image.hpp"
 #include "fthe_glue.h"
 #include "gen/montprog_blobs.h"
 
@@ -43,7 +44,7 @@ using namespace fthe;
 
 namespace {
 
-constexpr int MAX_VARIANTS = 9;
+constexpr int MAX_VARIANTS = 10;
 // s80: four lanes per element mod p^2 / q^2 of Paillier-2048 (small-batch decrypt latency);
 // 1000 + K: the P-adic exponentiation kernels mod P^2 (gen_padic.py, digits of K limbs, slots of 2K
 // limbs; the "S" here only names the variant): K = 37 runs on the s74 slots of Paillier-2048,
@@ -52,11 +53,13 @@ constexpr int MAX_VARIANTS = 9;
 // slots and programs, no fixed-base table ops;
 // 2000 + 76: the n-adic four-lane kernel (gen_nadic.py, base-n digits of 76 limbs) on the s152 slots;
 // 2100 + 76: its Montgomery form (gen_nadic.py mont: LSB-first reductions, no quotient estimates)
+// 2200 + 76: its matrix-core Barrett form (gen_nadicb.py: the products on the VALU, both Barrett reductions by n
+// on i8 MFMA; workgroups of kNbWaves waves, n of 2041..2048 bits)
 constexpr int kPadicS = 1037, kPadicK = 37, kPadicSmallK = 19, kNadicS = 2076, kPadicMfmaS = 1137,
-              kNadicMontS = 2176;
+              kNadicMontS = 2176, kNadicBarS = 2276;
 const Shape kVariants[MAX_VARIANTS] = {{37, 28, 1}, {74, 28, 1}, {152, 27, 4}, {80, 27, 4},
                                        {1000 + kPadicK, 28, 1}, {1000 + kPadicSmallK, 28, 1}, {kNadicS, 27, 4},
-                                       {kPadicMfmaS, 28, 1}, {kNadicMontS, 27, 4}};
+                                       {kPadicMfmaS, 28, 1}, {kNadicMontS, 27, 4}, {kNadicBarS, 27, 4}};
 constexpr Shape kLatShape{80, 27, 4};
 constexpr int kAddbBlob = 3152;           // fthe_addb_q152's code object in gen/montprog_blobs.h
 
@@ -323,6 +326,10 @@ struct fthe_key {
     bool nadic_mont = false;
     DevMod mnM;
     int c_Kn = -1;
+    // the matrix-core Barrett form (fthe_nadic_b76, the default for n of 2041..2048 bits; FTHE_NADIC_MONT=1
+    // keeps the Montgomery form): ctx = nadicb_image.hpp (LDS image, n limbs); the classical program
+    bool nadic_b = false;
+    DevMod mnB;
     // Paillier-1024 public-key encrypt (n of 1009..1030 bits) on the P-adic kernel with P = n
     bool padic_pub = false;
     DevMod mnP;
@@ -342,7 +349,7 @@ struct fthe_key {
     int pq_w = 0;
     ~fthe_key() {
         co.reset();
-        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA, &mnP, &mnM})
+        for (DevMod *d : {&mn2, &mp2, &mq2, &mp, &mq, &mp1, &mq1, &mp2l, &mq2l, &mpA, &mqA, &mnA, &mnP, &mnM, &mnB})
             if (d->d_ctx) (void)hipFree(d->d_ctx);
         if (d_consts) (void)hipFree(d_consts);
         if (d_progs) (void)hipFree(d_progs);
@@ -390,6 +397,7 @@ struct fthe_key {
     PH prP_dec_pre_p, prP_dec_pre_q, prP_dec_p, prP_dec_q, prP_dec_post_p, prP_dec_post_q;
     PH prN_enc_pub;                  // n-adic form of the public-key encrypt
     PH prM_enc_pub;                  // its Montgomery form (fthe_nadic_m76)
+    PH prB_enc_pub;                  // its matrix-core Barrett form (fthe_nadic_b76)
     PH prP_enc_pub;                  // P-adic form (P = n) of the Paillier-1024 public-key encrypt
 
     // ---- fixed-base randomizer (FTHE_ENC_FIXED_BASE), built on first use -----
@@ -508,7 +516,8 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
         if (!blob) return FTHE_ERR_HIP;
         HIPOK(hipModuleLoadData(&c->mod[i], blob));
         char name[64];
-        if (kVariants[i].S > 2100) snprintf(name, sizeof name, "fthe_nadic_m%d", kVariants[i].S - 2100);
+        if (kVariants[i].S > 2200) snprintf(name, sizeof name, "fthe_nadic_b%d", kVariants[i].S - 2200);
+        else if (kVariants[i].S > 2100) snprintf(name, sizeof name, "fthe_nadic_m%d", kVariants[i].S - 2100);
         else if (kVariants[i].S > 2000) snprintf(name, sizeof name, "fthe_nadic_q%d", kVariants[i].S - 2000);
         else if (kVariants[i].S > 1100) snprintf(name, sizeof name, "fthe_padic_m%d", kVariants[i].S - 1100);
         else if (kVariants[i].S > 1000) snprintf(name, sizeof name, "fthe_padic_k%d", kVariants[i].S - 1000);
@@ -714,6 +723,12 @@ static bool nadic_mont_ok(const fthe_key *k) {
     return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_CLASSICAL") && k->sn2.S == 152 && k->sn2.B == 27 &&
            k->sn2.lanes == 4 && mpz_sizeinbase(k->n, 2) <= 2048;
 }
+// its matrix-core Barrett form (fthe_nadic_b76, the default where it applies): n of 2041..2048 bits, n^2 on the
+// s152 slots; FTHE_NADIC_MONT=1 (A/B) or FTHE_NO_NADIC=1 turn it off
+static bool nadicb_ok(const fthe_key *k) {
+    return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_MONT") && !getenv("FTHE_NADIC_CLASSICAL") &&
+           k->sn2.S == 152 && k->sn2.B == 27 && k->sn2.lanes == 4 && nadicb::n_ok(k->n);
+}
 static int upload_nadic(DevMod &d, const mpz_t n, const mpz_t n2, Shape slots, bool classical = true) {
     d.m.init(n2, slots);
     MontMod dm;
@@ -782,6 +797,26 @@ static int key_finish(fthe_key *k) {
             h.alg = nadic_alg(x, k->n);
             h.exec = nadic_exec(x);
             k->prN_enc_pub = h;
+        }
+        // matrix-core Barrett form (tools/nadicb_model.py): the classical program (digits in [0, 3n) between
+        // products, CANON at the end); ctx: the LDS image and n's limbs (nadicb_image.hpp)
+        k->nadic_b = nadicb_ok(k);
+        if (k->nadic_b) {
+            std::vector<uint8_t> img;
+            if (!nadicb::build(k->n, img)) return FTHE_ERR_UNSUPPORTED;
+            k->mnB.m.init(k->n2, k->sn2);
+            if (hipMalloc(&k->mnB.d_ctx, img.size()) != hipSuccess) return FTHE_ERR_NOMEM;
+            HIPOK(hipMemcpy(k->mnB.d_ctx, img.data(), img.size(), hipMemcpyHostToDevice));
+            k->mnB.kernel_S = kNadicBarS;
+            if (k->c_n76 < 0) k->c_n76 = k->add_const(to_limbs(k->n, kNadicDigit.S, kNadicDigit.B));
+            Prog x;
+            x.loadx(SL_IN0); x.canon();
+            x.pow(k->n, SL_TAB, SL_SQ, k->w_pub);
+            x.mul(SL_C1); x.canon(); x.storex(SL_OUTP); x.end();
+            fthe_key::PH h = k->add_prog(x);
+            h.alg = nadic_alg(x, k->n);
+            h.exec = nadic_exec(x) / 2;             // the VALU half: the products (the reductions run on MFMA)
+            k->prB_enc_pub = h;
         }
         {
             // Montgomery form (tools/nadic_mont_model.py): the raw r is a Montgomery residue (value r R^-1),
@@ -1385,7 +1420,10 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     // only the workgroups that hold live elements (slot strides stay those of L)
     if (live > (size_t)L) return FTHE_ERR_ARG;
     if (live == 0) return FTHE_OK;
-    const unsigned blocks = (unsigned)((live * kVariants[vi].lanes + 255) / 256);
+    const bool nb = kVariants[vi].S == kNadicBarS;       // kNbPerWg ciphertexts per workgroup of kNbWaves waves
+    if (nb && L % kNbPerWg) return FTHE_ERR_ARG;          // the kernel covers whole workgroups of the slots
+    const unsigned blocks = nb ? (unsigned)((live + kNbPerWg - 1) / kNbPerWg)
+                               : (unsigned)((live * kVariants[vi].lanes + 255) / 256);
     std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
     if (c->prof) {
         if (c->prof_used == c->prof_ev.size()) {
@@ -1405,9 +1443,10 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     // workgroups onto one CU -- two waves per SIMD, each at half speed.  Dynamic LDS beyond half
     // the CU's 160 KB keeps one workgroup per CU while both launches fit on the chip together.
     unsigned shm = 0;
-    if (spread && 2 * blocks <= (unsigned)c->n_cu && c->static_lds[vi] < kSpreadLds)
+    if (!nb && spread && 2 * blocks <= (unsigned)c->n_cu && c->static_lds[vi] < kSpreadLds)
         shm = (unsigned)(kSpreadLds - c->static_lds[vi]);
-    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, 256, 1, 1, shm, st, nullptr, cfg) != hipSuccess)
+    if (hipModuleLaunchKernel(c->fn[vi], blocks, 1, 1, nb ? 64 * kNbWaves : 256, 1, 1, shm, st, nullptr, cfg) !=
+        hipSuccess)
         return FTHE_ERR_HIP;
     if (ev) {
         HIPOK(hipEventRecord(ev->second, st));
@@ -1511,10 +1550,12 @@ int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nsl
     if (k->device != c->device) return FTHE_ERR_ARG;
     if (!sh.S) return FTHE_ERR_UNSUPPORTED;
     HIPOK(hipSetDevice(c->device));
+    // L: a multiple of 768 ciphertexts -- the 256-thread glue grids and fthe_nadic_b76's workgroups of 192
+    // ciphertexts both cover the slots exactly
     size_t ch = (chunk ? chunk : chunk_lanes()) / (size_t)sh.lanes;    // same slot footprint per chunk
-    ch = (ch + 255) / 256 * 256;
-    size_t L = std::min(ch, (count + 255) / 256 * 256);
-    if (L == 0) L = 256;
+    ch = (ch + 767) / 768 * 768;
+    size_t L = std::min(ch, (count + 767) / 768 * 768);
+    if (L == 0) L = 768;
     Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = sh.S; Lc.B = sh.B;
     int rc = c->slots.ensure((size_t)nslots * sh.S * L * 4);
     Lc.base = c->slots.p;
@@ -1899,13 +1940,15 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             // c = cq + q^2 h   (< p^2 q^2 = n^2)
             mul_add_out(c->stream, Lc.grid(), Lc.slot(SL_OUTQ), S,
                         k->cst(k->c_q2), S, Lc.slot(SL_T2), S, L, cnt, out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
-        } else if (k->nadic || k->nadic_mont) {
+        } else if (k->nadic || k->nadic_mont || k->nadic_b) {
             // n-adic kernel: digits (r, 0) in IN0, (1, m) in C1; out = x0 + x1 n (x0, x1 < n: c < n^2)
             const int D = kNadicDigit.S;
             pack_rows(c->stream, rw, rwn, cnt, 0, Lc.slot(SL_IN0), S, L, Lc.B);
             Lc.fill(SL_C1, k->c_one_n2);
             m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_C1) + (size_t)D * L, D, L, Lc.B);
-            if (k->nadic_mont) {
+            if (k->nadic_b) {
+                if ((rc = Lc.prog(k->prB_enc_pub, k->mnB))) return rc;
+            } else if (k->nadic_mont) {
                 Lc.fill(SL_C2, k->c_Kn);
                 if ((rc = Lc.prog(k->prM_enc_pub, k->mnM))) return rc;
             } else if ((rc = Lc.prog(k->prN_enc_pub, k->mnA))) return rc;
@@ -3046,6 +3089,22 @@ extern "C" int fthe_debug_addb_image(const uint32_t *n, int n_words, uint8_t *ou
     mpz_import(nn, (size_t)n_words, -1, 4, 0, 0, n);
     std::vector<uint8_t> img;
     const bool ok = addb::build(nn, img);
+    mpz_clear(nn);
+    if (!ok) return FTHE_ERR_UNSUPPORTED;
+    *len = img.size();
+    if (!out) return FTHE_OK;
+    if (cap < img.size()) return FTHE_ERR_ARG;
+    memcpy(out, img.data(), img.size());
+    return FTHE_OK;
+}
+
+extern "C" int fthe_debug_nadicb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len) {
+    if (!n || n_words <= 0 || !len) return FTHE_ERR_ARG;
+    mpz_t nn;
+    mpz_init(nn);
+    mpz_import(nn, (size_t)n_words, -1, 4, 0, 0, n);
+    std::vector<uint8_t> img;
+    const bool ok = nadicb::build(nn, img);
     mpz_clear(nn);
     if (!ok) return FTHE_ERR_UNSUPPORTED;
     *len = img.size();

@@ -434,6 +434,11 @@ int fthe_debug_direct_y(fthe_key *key, fthe_ctx *ctx, uint64_t rng_seed, uint64_
  * out == NULL: only *len.  FTHE_ERR_UNSUPPORTED unless n^2 has 4095-4096 bits.
  * Host only (tests compare it with tools/addb_model.py addb_image). */
 int fthe_debug_addb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len);
+/* The per-key context of fthe_nadic_b76, the parties' public-key encrypt on base-n digits with matrix-core
+ * Barrett reductions (party.h:118-142 -> paillier.cpp:122-139): mu and n copies, column corrections, n's 27-bit
+ * limbs, built on the host from n exactly as at key set-up; out == NULL: only *len.  FTHE_ERR_UNSUPPORTED
+ * unless n is odd with 2041..2048 bits.  Host only (tests compare it with tools/nadicb_model.py). */
+int fthe_debug_nadicb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len);
 
 /* ---- profiling hooks: time of the last call's kernels on the stream ------ */
 double fthe_last_kernel_ms(fthe_ctx *ctx);

@@ -1,8 +1,11 @@
-"""The n-adic four-lane kernel (fthe_nadic_q76, gen_nadic.py) behind the public-key encrypt
-at Paillier-2048 (Party::encrypt_histogram, party.h:118-142 -> paillier.cpp:122-139): the same
-ciphertexts as the Montgomery s152 program it replaces (FTHE_NO_NADIC=1 at key set-up restores that),
-for injected r at the extremes and random r, u64 and word plaintexts, across a chunk boundary, on a
-public-only key too, and its launches really run.  Integer work: exact equality.
+"""The n-adic four-lane kernels behind the public-key encrypt at Paillier-2048 (Party::encrypt_histogram,
+party.h:118-142 -> paillier.cpp:122-139): the matrix-core Barrett form fthe_nadic_b76 (gen_nadicb.py,
+the default for n of 2041..2048 bits), the Montgomery form fthe_nadic_m76 (n of 1033..2048 bits, the default below
+2041; FTHE_NADIC_MONT=1 selects it everywhere) and the classical fthe_nadic_q76 (FTHE_NADIC_CLASSICAL=1): the
+same ciphertexts as each other and as the Montgomery s152 program they replace (FTHE_NO_NADIC=1), every one of
+them equal to the C oracle's (1 + m n) r^n mod n^2 on the sizes tested, for injected r at the extremes and random
+r, u64 and word plaintexts, across a chunk boundary, on a public-only key too, and their launches really run.
+Integer work: exact equality.
 """
 import ctypes
 import os
@@ -38,7 +41,7 @@ def _nadic_launches(dev, fn):
         vals = [ctypes.c_double() for _ in range(7)]
         assert lib.fthe_prof_read(dev.ctx, *[ctypes.byref(v) for v in vals]) == 0
         launches = 0.0
-        for variant in (2076, 2176):            # the classical and the Montgomery form (default)
+        for variant in (2076, 2176, 2276):      # the classical, Montgomery and matrix-core Barrett forms
             ms, nl = ctypes.c_double(), ctypes.c_double()
             assert lib.fthe_prof_variant(dev.ctx, variant, ctypes.byref(ms), ctypes.byref(nl)) == 0
             launches += nl.value
@@ -61,17 +64,20 @@ def _variant_launches(dev, fn, variant):
     return out, nl.value
 
 
-def test_montgomery_form_same_ciphertexts_as_classical(keys):
-    """fthe_nadic_m76 (Montgomery n-adic, default; tools/nadic_mont_model.py) against fthe_nadic_q76
-    (FTHE_NADIC_CLASSICAL=1) and the oracle's formula: injected r at the extremes (r >= n included) and
-    random, plaintexts up to 2^64 - 1, across a chunk boundary; each form's launches are its own kernel."""
+def test_three_forms_same_ciphertexts(keys):
+    """fthe_nadic_b76 (matrix-core Barrett, default at 2048 bits; tools/nadicb_model.py), fthe_nadic_m76
+    (FTHE_NADIC_MONT=1) and fthe_nadic_q76 (FTHE_NADIC_CLASSICAL=1): identical ciphertexts for injected r at the
+    extremes (r >= n included) and random, plaintexts up to 2^64 - 1, across a chunk boundary; each form's
+    launches are its own kernel; 64 of them against the formula (every one against the oracle below)."""
     dev, pa, pm = keys
     from fedtree_amd.paillier import Paillier
-    os.environ["FTHE_NADIC_CLASSICAL"] = "1"
-    try:
-        pc = Paillier.from_primes(pa.p, pa.q, dev)
-    finally:
-        del os.environ["FTHE_NADIC_CLASSICAL"]
+    forms = {}
+    for env, variant in (("FTHE_NADIC_MONT", 2176), ("FTHE_NADIC_CLASSICAL", 2076)):
+        os.environ[env] = "1"
+        try:
+            forms[variant] = Paillier.from_primes(pa.p, pa.q, dev)
+        finally:
+            del os.environ[env]
     rng = np.random.default_rng(SEED + 5)
     n = pa.modulus
     cnt = 98304 + 1000                          # one launch's 98,304 ciphertexts + a partial one
@@ -80,11 +86,13 @@ def test_montgomery_form_same_ciphertexts_as_classical(keys):
     m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
     m[:3] = [0, 2**64 - 1, 1]
     rw = pyoracle.ints_to_words(rs, pa.n_words)
-    ca, la = _variant_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True), 2176)
-    cc, lc = _variant_launches(dev, lambda: pc.encrypt_u64(m, r=rw, public=True), 2076)
-    assert la == lc and la >= 2
-    assert np.array_equal(ca, cc)
-    got = pyoracle.words_to_ints(ca[:64])
+    cb, lb = _variant_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True), 2276)
+    assert lb >= 2
+    for variant, pl in forms.items():
+        cv, lv = _variant_launches(dev, lambda: pl.encrypt_u64(m, r=rw, public=True), variant)
+        assert lv == lb, variant
+        assert np.array_equal(cb, cv), variant
+    got = pyoracle.words_to_ints(cb[:64])
     n2 = n * n
     for i in range(64):
         assert got[i] == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
@@ -154,30 +162,49 @@ def _prime_of_bits(rng, bits):
             return p
 
 
-# the Montgomery form (default) runs every n of 1033..2048 bits (n^2 on the s152 slots); the classical form
-# needs n >= 2^(27*76 - 10) for its quotient estimate (n of 2042..2048), below that FTHE_NADIC_CLASSICAL=1
-# keys fall back to the Montgomery s152 program (tests/test_gpu_nadic.py::test_classical_form_range)
-@pytest.mark.parametrize("nbits,nadic", [(2042, True), (2045, True), (2041, True), (2030, True), (1536, True)])
-def test_modulus_range_edges(nbits, nadic):
-    from fedtree_amd.paillier import Device, Paillier
-    dev = Device(0)
-    rng = np.random.default_rng(nbits)
+def _key_of_bits(rng, nbits):
     while True:
         p = _prime_of_bits(rng, nbits // 2)
         q = _prime_of_bits(rng, nbits - nbits // 2)
         n = p * q
-        if n.bit_length() == nbits:
-            break
+        if n.bit_length() == nbits and p != q:
+            return p, q, n
+
+
+# which kernel a party's key of n bits runs: the matrix-core Barrett form for n of 2041..2048 bits, the Montgomery
+# form for 1033..2040 (n^2 on the s152 slots; no quotient estimate, so no lower bound of its own), below 1033 bits
+# n^2 takes the s74 slots and neither n-adic form (1032: the Montgomery s74 program, 1009..1030: the P-adic one)
+@pytest.mark.parametrize("nbits,variant", [(2048, 2276), (2045, 2276), (2042, 2276), (2041, 2276), (2040, 2176),
+                                           (2030, 2176), (1536, 2176), (1033, 2176), (1032, None)])
+def test_modulus_range_edges(nbits, variant):
+    """every ciphertext of a party's public-key encrypt (600 per size, injected r incl. 1 and n - 1) equals the
+    C oracle's full formula PowerMod(g, m, n^2) PowerMod(r, n, n^2) (paillier.cpp:134-137), on the kernel the
+    size selects; all decrypt back"""
+    from fedtree_amd.paillier import Device, Paillier
+    dev = Device(0)
+    rng = np.random.default_rng(nbits)
+    p, q, n = _key_of_bits(rng, nbits)
     pl = Paillier.from_public(n, dev)
     cnt = 600
     rs = [1, n - 1] + [int.from_bytes(rng.bytes(260), "little") % (n - 1) + 1 for _ in range(cnt - 2)]
     m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
+    m[:2] = [0, 2**64 - 1]
     rw = pyoracle.ints_to_words(rs, pl.n_words)
     c, launches = _nadic_launches(dev, lambda: pl.encrypt_u64(m, r=rw))
-    assert launches == (1 if nadic else 0)
-    n2 = n * n
-    for i in (0, 1, 2, cnt - 1):                         # paillier.cpp:134-137 with g = n + 1
-        assert pyoracle.from_words(c[i]) == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, i
+    if variant is None:
+        assert launches == 0
+    else:
+        _, lv = _variant_launches(dev, lambda: pl.encrypt_u64(m, r=rw), variant)
+        assert launches == 1 and lv == 1
+    if pl.n_words % 2 == 0:                                  # the C oracle (GMP, threads): p, q of n_words / 2
+        o = pyoracle.COracle()
+        ok = o.key(pyoracle.to_words(p, pl.n_words // 2), pyoracle.to_words(q, pl.n_words // 2))
+        assert np.array_equal(c, ok.encrypt_batch(m, rw))
+    else:
+        n2 = n * n
+        got = pyoracle.words_to_ints(c)
+        for i in range(cnt):
+            assert got[i] == pow(n + 1, int(m[i]), n2) * pow(rs[i], n, n2) % n2, i
     full = Paillier.from_primes(p, q, dev)
     assert np.array_equal(full.decrypt_u64(c), m)
 

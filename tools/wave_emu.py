@@ -277,6 +277,20 @@ class Wave:
             raise NotImplementedError(op)
 
     def ds(self, op, a):
+        if op == 'ds_write2_b32':                  # two dwords at vaddr + 4 offset0 / + 4 offset1
+            o0 = o1 = 0
+            for t in a[3:]:
+                if t.startswith('offset0:'):
+                    o0 = int(t[8:], 0)
+                elif t.startswith('offset1:'):
+                    o1 = int(t[8:], 0)
+            for l in self.lanes():
+                base = self.vget(l, a[0])
+                for tok, oo in ((a[1], o0), (a[2], o1)):
+                    addr = base + 4 * oo
+                    assert 0 <= addr and addr + 4 <= len(self.lds) and addr % 4 == 0, f"LDS write2 at {addr}"
+                    self.lds[addr:addr + 4] = self.vget(l, tok).to_bytes(4, 'little')
+            return
         width = {'ds_read_b32': 4, 'ds_read_b64': 8, 'ds_read_b128': 16, 'ds_write_b32': 4, 'ds_write_b64': 8,
                  'ds_write_b128': 16}[op]
         off = 0
@@ -434,6 +448,12 @@ class Wave:
                 nv |= int(g(l, a[1]) > g(l, a[2])) << l
             self.vcc = nv
             return
+        if op == 'v_cmp_eq_u32_e32':
+            nv = 0
+            for l in lanes:
+                nv |= int(g(l, a[1]) == g(l, a[2])) << l
+            self.vcc = nv
+            return
         if op == 'v_cmp_ne_u32_e32':
             nv = 0
             for l in lanes:
@@ -475,6 +495,8 @@ class Wave:
                 r = g(l, a[1]) - g(l, a[2])
             elif op == 'v_subrev_u32_e32':
                 r = g(l, a[2]) - g(l, a[1])
+            elif op == 'v_mul_lo_u32':
+                r = g(l, a[1]) * g(l, a[2])
             elif op == 'v_mul_u32_u24_e32':
                 r = (g(l, a[1]) & 0xFFFFFF) * (g(l, a[2]) & 0xFFFFFF)
             elif op == 'v_add3_u32':
@@ -610,6 +632,60 @@ def selftest(ntests=16, count0=None):
     print("wave_emu selftest OK")
 
 
+def nadicb_selftest(seed=1, bits=2048, count=16):
+    """one wave of fthe_nadic_b76 (a workgroup generated with one wave: 16 ciphertexts): LOADX r; CANON;
+    STOREX T; SQR 1; STOREX U (digits up to 3n); SQR 1; MUL U; MUL T; CANON; STOREX OUT -> r^7 mod n^2 as
+    canonical digits, against Python integers (r: 0, 1, n - 1, random)"""
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
+    sys.path.insert(0, here)
+    import gen_nadicb as gb
+    import nadicb_model as nm
+    rng = random.Random(seed)
+    n = nm.rand_n(rng, bits)
+    N2 = n * n
+    S, L, B = 152, 16, 27
+    asm = gb.gen_nadicb('fthe_nadic_b76', waves=1)
+    nv = int(re.search(r'\.amdhsa_next_free_vgpr (\d+)', asm).group(1))
+    lds_bytes = int(re.search(r'\.amdhsa_group_segment_fixed_size (\d+)', asm).group(1))
+    ctx = bytearray(gb.CTX_BYTES)
+    img = nm.nadicb_image(n)
+    ctx[:len(img)] = img
+    for j in range(76):
+        ctx[gb.N_OFF + 4 * j:gb.N_OFF + 4 * j + 4] = ((n >> (B * j)) & ((1 << B) - 1)).to_bytes(4, 'little')
+    rs = [rng.randrange(n) for _ in range(L)]
+    rs[:3] = [0, 1, n - 1]
+    IN, T, U, OUT = 0, 1, 2, 3
+    slots = bytearray(4 * S * L * 4)
+    for g_, r in enumerate(rs):
+        for k in range(76):
+            off = (IN * S + k) * L * 4 + 4 * g_
+            slots[off:off + 4] = ((r >> (B * k)) & ((1 << B) - 1)).to_bytes(4, 'little')
+    prog = [1, IN, 20, 0, 2, T, 3, 1, 2, U, 3, 1, 4, U, 4, T, 20, 0, 2, OUT, 0, 0]
+    mem = Mem()
+    SB, PB, CB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000
+    mem.alloc(slots, SB)
+    mem.alloc(b''.join(w.to_bytes(4, 'little') for w in prog), PB)
+    mem.alloc(bytes(ctx), CB)
+    karg = SB.to_bytes(8, 'little') + PB.to_bytes(8, 'little') + CB.to_bytes(8, 'little') + \
+        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + bytes(4 + 128)
+    mem.alloc(karg, KA)
+    steps = run_workgroup(asm, lds_bytes, 1, mem, KA, 0, nv)
+    bad = 0
+    for g_ in range(count):
+        x0 = x1 = 0
+        for k in reversed(range(76)):
+            x0 = (x0 << B) + mem.read(SB + (OUT * S + k) * L * 4 + 4 * g_, 4)
+            x1 = (x1 << B) + mem.read(SB + (OUT * S + 76 + k) * L * 4 + 4 * g_, 4)
+        want = pow(rs[g_], 7, N2)
+        if not (x0 < n and x1 < n and x0 + x1 * n == want):
+            bad += 1
+            if bad <= 3:
+                print(f"  ciphertext {g_}: x0 {x0:#x}\n  x1 {x1:#x}\n  want {want:#x}")
+    print(f"nadic_b76: {count} ciphertexts, {bad} mismatches, {steps} wave-instructions emulated")
+    return bad
+
+
 def m37_selftest(seed=1, ab=None, bits=1024):
     """wave 0 of fthe_padic_m37 (one workgroup of 256 lanes, 4 waves fill the LDS tile image, wave 0 runs on):
     LOADP x; STOREX t; SQR 1; MUL t; STOREP -> x^3 mod P^2 (< 6 P^2), against Python integers on its 64 lanes
@@ -667,6 +743,8 @@ def m37_selftest(seed=1, ab=None, bits=1024):
 
 
 if __name__ == '__main__':
+    if len(sys.argv) > 1 and sys.argv[1] == 'nadicb':
+        sys.exit(1 if nadicb_selftest() else 0)
     if len(sys.argv) > 1 and sys.argv[1] == 'm37':
         sys.exit(1 if m37_selftest(ab=sys.argv[2] if len(sys.argv) > 2 else None) else 0)
     elif len(sys.argv) > 1:                   # e.g. 211: wave 0 takes a second batch (the grid-stride loop)
