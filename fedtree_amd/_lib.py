@@ -51,6 +51,7 @@ _PROTOS = {
     "fthe_host_alloc": (_I, [_SZ, _PP]),
     "fthe_debug_addb_image": (_I, [_P, _I, _P, _SZ, _P]),
     "fthe_debug_nadicb_image": (_I, [_P, _I, _P, _SZ, _P]),
+    "fthe_debug_nadicb_prog": (_I, [_P, _P, _P, _I, _P, _I, _SZ, _I, _P]),
     "fthe_host_free": (None, [_P]),
     "fthe_key_generate": (_I, [_P, _I, _U64, _PP]),
     "fthe_key_generate_ex": (_I, [_P, _I, _U64, _I, _PP]),

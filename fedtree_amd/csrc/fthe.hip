@@ -3098,6 +3098,39 @@ extern "C" int fthe_debug_addb_image(const uint32_t *n, int n_words, uint8_t *ou
     return FTHE_OK;
 }
 
+// Bring-up / test hook of fthe_nadic_b76: run an op program (uint32 pairs, gen_nadicb.py ops; prog_words words) on
+// the key's matrix-core Barrett n-adic kernel over `count` ciphertexts whose slots 0 .. nslots-1 are given as
+// host limbs (in: nslots x count x 152 limbs of 27 bits: digit x0 in limbs 0..75, x1 in 76..151); slot out_slot
+// is returned the same way.  FTHE_ERR_UNSUPPORTED unless the key runs fthe_nadic_b76.
+extern "C" int fthe_debug_nadicb_prog(fthe_key *k, fthe_ctx *c, const uint32_t *prog, int prog_words,
+                                      const uint32_t *in, int nslots, size_t count, int out_slot, uint32_t *out) {
+    if (!k || !c || !prog || prog_words < 2 || !in || nslots <= 0 || nslots > 16 || !count || !out ||
+        out_slot < 0 || out_slot >= nslots)
+        return FTHE_ERR_ARG;
+    if (!k->nadic_b) return FTHE_ERR_UNSUPPORTED;
+    Launch Lc;
+    int rc = begin_call(c, k, count, Lc, nslots, k->sn2);
+    if (rc) return rc;
+    if (count > (size_t)Lc.L) return FTHE_ERR_ARG;
+    const int S = Lc.S, L = Lc.L;
+    std::vector<uint32_t> slab((size_t)nslots * S * L, 0u);
+    for (int s = 0; s < nslots; s++)
+        for (size_t g = 0; g < count; g++)
+            for (int j = 0; j < S; j++) slab[((size_t)s * S + j) * L + g] = in[((size_t)s * count + g) * S + j];
+    HIPOK(hipMemcpy(Lc.base, slab.data(), slab.size() * 4, hipMemcpyHostToDevice));
+    Prog p;
+    p.w.assign(prog, prog + prog_words);
+    fthe_key::PH ph;
+    if ((rc = upload_dyn_prog(c, p, ph, c->io[3]))) return rc;
+    Lc.live = count;
+    if ((rc = launch_dyn(Lc, c->io[3].p, 0, k->mnB))) return rc;
+    HIPOK(hipStreamSynchronize(c->stream));
+    HIPOK(hipMemcpy(slab.data(), Lc.slot(out_slot), (size_t)S * L * 4, hipMemcpyDeviceToHost));
+    for (size_t g = 0; g < count; g++)
+        for (int j = 0; j < S; j++) out[g * S + j] = slab[(size_t)j * L + g];
+    return end_call(c, Lc);
+}
+
 extern "C" int fthe_debug_nadicb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len) {
     if (!n || n_words <= 0 || !len) return FTHE_ERR_ARG;
     mpz_t nn;
@@ -3188,10 +3221,11 @@ static int rowprod_impl(fthe_key *k, fthe_ctx *c, const uint32_t *const *xs, int
     const bool rowio = k->rowio && kk + 1 <= 16;
     Launch Lc;
     bool chain = classical && kk >= 2 && k->d_addb && c->fn_addb;
-    for (int j = 2; j < kk && chain; j++) {       // out must not overlap an input still to be read
+    for (int j = 0; j < kk && chain; j++) {       // out must not overlap an input still to be read
         const size_t bytes = count * 8 * (size_t)k->n_words;
         const char *o = (const char *)out, *x = (const char *)xs[j];
-        chain = o + bytes <= x || x + bytes <= o;
+        // the first launch reads x_0, x_1 row by row before writing that row: out may be exactly one of them
+        chain = o + bytes <= x || x + bytes <= o || (j < 2 && o == x);
     }
     if (chain) {
         // plain k-way products with a 2048-bit n: a chain of matrix-core Barrett adds over the whole batch,
@@ -3327,19 +3361,23 @@ struct GatherProd {
                            (const uint32_t *)c->io[3].p + prog_words, Lc.slot(SL_C0), Lc.S, Lc.L);
         return FTHE_OK;
     }
-    // idx: K x G host indices into src (rows of cw words)
-    int run(const uint32_t *src, const std::vector<int64_t> &idx, size_t G, uint32_t *dst) {
+    // idx: K x G host indices into src (rows of cw words; src holds src_rows rows)
+    int run(const uint32_t *src, size_t src_rows, const std::vector<int64_t> &idx, size_t G, uint32_t *dst) {
         int rc;
         HIPOK(hipStreamSynchronize(c->stream));          // previous pass done with scratch
         if ((rc = c->scratch.ensure(std::max<size_t>(8, idx.size() * 8)))) return rc;
         if (!idx.empty()) HIPOK(hipMemcpy(c->scratch.p, idx.data(), idx.size() * 8, hipMemcpyHostToDevice));
-        return run_dev(src, (const int64_t *)c->scratch.p, G, dst);
+        return run_dev(src, src_rows, (const int64_t *)c->scratch.p, G, dst);
     }
-    // gidx: K x G device indices into src
-    int run_dev(const uint32_t *src, const int64_t *gidx, size_t G, uint32_t *dst) {
+    // gidx: K x G device indices into src (src_rows rows)
+    int run_dev(const uint32_t *src, size_t src_rows, const int64_t *gidx, size_t G, uint32_t *dst) {
         const int cw = 2 * k->n_words, S = Lc.S, L = Lc.L;
         int rc;
-        if (k->d_addb && c->fn_addb && dst != src) {
+        // the chain of launches re-reads src after the first one has written dst: only for disjoint ranges
+        const size_t rb = (size_t)cw * 4;
+        const char *d0 = (const char *)dst, *s0 = (const char *)src;
+        const bool disjoint = d0 + G * rb <= s0 || s0 + src_rows * rb <= d0;
+        if (k->d_addb && c->fn_addb && disjoint) {
             // 2048-bit n: K - 1 matrix-core Barrett add launches over all G rows, gathered operands
             // (dst = src[i_0] src[i_1], then dst = dst src[i_j]; an index < 0 is the integer 1)
             if ((rc = launch_addb(c, k, src, src, dst, G, gidx, gidx + G))) return rc;
@@ -3398,6 +3436,7 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
     GatherProd gp{k, c};
     if ((rc = gp.init(maxg))) return rc;
     const uint32_t *src = x;
+    size_t src_rows = count;
     int bufsel = 1;
     std::vector<int64_t> gidx;
     while (true) {
@@ -3419,10 +3458,11 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
             if (ng > 1) done_after = false;
         }
         uint32_t *dst = done_after ? out : (uint32_t *)c->io[bufsel].p;
-        if ((rc = gp.run(src, gidx, G, dst))) return rc;
+        if ((rc = gp.run(src, src_rows, gidx, G, dst))) return rc;
         if (done_after) break;
         members.swap(next);
         src = dst;
+        src_rows = G;
         bufsel = 3 - bufsel;       // ping-pong io[1] / io[2]
     }
     return end_call(c, gp.Lc);
@@ -3433,8 +3473,8 @@ extern "C" int fthe_reduce_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t
 // group count per pass).  seg_ptr (nseg+1) and idx (nullable: identity) are
 // device arrays and are only read.
 namespace {
-int reduce_segments_csr(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64_t *seg_dev, const int64_t *idx_dev,
-                        size_t nseg, int64_t total, uint32_t *out) {
+int reduce_segments_csr(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t x_rows, const int64_t *seg_dev,
+                        const int64_t *idx_dev, size_t nseg, int64_t total, uint32_t *out) {
     const int K = GatherProd::K;
     const int cw = 2 * k->n_words;
     const size_t maxg = (size_t)total / K + nseg;                // groups of the first (largest) pass
@@ -3447,6 +3487,7 @@ int reduce_segments_csr(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64
     hipStream_t st = c->stream;
     const int64_t *seg = seg_dev, *members = idx_dev;
     const uint32_t *src = x;
+    size_t src_rows = x_rows;
     int bufsel = 1, gsel = 3;
     size_t n = nseg;
     while (true) {
@@ -3463,10 +3504,10 @@ int reduce_segments_csr(fthe_key *k, fthe_ctx *c, const uint32_t *x, const int64
                            (size_t)G, K, gidx);
         const bool last = (size_t)G == nseg;                      // one group per segment: final pass
         uint32_t *dst = last ? out : (uint32_t *)c->io[bufsel].p;
-        if ((rc = gp.run_dev(src, gidx, (size_t)G, dst))) return rc;
+        if ((rc = gp.run_dev(src, src_rows, gidx, (size_t)G, dst))) return rc;
         if (last) break;
         // next pass: segment s owns groups [gptr[s], gptr[s+1]) of dst, members = identity
-        seg = gptr; members = nullptr; src = dst;
+        seg = gptr; members = nullptr; src = dst; src_rows = (size_t)G;
         bufsel = 3 - bufsel; gsel = 7 - gsel;                      // ping-pong io[1]/io[2], hb[3]/hb[4]
         // n stays nseg: the segments are the same, only their members shrink
     }
@@ -3500,7 +3541,7 @@ extern "C" int fthe_reduce_segments_csr_dev(fthe_key *k, fthe_ctx *c, const uint
     if (ends[0] < 0 || (!idx && (size_t)ends[0] > count)) return FTHE_ERR_ARG;
     if (!x && ends[0]) return FTHE_ERR_ARG;
     (void)count;
-    return reduce_segments_csr(k, c, x, seg_ptr, idx, nseg, ends[0], out);
+    return reduce_segments_csr(k, c, x, count, seg_ptr, idx, nseg, ends[0], out);
 }
 
 // Histogram of a node on the device (hist_tree_builder.cpp:565-595 for the root,
@@ -3551,7 +3592,7 @@ static int histogram_impl(fthe_key *k, fthe_ctx *c, const uint32_t *x, size_t co
         hipLaunchKernelGGL(k_hist_scatter, dim3(gb), dim3(256), 0, st, bin_ids, n_col, d_cut, max_num_bin, inst, n_sel,
                            planes, n_bins, count, seg, cursor, idx);
     // io[0] (idx) and hb[1] (seg) stay untouched by the product passes (io[1]/io[2], hb[2..5])
-    if ((rc = reduce_segments_csr(k, c, x, seg, idx, nseg, total, out))) return rc;
+    if ((rc = reduce_segments_csr(k, c, x, (size_t)planes * count, seg, idx, nseg, total, out))) return rc;
     return enc_zero ? fold_zero_first(k, c, seg, nseg, enc_zero, out) : FTHE_OK;
 }
 
@@ -3610,7 +3651,7 @@ extern "C" int fthe_scan_segments_dev(fthe_key *k, fthe_ctx *c, const uint32_t *
                 gidx[(size_t)j * N + t] = from >= start[t] ? from : -1;
             }
         uint32_t *dst = p == npass - 1 ? out : (uint32_t *)c->io[bufsel].p;
-        if ((rc = gp.run(src, gidx, N, dst))) return rc;
+        if ((rc = gp.run(src, N, gidx, N, dst))) return rc;
         src = dst;
         bufsel = 3 - bufsel;
     }

@@ -123,9 +123,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     Z1B, Z2B = 14, 47                 # 33 dwords each (lane 3's dword 128 in local 32)
     BQ = 80                           # B operands, KB x 4 = v80..v99
     ACC = (100, 104)                  # two accumulator sets
-    AOP = (108, 112, 116)             # three A-operand buffers
-    DQ = 120                          # chunk dwords v120..v153 (34: the carry rides in DQ + g + 1)
-    GB = 154                          # group read buffer, 4 int64 = v154..v161
+    AOP = (108, 112, 116, 120)        # four A-operand buffers (reads two MFMAs ahead, as gen_addb)
+    DQ = 124                          # chunk dwords v124..v157 (34: the carry rides in DQ + g + 1)
+    GB = 158                          # group read buffer, 2 int64 = v158..v161
     PG, FV = 162, 164                 # int64 pairs
     CR = 166                          # chunk carry
     NVGPR = 168
@@ -588,7 +588,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 n, t, kb = ops[x]
                 off = KO + 16 * (4 * kb - t)
                 assert 0 <= off and off + 64 <= COPY
-                issue(('a', x), f'  ds_read_b128 {quad4(AOP[x % 3])}, v{A} offset:{off}')
+                issue(('a', x), f'  ds_read_b128 {quad4(AOP[x % 4])}, v{A} offset:{off}')
 
             def read_corr(n, t):
                 issue(('c', n), f'  ds_read_b128 {quad4(ACC[n % 2])}, v{V_C} offset:{corr + 64 * t}')
@@ -600,7 +600,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 if x == 0 or ops[x - 1][0] != n:
                     wait_for(('c', n))
                 wait_for(('a', x))
-                e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 3])}, {quad4(BQ + 4 * kb)}, '
+                e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
                   f'{quad4(ACC[n % 2])}')
                 if x + 2 < len(ops):
                     read_a(x + 2)
@@ -624,11 +624,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
             ng = 4 * len(tiles)
             cv = f"v{V_TMP}" if j else f"v{CR}"
-            for g0 in range(0, ng, 4):
-                for g in range(g0, min(ng, g0 + 4)):
+            for g0 in range(0, ng, 2):
+                for g in range(g0, min(ng, g0 + 2)):
                     e(f'  ds_read_b64 {pair(GB + 2 * (g - g0))}, v{V_GR} offset:{8 * g}')
                 e('  s_waitcnt lgkmcnt(0)')
-                for g in range(g0, min(ng, g0 + 4)):
+                for g in range(g0, min(ng, g0 + 2)):
                     if g % 2 == 0:
                         e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
                         cv = f"v{DQ + g + 1}"

@@ -439,6 +439,12 @@ int fthe_debug_addb_image(const uint32_t *n, int n_words, uint8_t *out, size_t c
  * limbs, built on the host from n exactly as at key set-up; out == NULL: only *len.  FTHE_ERR_UNSUPPORTED
  * unless n is odd with 2041..2048 bits.  Host only (tests compare it with tools/nadicb_model.py). */
 int fthe_debug_nadicb_image(const uint32_t *n, int n_words, uint8_t *out, size_t cap, size_t *len);
+/* Test hook of fthe_nadic_b76: run the op program `prog` (prog_words uint32) over `count` ciphertexts whose slots
+ * 0 .. nslots-1 are given as host limbs (nslots x count x 152 limbs of 27 bits: x0 in 0..75, x1 in 76..151) and
+ * return slot out_slot the same way.  FTHE_ERR_UNSUPPORTED unless the key runs fthe_nadic_b76 (n of 2041..2048
+ * bits).  For tests and bring-up only. */
+int fthe_debug_nadicb_prog(fthe_key *key, fthe_ctx *ctx, const uint32_t *prog, int prog_words, const uint32_t *in,
+                           int nslots, size_t count, int out_slot, uint32_t *out);
 
 /* ---- profiling hooks: time of the last call's kernels on the stream ------ */
 double fthe_last_kernel_ms(fthe_ctx *ctx);

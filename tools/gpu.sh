@@ -10,9 +10,11 @@
 #   trace          the bench's timed region under rocprofv3 --kernel-trace --stats
 #   pmc:W          separate PMC passes (one counter group per run, never with tracing) over workload W:
 #                    enc  the bench's encrypt at 262,144 pairs (fthe_padic_m37 + s74 tails)
-#                    add  one device-resident P-2048 add of 1M ciphertexts (s152 row I/O)
+#                    add  one device-resident P-2048 add of 1M distinct ciphertext pairs (fthe_addb_q152)
+#                    addsame  the same with x = y (each row read once for both operands: counter calibration)
 #                    kway three 8-party merges of 1,048,576 bins
-#                    pub  public-key encrypt of 131,072 ciphertexts (tools/nadic_ab.py)
+#                    pub  public-key encrypt of 196,608 ciphertexts on fthe_nadic_b76 and fthe_nadic_m76
+#                         (tools/nadicb_ab.py; the PMC summary separates the kernels by name)
 #                  then: python tools/rocprof_summary.py pmc gpurun_out/TAG_pmc_W_* out.json (CPU side)
 #   opstrace       kernel trace of tools/prof_ops.py add,kway (the add / merge launch durations for pmc:add)
 #   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo)
@@ -32,8 +34,9 @@ pmc_pass() {  # workload tag counters...
   case $w in
     enc)  cmd="python3 bench.py --pairs 262144 --steps 1 --warmup 0 --no-cpu --no-secondary";;
     add)  cmd="python3 tools/prof_ops.py --n 1048576 --ops add";;
+    addsame) cmd="python3 tools/prof_ops.py --n 1048576 --ops addsame";;
     kway) cmd="python3 tools/prof_ops.py --n 1048576 --ops kway";;
-    pub)  cmd="python3 tools/nadic_ab.py 131072";;
+    pub)  cmd="python3 tools/nadicb_ab.py 196608 1";;
     *) echo "unknown pmc workload $w"; exit 2;;
   esac
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d ${O}_pmc_${w}_${tag} -- $cmd \

@@ -1,5 +1,6 @@
 """Small driver for kernel traces / counters of the mod-n^2 (four-lane) kernel:
-one device-resident add, one 8-way reduce, one Montgomery-resident add, one party encrypt
+one device-resident add of distinct rows (addsame: the same rows as both operands, half the unique bytes),
+one 8-way reduce, one Montgomery-resident add, one party encrypt
 from published bases and one histogram scatter at Paillier-2048 (--ops selects).
 
   python tools/prof_ops.py [--n 262144]
@@ -32,10 +33,17 @@ def main():
         return
     o = torch.empty_like(c)
     ops = a.ops.split(",")
-    if "add" in ops:
-        pl.add_dev(c, c, o)
+    if "add" in ops:                                  # distinct operand rows (the bench's adds): 2 n rows read
+        c2 = torch.empty_like(c)
+        pl.encrypt_u64_dev(m, c2, seed=2)
+        pl.add_dev(c, c2, o)
         dev.sync()
         print("add", n, "ms", dev.last_kernel_ms())
+        del c2
+    if "addsame" in ops:                              # x = y: each row read once for both operands (calibration)
+        pl.add_dev(c, c, o)
+        dev.sync()
+        print("addsame", n, "ms", dev.last_kernel_ms())
     if "kway" in ops:
         x = torch.stack([c] * 8)
         for _ in range(3):                            # configs[3] at --n 2097152 (256 x 4096 bins x {g, h})
