@@ -206,6 +206,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_lshrrev_b32_e32 v{V_TMP}, 6, v{V_LANE}')                    # wave
     e(f'  v_mul_u32_u24_e32 v{V_TMP}, {WAVE_AREA}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_TMP}, {IMG_BYTES}, v{V_TMP}')              # wave area base
+    e(f'  v_mov_b32_e32 v{V_A2X}, v{V_TMP}')                           # (kept for V_G, V_B below)
     e(f'  v_and_b32_e32 v{V_LANE}, 63, v{V_LANE}')                     # lane
     e(f'  v_lshrrev_b32_e32 v{V_TMP + 1}, 2, v{V_LANE}')               # c (ciphertext of the wave)
     e(f'  v_lshl_add_u32 v{V_LDSI}, v{V_TMP + 1}, 2, v{V_TMP}')        # area + 4 c
@@ -237,12 +238,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_add_u32_e32 v{V_G}, {GST_OFF}, v{V_G}')                   # group row m + 8 h (area added below)
     e(f'  v_mul_u32_u24_e32 v{V_TMP}, {QROW}, v{V_TMP + 1}')
     e(f'  v_add_u32_e32 v{V_B}, v{V_B}, v{V_TMP}')                    # staging row m + 16 h (area below)
-    e(f'  v_lshrrev_b32_e32 v{V_TMP}, 6, v{V_LANE}')
-    e(f'  v_mov_b32_e32 v{V_TMP + 1}, 0')
-    e(f'  v_mul_u32_u24_e32 v{V_TMP}, {WAVE_AREA}, v{V_TMP}')
-    e(f'  v_add_u32_e32 v{V_TMP}, {IMG_BYTES}, v{V_TMP}')
-    e(f'  v_add_u32_e32 v{V_G}, v{V_G}, v{V_TMP}')
-    e(f'  v_add_u32_e32 v{V_B}, v{V_B}, v{V_TMP}')
+    e(f'  v_add_u32_e32 v{V_G}, v{V_G}, v{V_A2X}')                    # + the wave's area
+    e(f'  v_add_u32_e32 v{V_B}, v{V_B}, v{V_A2X}')
     e(f'  v_lshlrev_b32_e32 v{V_SH}, 1, v{V_SH}')                      # 2 k
     e(f'  v_lshlrev_b32_e32 v{V_LANE}, 2, v{V_LANE}')                  # lane * 4 (unused now; kept)
     e('  s_add_u32 s36, s8, ' + hex(N_OFF))

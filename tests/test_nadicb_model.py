@@ -87,4 +87,4 @@ def test_host_image_matches_model():
 
 def test_kernel_on_wave_emulator():
     import wave_emu
-    assert wave_emu.nadicb_selftest() == 0
+    assert wave_emu.nadicb_selftest(waves=2) == 0          # two waves: per-wave LDS areas and rows

@@ -632,7 +632,7 @@ def selftest(ntests=16, count0=None):
     print("wave_emu selftest OK")
 
 
-def nadicb_selftest(seed=1, bits=2048, count=16):
+def nadicb_selftest(seed=1, bits=2048, count=16, waves=1):
     """one wave of fthe_nadic_b76 (a workgroup generated with one wave: 16 ciphertexts): LOADX r; CANON;
     STOREX T; SQR 1; STOREX U (digits up to 3n); SQR 1; MUL U; MUL T; CANON; STOREX OUT -> r^7 mod n^2 as
     canonical digits, against Python integers (r: 0, 1, n - 1, random)"""
@@ -644,8 +644,9 @@ def nadicb_selftest(seed=1, bits=2048, count=16):
     rng = random.Random(seed)
     n = nm.rand_n(rng, bits)
     N2 = n * n
-    S, L, B = 152, 16, 27
-    asm = gb.gen_nadicb('fthe_nadic_b76', waves=1)
+    S, L, B = 152, 16 * waves, 27
+    count = max(count, L) if waves > 1 else count
+    asm = gb.gen_nadicb('fthe_nadic_b76', waves=waves)
     nv = int(re.search(r'\.amdhsa_next_free_vgpr (\d+)', asm).group(1))
     lds_bytes = int(re.search(r'\.amdhsa_group_segment_fixed_size (\d+)', asm).group(1))
     ctx = bytearray(gb.CTX_BYTES)
@@ -670,7 +671,7 @@ def nadicb_selftest(seed=1, bits=2048, count=16):
     karg = SB.to_bytes(8, 'little') + PB.to_bytes(8, 'little') + CB.to_bytes(8, 'little') + \
         (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + bytes(4 + 128)
     mem.alloc(karg, KA)
-    steps = run_workgroup(asm, lds_bytes, 1, mem, KA, 0, nv)
+    steps = run_workgroup(asm, lds_bytes, waves, mem, KA, 0, nv)
     bad = 0
     for g_ in range(count):
         x0 = x1 = 0
@@ -744,7 +745,7 @@ def m37_selftest(seed=1, ab=None, bits=1024):
 
 if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'nadicb':
-        sys.exit(1 if nadicb_selftest() else 0)
+        sys.exit(1 if nadicb_selftest(waves=int(sys.argv[2]) if len(sys.argv) > 2 else 1) else 0)
     if len(sys.argv) > 1 and sys.argv[1] == 'm37':
         sys.exit(1 if m37_selftest(ab=sys.argv[2] if len(sys.argv) > 2 else None) else 0)
     elif len(sys.argv) > 1:                   # e.g. 211: wave 0 takes a second batch (the grid-stride loop)
