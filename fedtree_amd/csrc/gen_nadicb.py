@@ -75,7 +75,8 @@ IMG_BYTES = CORR2_OFF + TILES2 * 64
 N_OFF = IMG_BYTES                                     # n limbs (76 x u32) in ctx, not copied to LDS
 CTX_BYTES = N_OFF + 4 * S
 QROW = 400                       # q / r staging row: 80 dwords used; 100 dwords == 4 mod 32 (4-way stores)
-GROW = 296                       # group staging row (one chunk: <= 32 int64 groups + pad)
+GROW = 304                       # group staging row (one chunk: <= 32 int64 groups + pad; 16-byte aligned rows
+                                 # for the normalisation's ds_read_b128 of two groups)
 QST_OFF = 0                      # staging areas inside the wave area (the A column is dead in the Barretts)
 GST_OFF = 16 * QROW
 WAVE_AREA = max(ROWS * RB, GST_OFF + 16 * GROW)
@@ -124,9 +125,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     BQ = 80                           # B operands, KB x 4 = v80..v99
     ACC = (100, 104)                  # two accumulator sets
     AOP = (108, 112, 116, 120)        # four A-operand buffers (reads two MFMAs ahead, as gen_addb)
-    DQ = 124                          # chunk dwords v124..v157 (34: the carry rides in DQ + g + 1)
-    GB = 158                          # group read buffer, 2 int64 = v158..v161
-    PG, FV = 162, 164                 # int64 pairs
+    DQ = 124                          # chunk dwords v124..v155 (the carry rides in DQ + g + 1 until g + 1 is done)
+    GB = 156                          # group read buffers: 2 x (2 int64) = v156..v163, ds_read_b128 each
+    PG = FV = 164                     # int64 pair (the fold's group; the normalisation's odd-group sum)
     CR = 166                          # chunk carry
     NVGPR = 168
     assert T2B + 2 * NT <= V_AI[0] and V_A2X < NVGPR
@@ -472,7 +473,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 if j == 16:
                     handoff(T2B, u)
             if not last:
-                e('  s_waitcnt lgkmcnt(0)')
+                e('  s_waitcnt lgkmcnt(2)')                      # the prefetch reads (issued before the writes)
 
         e(f'{lab}:')
         for k in range(NT):
@@ -621,18 +622,26 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
             ng = 4 * len(tiles)
             cv = f"v{V_TMP}" if j else f"v{CR}"
+            # two groups per ds_read_b128, two buffers: the read of groups g + 2, g + 3 is in flight while
+            # g, g + 1 are normalised (LDS returns in order: lgkmcnt(1) waits for the older read only)
+            def rd(g):
+                e(f'  ds_read_b128 {quad4(GB + 4 * ((g // 2) % 2))}, v{V_GR} offset:{8 * g}')
+            rd(0)
+            if ng > 2:
+                rd(2)
             for g0 in range(0, ng, 2):
-                for g in range(g0, min(ng, g0 + 2)):
-                    e(f'  ds_read_b64 {pair(GB + 2 * (g - g0))}, v{V_GR} offset:{8 * g}')
-                e('  s_waitcnt lgkmcnt(0)')
-                for g in range(g0, min(ng, g0 + 2)):
+                e(f'  s_waitcnt lgkmcnt({1 if g0 + 2 < ng else 0})')
+                for g in (g0, g0 + 1):
+                    src = pair(GB + 4 * ((g0 // 2) % 2) + 2 * (g - g0))
                     if g % 2 == 0:
-                        e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
+                        e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {src}')
                         cv = f"v{DQ + g + 1}"
                     else:
-                        e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
+                        e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {src}')
                         e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
                         cv = f"v{FV + 1}"
+                if g0 + 4 < ng:
+                    rd(g0 + 4)
             e(f'  v_mov_b32_e32 v{CR}, {cv}')
             e('  s_mov_b64 exec, -1')
 
@@ -669,7 +678,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e('  s_waitcnt lgkmcnt(0)')
 
     def clear_dq():
-        for i in range(34):
+        for i in range(32):
             e(f'  v_mov_b32_e32 v{DQ + i}, 0')
 
     def stage_q3():
