@@ -591,24 +591,30 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             def read_corr(n, t):
                 issue(('c', n), f'  ds_read_b128 {quad4(ACC[n % 2])}, v{V_C} offset:{corr + 64 * t}')
 
+            # A operands are read three MFMAs ahead into four buffers (the buffer re-filled after MFMA x is MFMA
+            # x - 1's, whose operands were read at its issue); tile n - 1 is folded right after tile n's FIRST
+            # MFMA (>= 18 wait states after tile n - 1's last: the MFMA and three s_nops), and tile n + 1's
+            # corrections (its accumulators' srcC, the set tile n - 1 used) are read then, a whole tile ahead
             read_corr(0, tiles[0])
-            for x in range(min(2, len(ops))):
+            if len(tiles) > 1:
+                read_corr(1, tiles[1])
+            for x in range(min(3, len(ops))):
                 read_a(x)
             for x, (n, t, kb) in enumerate(ops):
-                if x == 0 or ops[x - 1][0] != n:
+                first = x == 0 or ops[x - 1][0] != n
+                if first:
                     wait_for(('c', n))
                 wait_for(('a', x))
                 e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
                   f'{quad4(ACC[n % 2])}')
-                if x + 2 < len(ops):
-                    read_a(x + 2)
-                last = x + 1 == len(ops) or ops[x + 1][0] != n
-                if last:
-                    if n >= 1:
-                        e('  s_nop 7')
-                        e('  s_nop 7')
-                        fold_tile(ACC[(n - 1) % 2], 4 * (tiles[n - 1] - t0))
-                        q.append(('w', n - 1))
+                if x + 3 < len(ops):
+                    read_a(x + 3)
+                if first and n >= 1:
+                    e('  s_nop 7')
+                    e('  s_nop 7')
+                    e('  s_nop 3')
+                    fold_tile(ACC[(n - 1) % 2], 4 * (tiles[n - 1] - t0))
+                    q.append(('w', n - 1))
                     if n + 1 < len(tiles):
                         read_corr(n + 1, tiles[n + 1])
             e('  s_nop 7')
