@@ -109,6 +109,9 @@ def layout_header():
 
 
 def gen_nadicb(name: str, waves: int = WAVES) -> str:
+    # timing-only switches (wrong results; fedtree_amd/build.py never lets FTHE_GEN_* reach the in-tree library):
+    # noprod (no VALU product steps), nobarrett (no reductions), nomfma (no MFMAs), noconv (no z -> dword moves)
+    DBG = set(os.environ.get("FTHE_GEN_NADICB_DBG", "").split(","))
     DPP = "row_mask:0xf bank_mask:0xf"
     LDSB = lds_bytes(waves)
     # ---- VGPRs ---------------------------------------------------------------------------------------------
@@ -487,6 +490,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         # trip), then TL steps
         NTRIP, TL = S // NT, S % NT
         assert NT % 2 == 0 and TL > 0
+        if "noprod" in DBG:
+            e(f'  s_branch {lab}_skip')
         e(f'  s_mov_b32 s18, {NTRIP}')
         e(f'{lab}_trip:')
         for u in range(NT):
@@ -498,6 +503,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         for u in range(TL):
             step(u, u, u == TL - 1)
         e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB)}, v{V_LDSI}')
+        if "noprod" in DBG:
+            e(f'{lab}_skip:')
         e('  s_waitcnt lgkmcnt(0)')
         # ---- normalise both windows: positions TL .. TL + 18 -> 19 limbs (z limbs 76 + 19 k + j) --------
         for tb, tag in ((T1B, 'n1'), (T2B, 'n2')):
@@ -509,7 +516,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             ripple_quad(f'{lab}_{tag}', lambda k, tb=tb: Tlo(tb, TL + k), Q)
         # ---- z1, z2 -> dwords Z1, Z2 (quad layout of the add kernel) ----------------------------------------
         for tb, zb, row0, tag in ((T1B, Z1B, 0, 'z1'), (T2B, Z2B, S, 'z2')):
-            to_dwords(zb, row0, lambda k, tb=tb: Tlo(tb, TL + k))
+            if "noconv" not in DBG:
+                to_dwords(zb, row0, lambda k, tb=tb: Tlo(tb, TL + k))
         e('  s_branch .Lbarrett')
 
     def to_dwords(zb, row0, W):
@@ -605,8 +613,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 if first:
                     wait_for(('c', n))
                 wait_for(('a', x))
-                e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
-                  f'{quad4(ACC[n % 2])}')
+                if "nomfma" not in DBG:
+                    e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
+                      f'{quad4(ACC[n % 2])}')
                 if x + 3 < len(ops):
                     read_a(x + 3)
                 if first and n >= 1:
@@ -819,6 +828,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 e(f'  v_and_b32_e32 {X(jj)}, {hex(MASK)}, {X(jj)}')
 
     e('.Lbarrett:')
+    if "nobarrett" in DBG:
+        e('  s_branch .Lbarrett_end')
     # ---- Barrett 1: z1 -> q3_1, r1 (new x0) ---------------------------------------------------------------
     stage_q1(Z1B)
     clear_dq()
@@ -850,6 +861,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     stage_q3()
     mfma_product(2)
     remainder_to_digit(Z2B, X1, 'b2')
+    e('.Lbarrett_end:')
     e('  s_cmp_eq_u32 s19, 0')
     e('  s_cbranch_scc1 .Lprog')
     e('  s_sub_u32 s19, s19, 1')
