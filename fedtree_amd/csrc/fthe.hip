@@ -723,10 +723,13 @@ static bool nadic_mont_ok(const fthe_key *k) {
     return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_CLASSICAL") && k->sn2.S == 152 && k->sn2.B == 27 &&
            k->sn2.lanes == 4 && mpz_sizeinbase(k->n, 2) <= 2048;
 }
-// its matrix-core Barrett form (fthe_nadic_b76, the default where it applies): n of 2041..2048 bits, n^2 on the
-// s152 slots; FTHE_NADIC_MONT=1 (A/B) or FTHE_NO_NADIC=1 turn it off
+// its matrix-core Barrett form (fthe_nadic_b76; opt-in, FTHE_NADIC_BARRETT=1 at key set-up): n of 2041..2048 bits,
+// n^2 on the s152 slots.  Bit-exact, but measured slower than the Montgomery form (477k vs 519k public-key
+// encrypts/s, tools/nadicb_ab.py): its VALU products run at the issue rate, its reductions at about half of it
+// (DESIGN.md 8), so fthe_nadic_m76 stays the default
 static bool nadicb_ok(const fthe_key *k) {
-    return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_MONT") && !getenv("FTHE_NADIC_CLASSICAL") &&
+    const char *b = getenv("FTHE_NADIC_BARRETT");
+    return b && *b == '1' && !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_MONT") && !getenv("FTHE_NADIC_CLASSICAL") &&
            k->sn2.S == 152 && k->sn2.B == 27 && k->sn2.lanes == 4 && nadicb::n_ok(k->n);
 }
 static int upload_nadic(DevMod &d, const mpz_t n, const mpz_t n2, Shape slots, bool classical = true) {
