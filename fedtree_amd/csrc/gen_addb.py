@@ -103,6 +103,11 @@ CHUNKS = [list(range(0, 8)), list(range(8, 16)), list(range(16, 24)), list(range
 
 
 def gen_addb(name: str) -> str:
+    # timing-only knock-outs (wrong results; a library built elsewhere, tools/addb_lib_ab.sh): noprod (no product
+    # MADs), nomfma (no MFMAs), nonorm (no group normalisation), nobarrett (no q1/q3 staging, products, folds),
+    # nocanon (no conditional subtractions); stamp: per-phase s_memtime cycle sums per wave, written after the
+    # launch's output rows (tools/addb_stamps.py; the stamps' lgkmcnt(0) drains cost some overlap)
+    DBG = set(os.environ.get("FTHE_GEN_ADDB_DBG", "").split(","))
     o = []
     e = o.append
     DPP = "row_mask:0xf bank_mask:0xf"
@@ -110,8 +115,11 @@ def gen_addb(name: str) -> str:
     V_TID, V_ROW, V_LDSI, V_AI, V_SH = 0, 1, 2, (3, 4), 5
     V_TMP = 6                                     # pair 6:7
     XB = 8                                        # X limbs v8..v45 (product phase), later other limbs
-    TB = 46                                       # ring of NT 64-bit columns v46..v125
-    NT = Q + 2
+    TB = 46                                       # ring of NT 64-bit columns v46..v121
+    NT = Q
+    HO = 122                                      # hand-off pair v[122:123] (v123 = 0 in the product phase): the
+                                                  # column lane j+1 retired, src2 of the next step's top MAD
+    VMASK = 124                                   # 2^27 - 1 on quad lanes 0..2, 0 on lane 3
     WD = 47                                       # W dwords (after the product) v47..v78: W[i], W[i+1] of odd i
                                                   # is an even register pair (one ds_write_b64)
     ZLB = 80                                      # z mod 2^4104 dwords v80..v111, v112 = bits 4096..4103
@@ -158,7 +166,7 @@ def gen_addb(name: str) -> str:
     # s[36:37] y index list (0: direct rows), s[38:39] carry scratch of the gathered addresses
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
     LIVE = "s[28:29]"
-    NSGPR = 40
+    NSGPR = 60 if "stamp" in DBG else 40
 
     e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
     e('.amdhsa_code_object_version 5')
@@ -256,6 +264,10 @@ def gen_addb(name: str) -> str:
     e(f'  v_and_b32_e32 v{V_TID}, 63, v{V_TID}')
     e(f'  v_lshlrev_b32_e32 v{V_TID}, 7, v{V_TID}')                    # v0 = lane * 128 from here on
     e('.Lbatch:')
+    if "prio" in DBG:
+        e('  s_setprio 3')
+    if "prioinv" in DBG:
+        e('  s_setprio 0')
     e('  s_cmp_ge_u32 s13, s12')
     e('  s_cbranch_scc1 .Lend')
     # ROW = g*512 + j*128 = first*512 + lane*128; live lanes: g < count
@@ -394,9 +406,19 @@ def gen_addb(name: str) -> str:
     e('  s_waitcnt lgkmcnt(0)')
 
     e('// @phase product')
+    e(f'  v_mov_b64_e32 {pair(HO)}, 0')
+    e(f'  v_mov_b32_e32 v{VMASK}, {hex(MASK)}')
+    e(f'  v_cndmask_b32_e64 v{VMASK}, v{VMASK}, 0, s[20:21]')
+    if "prio" in DBG:
+        e('  s_setprio 0')
+    if "prioinv" in DBG:
+        e('  s_setprio 3')
     # ---- 2. z = x y: 152 steps; step i reads a_i (prefetched), adds a_i X into the window, retires the
     #         lowest column: its carry stays in the lane's next column, its low 27 bits go one lane down (the
-    #         top column of lane j-1), and lane 0's -- the product limb z_i -- into A-column row i ---------
+    #         top column of lane j-1: one v_and_b32 with DPP into the hand-off pair, lane 3 receiving 0, that
+    #         the next step's top multiply-add takes as its addend, so the ring needs no fresh column), and
+    #         lane 0's -- the product limb z_i, written unmasked and masked when read back -- into A-column
+    #         row i.  Three VALU instructions per step beside the 38 multiply-adds. -------------------------
     for k in range(NT):
         e(f'  v_mov_b64_e32 {T(k)}, 0')
     e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
@@ -405,28 +427,25 @@ def gen_addb(name: str) -> str:
     def step(u, row, prefetch):
         ai, nai = f"v{V_AI[u % 2]}", f"v{V_AI[(u + 1) % 2]}"
         for k in range(Q):
-            e(f'  v_mad_u64_u32 {T(u + k)}, vcc, {ai}, {X(k)}, {T(u + k)}')
+            if "noprod" not in DBG:
+                src2 = pair(HO) if k == Q - 1 else T(u + k)   # T(u + Q - 1): the slot of the retired T(u - 1)
+                e(f'  v_mad_u64_u32 {T(u + k)}, vcc, {ai}, {X(k)}, {src2}')
             if k == 2:
                 e(f'  v_lshrrev_b64 {tmp}, {B}, {T(u)}')
             if k == 5:
                 e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
-            if k == 7:
-                e(f'  v_and_b32_e32 {Tlo(u)}, {hex(MASK)}, {Tlo(u)}')
             if k == 10 and prefetch is not None:
                 e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{prefetch * RB}')
             if k == 12:                              # after the read: the step's wait leaves the write out
                 e('  s_mov_b64 exec, s[22:23]')
                 e(f'  ds_write_b32 v{V_LDSI}, {Tlo(u)} offset:{row * RB}')
                 e('  s_mov_b64 exec, -1')
-            if k == 14:
-                e(f'  v_cndmask_b32_e64 {Tlo(u)}, {Tlo(u)}, 0, s[22:23]')
-        e(f'  v_mov_b32_dpp {Tlo(u + Q)}, {Tlo(u)} quad_perm:[1,2,3,0] {DPP}')
-        e(f'  v_mov_b32_e32 {Thi(u + Q)}, 0')
+        e(f'  v_and_b32_dpp v{HO}, {Tlo(u)}, v{VMASK} quad_perm:[1,2,3,0] {DPP}')
         if prefetch is not None:
             e('  s_waitcnt lgkmcnt(1)')
 
     NTRIP, TL = S // NT, S % NT
-    assert NT % 2 == 0
+    assert NT % 2 == 0 and TL == 0
     e(f'  s_mov_b32 s18, {NTRIP}')
     e('.Ltrip:')
     for u in range(NT):
@@ -440,10 +459,14 @@ def gen_addb(name: str) -> str:
     e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB)}, v{V_LDSI}')
 
     e('// @phase window')
+    if "prio" in DBG:
+        e('  s_setprio 3')
+    if "prioinv" in DBG:
+        e('  s_setprio 0')
     # ---- 3. window -> W limbs (X), W -> dwords WD; z mod 2^4104 limbs (LDS) -> dwords ZL ---------------
     e(f'  v_mov_b64_e32 {tmp}, 0')
-    for k in range(Q):
-        e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TL + k)}')
+    for k in range(Q):                            # columns 152 + k: T(k), the top one in the hand-off pair
+        e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TL + k) if k < Q - 1 else pair(HO)}')
         e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
         e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
     ripple_quad('.Lrw', X, Q, (V_TMP, V_TMP + 1))
@@ -451,9 +474,13 @@ def gen_addb(name: str) -> str:
     for k in range(Q):
         e(f'  ds_read_b32 {X(k)}, v{V_ZR} offset:{k * RB}')
     e('  s_waitcnt lgkmcnt(0)')
+    for k in range(Q):                            # the limbs were stored with their carries above bit 27
+        e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, {X(k)}')
     limbs_to_words(X, lambda i: f"v{ZLB + i}", f"v{V_AI[1]}", f"v{V_AI[0]}")
     e(f'  v_lshrrev_b32_e32 v{ZL128}, 19, {X(Q - 1)}')                # lane 3: bits 4096..4103 (limb 151 >> 19)
 
+    if "nobarrett" in DBG:
+        e('  s_branch .Ldbg_sub')
     e('// @phase q1stage')
     # ---- 4. q1 staging: dword 0 = bits 4072..4103 (lane 3), dwords 1.. = W, 129..143 = 0 (fed 0) --------
     e(f'  v_lshrrev_b32_e32 v{V_TMP}, 8, v{ZLB + 31}')
@@ -524,8 +551,9 @@ def gen_addb(name: str) -> str:
                 if first:
                     wait_for(('c', n))
                 wait_for(('a', x))
-                e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
-                  f'{quad4(ACC[n % 2])}')
+                if "nomfma" not in DBG:
+                    e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
+                      f'{quad4(ACC[n % 2])}')
                 if x + 2 < len(ops):
                     read_a(x + 2)
                 last = x + 1 == len(ops) or ops[x + 1][0] != n
@@ -547,6 +575,8 @@ def gen_addb(name: str) -> str:
                 e('  s_nop 1')
                 e(f'  v_mov_b32_dpp v{CR2}, v{CR} quad_perm:[0,0,1,2] {DPP}')
             e('// @phase norm')
+            if "nonorm" in DBG:
+                continue
             e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
             ng = 4 * len(tiles)
             # D_g = low dword of (group g + carry), carry = its high dword (signed): one v_mad_i64_i32 per
@@ -612,6 +642,7 @@ def gen_addb(name: str) -> str:
     mfma_product(2)
     # lane 3 keeps D2_128's low 8 bits (r2 mod 2^4104)
 
+    e('.Ldbg_sub:')
     e('// @phase sub')
     # ---- 7. r = (z - r2) mod 2^4104: borrow chains per lane, rippled across the quad --------------------
     def borrow_ripple(lab, R, R128_, bo, bin_):
@@ -642,6 +673,8 @@ def gen_addb(name: str) -> str:
     e(f'  v_and_b32_e32 v{R128}, 0xff, v{R128}')                        # r = (z - r2) mod 2^4104, < 3N
 
     e('// @phase canon')
+    if "nocanon" in DBG:
+        e('  s_branch .Ldbg_store')
     # ---- 8. two conditional subtractions of N, then the canonical row ------------------------------------
     e(f'  v_bfe_u32 v{V_TMP}, v{V_ROW}, 7, 2')
     e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_TMP}')                     # 128 j
@@ -663,20 +696,65 @@ def gen_addb(name: str) -> str:
         for i in range(32):
             e(f'  v_cndmask_b32_e32 v{RR + i}, v{RR + i}, v{TT + i}, vcc')
         e(f'  v_cndmask_b32_e32 v{R128}, v{R128}, v{TT128}, vcc')
+    e('.Ldbg_store:')
     e('// @phase store')
     e(f'  s_mov_b64 exec, {LIVE}')
     for i in range(8):
         e(f'  global_store_dwordx4 v{V_ROW}, {quad4(RR + 4 * i)}, s[8:9] offset:{16 * i}')
     e('  s_mov_b64 exec, -1')
     e('  s_add_u32 s13, s13, s19')
+    e('// @phase loop')
     e('  s_branch .Lbatch')
     e('.Lend:')
+    e('// @stampout')
     e('  s_waitcnt vmcnt(0)')
     e('  s_endpgm')
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
     e('')
+    if "stamp" in DBG:
+        o = stamp_pass(o)
     return "\n".join(o) + "\n" + descriptor(name, LDS_BYTES, NVGPR, NSGPR)
+
+
+STAMP_PHASES = ['entry', 'load', 'product', 'window', 'q1stage', 'prod1', 'norm', 'q3stage', 'prod2', 'sub',
+                'canon', 'store', 'loop']
+
+
+def stamp_pass(o):
+    """the stamp build: every '// @phase X' marker adds the cycles since the last stamp to the accumulator of the
+    phase the marker ends (the textually previous one; the loop head is ended by 'load'), s[40:41] the last
+    stamp, s45 + p the sums, s58 the wave's global index, s59 the batches; after the last batch lane 0 stores
+    16 dwords per wave at out + 512 count + 64 wave: the 13 sums, the batches, 0, 0"""
+    acc = {ph: 45 + i for i, ph in enumerate(STAMP_PHASES)}
+    out, cur = [], 'entry'
+
+    def stamp(ended):
+        return ['  s_memtime s[42:43]', '  s_waitcnt lgkmcnt(0)', '  s_sub_u32 s44, s42, s40',
+                f'  s_add_u32 s{acc[ended]}, s{acc[ended]}, s44', '  s_mov_b64 s[40:41], s[42:43]']
+    for line in o:
+        if line.startswith('// @phase'):
+            ph = line.split()[2]
+            ended = 'loop' if ph == 'load' else cur
+            out += stamp(ended)
+            if ph == 'load':
+                out.append('  s_add_u32 s59, s59, 1')
+            cur = ph
+            out.append(line)
+        elif line == '// @stampout':
+            out += ['  s_mov_b64 exec, 1', '  s_lshl_b32 s44, s12, 9', '  s_lshl_b32 s42, s58, 6',
+                    '  s_add_u32 s44, s44, s42', '  v_mov_b32_e32 v1, s44']
+            for i, ph in enumerate(STAMP_PHASES):
+                out += [f'  v_mov_b32_e32 v2, s{acc[ph]}', f'  global_store_dword v1, v2, s[8:9] offset:{4 * i}']
+            out += ['  v_mov_b32_e32 v2, s59', f'  global_store_dword v1, v2, s[8:9] offset:{4 * len(STAMP_PHASES)}']
+        elif line == '.Lbatch:':
+            # first pass: zero the sums, the wave's index, the first stamp
+            out += [f'  s_mov_b32 s{45 + i}, 0' for i in range(len(STAMP_PHASES))]
+            out += ['  s_mov_b32 s59, 0', '  s_lshr_b32 s58, s13, 4', '  s_memtime s[40:41]', '  s_waitcnt lgkmcnt(0)',
+                    '.Lbatch:']
+        else:
+            out.append(line)
+    return out
 
 
 def descriptor(name, lds_bytes, nvgpr, nsgpr):

@@ -205,6 +205,15 @@ class Wave:
             ln = self.lanes()
             self.sset(a[0], self.vget(ln[0] if ln else 0, a[1]))
             return
+        if op == 'v_and_b32_dpp':                  # dst = dpp(src0) & src1
+            perm = [int(x) for x in re.search(r'quad_perm:\[([0-9,]+)\]', ' '.join(a)).group(1).split(',')]
+            src, msk, dst = self.rr(a[1])[1], self.rr(a[2])[1], self.rr(a[0])[1]
+            old, om = list(self.v[src]), list(self.v[msk])
+            for l in self.lanes():
+                sl = (l & ~3) + perm[l & 3]
+                assert self.exec >> sl & 1, "DPP source lane disabled"
+                self.v[dst][l] = old[sl] & om[l]
+            return
         if op == 'v_mov_b32_dpp':
             perm = [int(x) for x in re.search(r'quad_perm:\[([0-9,]+)\]', ' '.join(a)).group(1).split(',')]
             src = self.rr(a[1])[1]
