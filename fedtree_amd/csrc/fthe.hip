@@ -1413,6 +1413,15 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     static_assert(sizeof(args) == 168, "kernarg layout of gen_montprog.py");
     if (nrows > 16) return FTHE_ERR_ARG;
     for (int i = 0; i < nrows; i++) args.rows[i] = rows[i];
+    // timing builds only (FTHE_GEN_M37_AB=stamp, tools/m37_stamps.py): FTHE_STAMP_PTR = a device buffer of
+    // FTHE_STAMP_LAUNCHES x 128 KiB, one 128 KiB record area per launch in turn; other kernels ignore rows[15]
+    static const char *stamp_ptr = getenv("FTHE_STAMP_PTR");
+    static std::atomic<unsigned> stamp_launch{0};
+    if (stamp_ptr && nrows < 16) {
+        static const unsigned nl = getenv("FTHE_STAMP_LAUNCHES") ? (unsigned)atoi(getenv("FTHE_STAMP_LAUNCHES")) : 1;
+        const unsigned i = stamp_launch.fetch_add(1);
+        if (i < nl) args.rows[15] = (const char *)(uintptr_t)strtoull(stamp_ptr, nullptr, 0) + (size_t)i * 131072;
+    }
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     // programs without fixed-base table ops (the key's own) may take the MFMA-Barrett P-adic kernel

@@ -30,7 +30,9 @@ per wave, 12 waves per workgroup (one workgroup per CU: its LDS holds the key's 
      conditional subtractions of N (dwords from the key's context) make it canonical; rows are stored.
 
 kernarg: 0 u64 x rows, 8 u64 y rows, 16 u64 out rows, 24 u64 kctx, 32 u32 count, 36 u32 workgroups launched
-(persistent: each wave takes batches of 16 ciphertexts wg*12 + wave, + 12 * workgroups, ...), 40 u64 x index
+(persistent: workgroup wg owns the batches of 16 ciphertexts wg, wg + workgroups, ...; its waves take them in
+turn from a counter in LDS, so a wave that the SIMD's arbiter favours takes more of them and the 12 waves end
+together), 40 u64 x index
 list, 48 u64 y index list (0: row g is operand row g; else operand row g is row idx[g] of the operand array,
 idx[g] < 0 the integer 1: the gathered products of the histogram scatter / segment sums).
 kctx: the LDS image (IMG_BYTES: mu copies, N copies, corrections), then N as 128 dwords, then the row 1.
@@ -59,7 +61,8 @@ ONE_OFF = N_OFF + 512                        # the integer 1 as a row (gathered 
 KCTX_BYTES = ONE_OFF + 512
 WAVE_AREA = 10496                            # A column (152 x 68) / q staging (16 x 656) / groups (16 x 296)
 LDS_WAVES = IMG_BYTES
-LDS_BYTES = LDS_WAVES + WAVES * WAVE_AREA    # 153,856
+LDS_CNT = LDS_WAVES + WAVES * WAVE_AREA      # the workgroup's batch counter (dword)
+LDS_BYTES = LDS_CNT + 16                     # 153,872
 QROW = 656                                   # q staging row: 9 K-blocks of 64 bytes, stride = 4 (mod 32)
                                              # dwords: the quads' staging writes 4-way, not 16-way, per bank
 GROW = 296                                   # group staging row (36 int64 groups + pad: conflict-free)
@@ -166,7 +169,7 @@ def gen_addb(name: str) -> str:
     # s[36:37] y index list (0: direct rows), s[38:39] carry scratch of the gathered addresses
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
     LIVE = "s[28:29]"
-    NSGPR = 60 if "stamp" in DBG else 40
+    NSGPR = 68 if "stamp" in DBG else 40
 
     e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
     e('.amdhsa_code_object_version 5')
@@ -206,19 +209,21 @@ def gen_addb(name: str) -> str:
         e(f'  ds_write_b128 v{V_LDSI}, v[8:11]')
         if part:
             e('  s_mov_b64 exec, s[16:17]')
+    e(f'  v_cmp_eq_u32_e32 vcc, 0, v{V_TID}')                           # thread 0: batch counter = 0
+    e('  s_and_saveexec_b64 s[16:17], vcc')
+    e(f'  v_mov_b32_e32 v{V_TMP}, {hex(LDS_CNT)}')
+    e(f'  v_mov_b32_e32 v{V_TMP + 1}, 0')
+    e(f'  ds_write_b32 v{V_TMP}, v{V_TMP + 1}')
+    e('  s_mov_b64 exec, s[16:17]')
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
-    # ---- the wave's batches of 16 ciphertexts: batch b = wg * WAVES + wave, then b += nwg * WAVES (kernarg
-    #      36: the launch's workgroup count) -- persistent waves, no workgroup tails, phases desynchronise ----
+    # ---- the wave's batches of 16 ciphertexts: the k-th batch the workgroup hands out is wg + k * nwg
+    #      (kernarg 36: the launch's workgroup count) -- persistent waves, no workgroup tails --------------
     e(f'  v_lshrrev_b32_e32 v{V_SH}, 6, v{V_TID}')                     # wave
     e('  s_nop 1')                                                      # VALU write -> v_readfirstlane: 1 state
     e('  v_readfirstlane_b32 s14, v5')
-    e('  s_load_dword s19, s[0:1], 0x24')
-    e(f'  s_mul_i32 s13, s2, {WAVES}')
-    e('  s_add_u32 s13, s13, s14')
-    e(f'  s_lshl_b32 s13, s13, 4')                                      # first ciphertext of the wave
+    e('  s_load_dword s19, s[0:1], 0x24')                              # workgroups launched
     e('  s_waitcnt lgkmcnt(0)')
-    e(f'  s_mul_i32 s19, s19, {WAVES * CT_PER_WAVE}')                   # ciphertexts per sweep of the grid
     # wave area base + 4c; lane j's A-column write base (rows 38j ..), the ciphertext's A column
     e(f'  s_mul_i32 s15, s14, {WAVE_AREA}')
     e(f'  s_add_u32 s15, s15, {LDS_WAVES}')
@@ -264,6 +269,17 @@ def gen_addb(name: str) -> str:
     e(f'  v_and_b32_e32 v{V_TID}, 63, v{V_TID}')
     e(f'  v_lshlrev_b32_e32 v{V_TID}, 7, v{V_TID}')                    # v0 = lane * 128 from here on
     e('.Lbatch:')
+    e('  s_mov_b64 exec, 1')                                            # lane 0 takes the next batch
+    e(f'  v_mov_b32_e32 v{V_TMP}, {hex(LDS_CNT)}')
+    e(f'  v_mov_b32_e32 v{V_TMP + 1}, 1')
+    e(f'  ds_add_rtn_u32 v{XB}, v{V_TMP}, v{V_TMP + 1}')
+    e('  s_waitcnt lgkmcnt(0)')
+    e('  s_mov_b64 exec, -1')
+    e('  s_nop 1')
+    e(f'  v_readfirstlane_b32 s13, v{XB}')
+    e('  s_mul_i32 s13, s13, s19')
+    e('  s_add_u32 s13, s13, s2')
+    e('  s_lshl_b32 s13, s13, 4')                                       # first ciphertext of the batch
     if "prio" in DBG:
         e('  s_setprio 3')
     if "prioinv" in DBG:
@@ -702,7 +718,6 @@ def gen_addb(name: str) -> str:
     for i in range(8):
         e(f'  global_store_dwordx4 v{V_ROW}, {quad4(RR + 4 * i)}, s[8:9] offset:{16 * i}')
     e('  s_mov_b64 exec, -1')
-    e('  s_add_u32 s13, s13, s19')
     e('// @phase loop')
     e('  s_branch .Lbatch')
     e('.Lend:')
@@ -725,7 +740,8 @@ def stamp_pass(o):
     """the stamp build: every '// @phase X' marker adds the cycles since the last stamp to the accumulator of the
     phase the marker ends (the textually previous one; the loop head is ended by 'load'), s[40:41] the last
     stamp, s45 + p the sums, s58 the wave's global index, s59 the batches; after the last batch lane 0 stores
-    16 dwords per wave at out + 512 count + 64 wave: the 13 sums, the batches, 0, 0"""
+    16 dwords per wave at out + 512 count + 64 wave: the 13 sums, the batches, the s_memtime and s_memrealtime
+    (100 MHz) ticks from the first batch to the end (the clock: their ratio x 100 MHz)"""
     acc = {ph: 45 + i for i, ph in enumerate(STAMP_PHASES)}
     out, cur = [], 'entry'
 
@@ -742,16 +758,21 @@ def stamp_pass(o):
             cur = ph
             out.append(line)
         elif line == '// @stampout':
+            out += ['  s_memtime s[42:43]', '  s_memrealtime s[64:65]', '  s_waitcnt lgkmcnt(0)',
+                    '  s_sub_u32 s62, s42, s62', '  s_sub_u32 s63, s64, s60']
             out += ['  s_mov_b64 exec, 1', '  s_lshl_b32 s44, s12, 9', '  s_lshl_b32 s42, s58, 6',
                     '  s_add_u32 s44, s44, s42', '  v_mov_b32_e32 v1, s44']
-            for i, ph in enumerate(STAMP_PHASES):
-                out += [f'  v_mov_b32_e32 v2, s{acc[ph]}', f'  global_store_dword v1, v2, s[8:9] offset:{4 * i}']
+            for i, ph in enumerate(STAMP_PHASES):        # 'entry' (never stamped): the first batch's realtime
+                out += [f'  v_mov_b32_e32 v2, s{acc[ph] if ph != "entry" else 60}',
+                        f'  global_store_dword v1, v2, s[8:9] offset:{4 * i}']
             out += ['  v_mov_b32_e32 v2, s59', f'  global_store_dword v1, v2, s[8:9] offset:{4 * len(STAMP_PHASES)}']
+            out += ['  v_mov_b32_e32 v2, s62', f'  global_store_dword v1, v2, s[8:9] offset:{4 * len(STAMP_PHASES) + 4}']
+            out += ['  v_mov_b32_e32 v2, s63', f'  global_store_dword v1, v2, s[8:9] offset:{4 * len(STAMP_PHASES) + 8}']
         elif line == '.Lbatch:':
             # first pass: zero the sums, the wave's index, the first stamp
             out += [f'  s_mov_b32 s{45 + i}, 0' for i in range(len(STAMP_PHASES))]
-            out += ['  s_mov_b32 s59, 0', '  s_lshr_b32 s58, s13, 4', '  s_memtime s[40:41]', '  s_waitcnt lgkmcnt(0)',
-                    '.Lbatch:']
+            out += ['  s_mov_b32 s59, 0', f'  s_mul_i32 s58, s2, {WAVES}', '  s_add_u32 s58, s58, s14', '  s_memtime s[40:41]', '  s_memrealtime s[60:61]',
+                    '  s_waitcnt lgkmcnt(0)', '  s_mov_b32 s62, s40', '.Lbatch:']
         else:
             out.append(line)
     return out

@@ -661,6 +661,10 @@ def gen_padic_mfma(name: str) -> str:
     e('.p2align 8')
     e(f'.type {name},@function')
     e(f'{name}:')
+    STAMP = "stamp" in AB                        # timing build: each wave's start / end realtime (100 MHz) and
+    if STAMP:                                    # where it ran, 16 B at kernarg rows[15] + 16 (4 wg + wave)
+        e('  s_memrealtime s[80:81]')
+        e('  s_mov_b32 s85, s2')
     e('  s_load_dwordx2 s[4:5], s[0:1], 0x0')
     e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
     e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
@@ -875,6 +879,26 @@ def gen_padic_mfma(name: str) -> str:
         e('  s_cbranch_scc0 .Lpp_end')
         e('  s_barrier')
         e('.Lpp_end:')
+    if STAMP:
+        e('  s_waitcnt vmcnt(0)')
+        e('  s_memrealtime s[82:83]')
+        e('  s_getreg_b32 s84, hwreg(HW_REG_HW_ID)')
+        e('  s_getreg_b32 s86, hwreg(HW_REG_XCC_ID)')
+        e('  s_load_dwordx2 s[88:89], s[0:1], 0xa0')
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_cmp_eq_u64 s[88:89], 0')
+        e('  s_cbranch_scc1 .Lstamp_done')
+        e('  s_mov_b64 exec, 1')
+        e(f'  v_lshrrev_b32_e32 v2, 6, v{V_TID}')
+        e(f'  v_lshl_add_u32 v2, s85, {3 if PP else 2}, v2')             # wave index in the launch
+        e('  v_lshlrev_b32_e32 v7, 4, v2')
+        e('  v_mov_b32_e32 v2, s80')
+        e('  v_mov_b32_e32 v3, s82')
+        e('  v_mov_b32_e32 v4, s84')
+        e('  v_mov_b32_e32 v5, s86')
+        e('  global_store_dwordx4 v7, v[2:5], s[88:89]')
+        e('  s_waitcnt vmcnt(0)')
+        e('.Lstamp_done:')
     e('  s_endpgm')
 
     # reduce (SQR, MUL): T (x0^2 or x0 y0), V (cross terms) -> x0 = T mod P, x1 = (V + T div P) mod P
@@ -915,7 +939,7 @@ def gen_padic_mfma(name: str) -> str:
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
     e('')
-    o.extend(_descriptor(name, LDS_BYTES, NVGPR, NSGPR, max_wg=512 if PP else 256).splitlines())
+    o.extend(_descriptor(name, LDS_BYTES, NVGPR, 90 if STAMP else NSGPR, max_wg=512 if PP else 256).splitlines())
     return "\n".join(o) + "\n"
 
 

@@ -39,12 +39,20 @@ def main():
     live = rec[rec[:, 13] > 0]
     batches = live[:, 13]
     per = {ph: round(float(np.mean(live[:, i] / batches)), 1) for i, ph in enumerate(PHASES) if ph != 'entry'}
-    per['entry_total'] = round(float(np.mean(live[:, 0])), 1)
-    wave_cycles = live[:, :13].sum(axis=1)
+    start = live[:, 0] - live[:, 0].min()                      # realtime ticks (10 ns), first batch
+    end = start + live[:, 15]
+    q = [0, 0.01, 0.1, 0.5, 0.9, 0.99, 1]
+    dist = {"start_us": [round(float(x) * 0.01, 2) for x in np.quantile(start, q)],
+            "end_us": [round(float(x) * 0.01, 2) for x in np.quantile(end, q)],
+            "batches": [int(x) for x in np.quantile(batches, q)],
+            "us_per_batch": [round(float(x) * 0.01, 2) for x in np.quantile(live[:, 15] / batches, q)]}
+    wave_cycles = live[:, 1:13].sum(axis=1)
     res = {"adds": n, "waves": int(len(live)), "batches_per_wave_mean": round(float(batches.mean()), 2),
            "kernel_ms": round(ms, 4), "cycles_per_batch_per_wave": per,
-           "wave_cycles_per_batch": round(float(np.mean((wave_cycles - live[:, 0]) / batches)), 1),
-           "implied_clock_ghz": round(float(np.median(wave_cycles)) / (ms * 1e-3) / 1e9, 3)}
+           "wave_cycles_per_batch": round(float(np.mean(wave_cycles / batches)), 1), "quantiles": q, **dist,
+           "implied_clock_ghz": round(float(np.median(wave_cycles)) / (ms * 1e-3) / 1e9, 3),
+           "memtime_over_realtime_ghz": round(float(np.median(live[:, 14] / live[:, 15])) * 0.1, 3),
+           "wave_realtime_ms_max": round(float(live[:, 15].max()) * 1e-5, 4)}
     print(json.dumps(res), flush=True)
 
 

@@ -286,6 +286,15 @@ class Wave:
             raise NotImplementedError(op)
 
     def ds(self, op, a):
+        if op == 'ds_add_rtn_u32':                 # vdst = old; LDS[vaddr + offset] += vdata (lanes in order)
+            off = next((int(t[7:], 0) for t in a[3:] if t.startswith('offset:')), 0)
+            for l in self.lanes():
+                addr = self.vget(l, a[1]) + off
+                assert 0 <= addr and addr + 4 <= len(self.lds) and addr % 4 == 0, f"LDS atomic at {addr}"
+                old = int.from_bytes(self.lds[addr:addr + 4], 'little')
+                self.lds[addr:addr + 4] = ((old + self.vget(l, a[2])) & 0xffffffff).to_bytes(4, 'little')
+                self.vset(l, a[0], old)
+            return
         if op == 'ds_write2_b32':                  # two dwords at vaddr + 4 offset0 / + 4 offset1
             o0 = o1 = 0
             for t in a[3:]:
