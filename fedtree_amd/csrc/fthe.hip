@@ -228,6 +228,8 @@ struct fthe_ctx {
     hipFunction_t fn[MAX_VARIANTS] = {};
     hipModule_t mod_addb = nullptr;           // fthe_addb_q152 (gen_addb.py): P-2048 adds, matrix-core Barrett
     hipFunction_t fn_addb = nullptr;
+    uint32_t *d_jobctr = nullptr;             // job counters of persistent launches (one per launch, in turn)
+    unsigned jobctr_i = 0;
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
     DevBuf hb[6];                           // histogram CSR / segmented-product plan (device)
     DevBuf ezm;                             // zero-first folds: Enc(0) rows masked to the populated segments
@@ -556,6 +558,7 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (c->side) (void)hipStreamSynchronize(c->side);
     for (int i = 0; i < MAX_VARIANTS; i++) if (c->mod[i]) (void)hipModuleUnload(c->mod[i]);
     if (c->mod_addb) (void)hipModuleUnload(c->mod_addb);
+    if (c->d_jobctr) (void)hipFree(c->d_jobctr);
     if (c->cub_tmp) (void)hipFree(c->cub_tmp);
     for (auto &e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1432,10 +1435,22 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     // only the workgroups that hold live elements (slot strides stay those of L)
     if (live > (size_t)L) return FTHE_ERR_ARG;
     if (live == 0) return FTHE_OK;
+    // fthe_padic_m37 built with dynamic jobs (FTHE_GEN_M37_AB=dyn, A/B under FTHE_M37_DYN=1): the resident
+    // workgroups only, a zeroed job counter per launch (gen_padic_mfma.py DYN)
+    static const bool m37_dyn = getenv("FTHE_M37_DYN") && *getenv("FTHE_M37_DYN") == '1';
+    const bool dyn = mfma && m37_dyn && nrows < 15;
     const bool nb = kVariants[vi].S == kNadicBarS;       // kNbPerWg ciphertexts per workgroup of kNbWaves waves
     if (nb && L % kNbPerWg) return FTHE_ERR_ARG;          // the kernel covers whole workgroups of the slots
-    const unsigned blocks = nb ? (unsigned)((live + kNbPerWg - 1) / kNbPerWg)
-                               : (unsigned)((live * kVariants[vi].lanes + 255) / 256);
+    unsigned blocks = nb ? (unsigned)((live + kNbPerWg - 1) / kNbPerWg)
+                         : (unsigned)((live * kVariants[vi].lanes + 255) / 256);
+    if (dyn) {
+        if (!c->d_jobctr) HIPOK(hipMalloc(&c->d_jobctr, 256 * sizeof(uint32_t)));
+        blocks = std::min(blocks, 2u * (unsigned)c->n_cu);          // 249 VGPRs: two waves per SIMD
+        uint32_t *ctr = c->d_jobctr + (c->jobctr_i++ % 256);
+        args.pad = 4 * blocks;
+        args.rows[14] = ctr;
+        if (hipMemsetAsync(ctr, 0, sizeof(uint32_t), st) != hipSuccess) return FTHE_ERR_HIP;
+    }
     std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
     if (c->prof) {
         if (c->prof_used == c->prof_ev.size()) {

@@ -661,6 +661,11 @@ def gen_padic_mfma(name: str) -> str:
     e('.p2align 8')
     e(f'.type {name},@function')
     e(f'{name}:')
+    # DYN: persistent waves with dynamic jobs -- the launch holds at most the resident workgroups; job j = the
+    # lanes [64 j, 64 j + 64); a wave's first job is 4 wg + wave (the static mapping), the next ones come from a
+    # device counter (kernarg rows[14], zeroed by the launcher) offset by the waves launched (kernarg 0x24), so
+    # a wave the SIMD's arbiter favours runs more jobs and the launch has no workgroup-granular tail
+    DYN = "dyn" in AB and not PP
     STAMP = "stamp" in AB                        # timing build: each wave's start / end realtime (100 MHz) and
     if STAMP:                                    # where it ran, 16 B at kernarg rows[15] + 16 (4 wg + wave)
         e('  s_memrealtime s[80:81]')
@@ -669,7 +674,14 @@ def gen_padic_mfma(name: str) -> str:
     e('  s_load_dwordx2 s[6:7], s[0:1], 0x8')
     e('  s_load_dwordx2 s[8:9], s[0:1], 0x10')
     e('  s_load_dwordx2 s[10:11], s[0:1], 0x18')
+    if DYN:
+        e('  s_load_dwordx2 s[92:93], s[0:1], 0x20')                  # live lanes, waves launched
+        e('  s_load_dwordx2 s[94:95], s[0:1], 0x98')                  # job counter
     e('  s_waitcnt lgkmcnt(0)')
+    if DYN:
+        e('  s_mov_b64 s[90:91], s[6:7]')                             # the program's first op
+        e('  s_add_u32 s92, s92, 63')
+        e('  s_lshr_b32 s92, s92, 6')                                 # jobs
     off, sreg, rem = 0, SNP, K
     for width in (16, 8, 4, 2, 1):
         while rem >= width:
@@ -874,6 +886,24 @@ def gen_padic_mfma(name: str) -> str:
     e('  s_branch .Lprog')
 
     e('.Lend:')
+    if DYN:
+        e('  s_mov_b64 exec, 1')
+        e('  v_mov_b32_e32 v2, 0')
+        e('  v_mov_b32_e32 v3, 1')
+        e('  global_atomic_add v4, v2, v3, s[94:95] sc0')
+        e('  s_waitcnt vmcnt(0)')
+        e('  s_mov_b64 exec, -1')
+        e('  v_readfirstlane_b32 s96, v4')
+        e('  s_add_u32 s96, s96, s93')                                # job = waves launched + draw
+        e('  s_cmp_ge_u32 s96, s92')
+        e('  s_cbranch_scc1 .Ljobs_done')
+        e('  s_lshl_b32 s96, s96, 8')
+        e(f'  v_and_b32_e32 v2, 63, v{V_TID}')
+        e('  v_lshlrev_b32_e32 v2, 2, v2')
+        e(f'  v_add_u32_e32 v{V_GOFF}, s96, v2')
+        e('  s_mov_b64 s[6:7], s[90:91]')
+        e('  s_branch .Lprog')
+        e('.Ljobs_done:')
     if PP:                                       # half 0 pays back half 1's extra barrier
         e('  s_cmp_eq_u32 s18, 0')
         e('  s_cbranch_scc0 .Lpp_end')
@@ -939,7 +969,8 @@ def gen_padic_mfma(name: str) -> str:
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
     e('')
-    o.extend(_descriptor(name, LDS_BYTES, NVGPR, 90 if STAMP else NSGPR, max_wg=512 if PP else 256).splitlines())
+    o.extend(_descriptor(name, LDS_BYTES, NVGPR, 98 if DYN else 90 if STAMP else NSGPR,
+                         max_wg=512 if PP else 256).splitlines())
     return "\n".join(o) + "\n"
 
 
