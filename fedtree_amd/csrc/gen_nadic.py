@@ -550,7 +550,10 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
         splits its lowest column, keeps hi in its next column and hands lo to the lane below as that
         lane's new top column (gen_montprog.py gen_quad's step; lane 0's lo is 0).  Window 2 takes -q1
         into its lowest column (lane 0) and its columns are signed (arithmetic split).  Rings of NTC
-        pairs per window: position k at step u in pair (u + k) mod NTC."""
+        pairs per window: position k at step u in pair (u + k) mod NTC.  The hand-off is one v_and_b32 with
+        DPP into a fixed pair per window whose high dword stays 0, the next step's first multiply-add into
+        that column takes the pair as its addend (no fresh column to clear), and q is masked and broadcast
+        by one v_and_b32 with DPP: 88 VALU instructions per step, 76 of them multiply-adds."""
         lab = '.Lprod_sq' if sq else '.Lprod_mul'
         NT = NTC
         assert NT % 2 == 0 and NT >= Q + 1
@@ -566,6 +569,8 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
             return f"v{tb + 2 * (k % NT) + 1}"
 
         tmp2 = f"v[{DF0}:{DF0 + 1}]"
+        HO = {TB1: DACC1, TB2: DACC2}            # hand-off pairs (the estimate registers of the classical form)
+        VMK = DBIAS                              # 2^27 - 1
 
         def reduce_split(tb, qreg, t, shr):
             for j in range(Q):
@@ -574,18 +579,18 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
                     e(f'  {shr} {t}, {B}, {T(tb, u_[0])}')
                 if j == 9:
                     e(f'  v_lshl_add_u64 {T(tb, u_[0] + 1)}, {t}, 0, {T(tb, u_[0] + 1)}')
-                if j == 12:
-                    e(f'  v_and_b32_e32 {Tlo(tb, u_[0])}, {hex(MASK)}, {Tlo(tb, u_[0])}')
-            e(f'  v_mov_b32_dpp {Tlo(tb, u_[0] + Q)}, {Tlo(tb, u_[0])} quad_perm:[1,2,3,0] {DPP}')
-            e(f'  v_mov_b32_e32 {Thi(tb, u_[0] + Q)}, 0')
+            e(f'  v_and_b32_dpp v{HO[tb]}, {Tlo(tb, u_[0])}, v{VMK} quad_perm:[1,2,3,0] {DPP}')
 
         def qstep(j, tb, qreg):
             if j == 3:
                 e(f'  v_mul_lo_u32 v{qreg}, {Tlo(tb, u_[0])}, s44')
-            if j == 6:
-                e(f'  v_and_b32_e32 v{qreg}, {hex(MASK)}, v{qreg}')
             if j == 9:
-                e(f'  v_mov_b32_dpp v{qreg}, v{qreg} quad_perm:[0,0,0,0] {DPP}')
+                e(f'  v_and_b32_dpp v{qreg}, v{qreg}, v{VMK} quad_perm:[0,0,0,0] {DPP}')
+
+        def top(tb, u, j):
+            """the addend of the multiply-add that first touches position u + j: the hand-off pair for the top
+            column (j = Q - 1), else the ring"""
+            return f"v[{HO[tb]}:{HO[tb] + 1}]" if j == Q - 1 else T(tb, u + j)
 
         u_ = [0]
 
@@ -600,7 +605,7 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
             a2 = bi if dbl else f"v{V_A2}"
             # window 1: + a_i X0, q1, + q1 N, split
             for j in range(Q):
-                e(f'  v_mad_u64_u32 {T(TB1, u + j)}, vcc, {ai}, {X0(j)}, {T(TB1, u + j)}')
+                e(f'  v_mad_u64_u32 {T(TB1, u + j)}, vcc, {ai}, {X0(j)}, {top(TB1, u, j)}')
                 qstep(j, TB1, V_Q)
                 if j == 11 and not last:
                     e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * RB_}')
@@ -610,9 +615,9 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
             # window 2: + 2 a_i X1 (SQR) / a_i X1 + b_i X0 (MUL), - q1 at position 0, q2, + q2 N, split
             for j in range(Q):
                 if sq:
-                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {a2}, {X1(j)}, {T(TB2, u + j)}')
+                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {a2}, {X1(j)}, {top(TB2, u, j)}')
                 else:
-                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {ai}, {X1(j)}, {T(TB2, u + j)}')
+                    e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {ai}, {X1(j)}, {top(TB2, u, j)}')
                     e(f'  v_mad_u64_u32 {T(TB2, u + j)}, vcc, {bi}, {X0(j)}, {T(TB2, u + j)}')
                 if j == 0:       # lane 0: += q1 (-1); the other lanes add 0
                     e(f'  v_mad_i64_i32 {T(TB2, u)}, vcc, v{V_Q}, v{V_L0N}, {T(TB2, u)}')
@@ -624,6 +629,9 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
         for k in range(NT):
             e(f'  v_mov_b64_e32 v[{TB1 + 2 * k}:{TB1 + 2 * k + 1}], 0')
             e(f'  v_mov_b64_e32 v[{TB2 + 2 * k}:{TB2 + 2 * k + 1}], 0')
+        e(f'  v_mov_b64_e32 v[{HO[TB1]}:{HO[TB1] + 1}], 0')
+        e(f'  v_mov_b64_e32 v[{HO[TB2]}:{HO[TB2] + 1}], 0')
+        e(f'  v_mov_b32_e32 v{VMK}, {hex(MASK)}')
         e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
         if not sq or dbl:
             e(f'  ds_read_b32 v{V_BI[0]}, v{V_LDSI} offset:{S * RB_}')
@@ -644,8 +652,8 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
 
         def normalise(tb, X):
             e(f'  v_mov_b64_e32 {tmp}, 0')
-            for k in range(Q):
-                e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(tb, TL + k)}')
+            for k in range(Q):                   # the top column is in the hand-off pair
+                e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(tb, TL + k) if k < Q - 1 else f"v[{HO[tb]}:{HO[tb] + 1}]"}')
                 e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
                 e(f'  v_ashrrev_i64 {tmp}, {B}, {tmp}')
             ripple_quad(X, signed=True)

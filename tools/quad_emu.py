@@ -236,6 +236,15 @@ class QuadEmu:
                 self.scc = int((self.sread(args[0]) & M32) != (self.sread(args[1]) & M32))
                 continue
             # ---- vector (per active lane) ----
+            if op == 'v_and_b32_dpp':                 # dst = dpp(src0) & src1
+                m = re.search(r'quad_perm:\[(\d),(\d),(\d),(\d)\]', ins)
+                perm = [int(m.group(i)) for i in range(1, 5)]
+                dst, src, msk = args[0], args[1], args[2].split()[0]
+                vals = [self.vread(ln, src) for ln in range(NL)]
+                for ln in self.active():
+                    q = ln & ~3
+                    self.vwrite(ln, dst, vals[q + perm[ln & 3]] & self.vread(ln, msk))
+                continue
             if op == 'v_mov_b32_dpp':
                 m = re.search(r'quad_perm:\[(\d),(\d),(\d),(\d)\]', ins)
                 perm = [int(m.group(i)) for i in range(1, 5)]
