@@ -47,7 +47,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
-PMC_FILE = "r03zb_pmc.json"
+PMC_FILE = "r04p_pmc.json"
 
 
 def parse():
@@ -812,6 +812,14 @@ def run(a, world):
         i8_peak = 1024 * 2.4e9 * (32 * 32 * 32 * 2) / 32
         secondary["p2048_add_hbm"] = {"algorithmic_GBps": round(na * 1536 / add_s / 1e9, 1),
                                       "pmc_GBps": pk.get("hbm_GBps"), "pmc_VALUBusy": pk.get("VALUBusy"),
+                                      # the same counters calibrated on the kernel's own access pattern (x = y:
+                                      # a known byte count), and the algorithmic bytes of the profiled launch
+                                      "pmc_GBps_calibrated": pk.get("calibration", {}).get("hbm_GBps"),
+                                      "pmc_calibration": pk.get("calibration"),
+                                      "pmc_launch_ms": pk.get("launch_ms"),
+                                      "pmc_algorithmic_GBps": (round(pk["algorithmic_bytes_per_launch"]
+                                                                     / (pk["launch_ms"] * 1e-3) / 1e9, 1)
+                                                               if pk.get("launch_ms") else None),
                                       "pmc_kernel": kname if pk else None,
                                       "pmc_source": f"profiles/{PMC_FILE}" if pk else None,
                                       "peak_GBps": 8000,

@@ -108,7 +108,7 @@ def pmc_round(tag, out):
     MI355X_MICROARCH.md HBM section) and the launch duration from the ops kernel
     trace (add, kway) or the bench trace (enc) for the achieved GB/s."""
     res = {}
-    for w in ("enc", "add", "kway", "pub"):
+    for w in ("enc", "add", "addsame", "kway", "pub"):
         per = {}
         for t in ("fetch", "write", "vb", "occ", "sq", "mf", "lds"):
             for f in glob.glob(f"gpurun_out/{tag}_pmc_{w}_{t}/**/*counter_collection.csv", recursive=True):
@@ -162,6 +162,20 @@ def pmc_round(tag, out):
                     k["hbm_GBps"] = round(k["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1)
                     k["hbm_frac_of_8TBps"] = round(k["hbm_bytes_per_launch"] / (ms * 1e-3) / 8e12, 4)
                 k["algorithmic_bytes_per_launch"] = rows * 512 * ins_of[w]
+        # counter calibration on this kernel's own access pattern (tools/prof_ops.py addsame: x = y, so the
+        # launch must read each of its `rows` rows once -- rows * 512 B -- and write as many): bytes per
+        # counted byte of FETCH_SIZE and of WRITE_SIZE, applied to the distinct-row launch
+        same = res.get("addsame", {}).get(kern, {})
+        k = res["add"].get(kern, {})
+        if same.get("FETCH_SIZE") and same.get("WRITE_SIZE") and k.get("FETCH_SIZE") and k.get("launch_ms"):
+            ff = rows * 512 / (same["FETCH_SIZE"] * 1024)
+            fw = rows * 512 / (same["WRITE_SIZE"] * 1024)
+            cb = (ff * k["FETCH_SIZE"] + fw * k["WRITE_SIZE"]) * 1024
+            k["calibration"] = {"source": "addsame (x = y): rows * 512 B read once and written once",
+                                "bytes_per_fetch_byte": round(ff, 3), "bytes_per_write_byte": round(fw, 3),
+                                "hbm_bytes_per_launch": round(cb),
+                                "hbm_GBps": round(cb / (k["launch_ms"] * 1e-3) / 1e9, 1),
+                                "vs_algorithmic": round(cb / k["algorithmic_bytes_per_launch"], 3)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
