@@ -501,7 +501,9 @@ def run(a, world):
                                    "note": "v_mfma_i32_32x32x32_i8: both Barrett products of every P-adic product"}
     # what the traffic is: SURVEY 8(d) algorithmic bytes (772 B per encrypt, half per prime launch) vs the
     # operand reads of the one-lane design (each window multiplication reads a 296-B table entry per lane)
-    lanes = 393216
+    # lanes per exponentiation launch of the timed path: fthe.hip enc_chunk_lanes() (2 x chunk_lanes())
+    lanes = int(os.environ.get("FTHE_ENC_CHUNK") or 2 * int(os.environ.get("FTHE_CHUNK") or 393216))
+    roof["lanes_per_expo_launch"] = lanes
     roof["algorithmic_bytes_per_launch"] = lanes * 772 // 2
     roof["window_operand_bytes_per_launch_model"] = int(lanes * (190 + 16 + 4) * 296)
     roof["traffic_note"] = ("HBM bytes are the per-lane window-table traffic (~180 window multiplications reading and "

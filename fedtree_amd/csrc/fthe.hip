@@ -174,6 +174,18 @@ size_t rowio_chunk_lanes() {
     return v;
 }
 
+// the key holder's large encrypt batches with device randomness (the direct-y path bench.py times) launch
+// twice chunk_lanes() per exponentiation: 786,432 lanes = six rounds of the P-adic kernel instead of three,
+// +1.5% encrypts/s (1.8% at 1,572,864; profiles/r04q_chunk_ab.jsonl); FTHE_ENC_CHUNK overrides
+size_t enc_chunk_lanes() {
+    static const size_t v = [] {
+        const char *e = getenv("FTHE_ENC_CHUNK");
+        size_t c = e ? (size_t)strtoull(e, nullptr, 10) : 2 * chunk_lanes();
+        return c < 1024 ? (size_t)1024 : c;
+    }();
+    return v;
+}
+
 // window width minimising table + multiplications for an e-bit exponent
 int best_window(size_t ebits) {
     int best = 1; double bc = 1e30;
@@ -1806,7 +1818,8 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     const bool split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2);
+    int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2,
+                        direct_y && !split && !quad ? enc_chunk_lanes() : 0);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     // Device-drawn randomness under CRT draws y_p, y_q uniform in [1,p), [1,q) and

@@ -11,8 +11,8 @@ sampled ciphertext is compared with the C oracle's encrypt(m, r) -- the full
 PowerMod formula, no CRT, no 1 + mn shortcut (oracle/paillier_oracle.c).
 
 Covered: the four-lane small-batch path (<= 16,384 ciphertexts), the two-stream
-split path (one chunk, <= 393,216), and the chunked large-batch path across the 393,216-lane
-chunk boundary.  Integer work: exact equality.
+split path (one chunk, <= 393,216), and the chunked large-batch path across its 786,432-lane
+launch boundary (enc_chunk_lanes(), twice the engine's chunk).  Integer work: exact equality.
 """
 import numpy as np
 import pytest
@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 
 SEED = 20261015
 CHUNK = 393216                  # chunk_lanes() of the engine (fthe.hip)
+ENC_CHUNK = 2 * CHUNK           # enc_chunk_lanes(): the large direct-y batches' launches
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +34,7 @@ def setup(coracle):
     pl = Paillier(dev).keygen(2048, seed=SEED)
     pw = (max(pl.p.bit_length(), pl.q.bit_length()) + 31) // 32
     ok = coracle.key(pyoracle.to_words(pl.p, pw), pyoracle.to_words(pl.q, pw))
-    g, h = logistic_gradients(CHUNK // 2 + 4096, SEED)
+    g, h = logistic_gradients(ENC_CHUNK // 2 + 4096, SEED)
     m = np.concatenate([encode_fixed(g), encode_fixed(h)])
     return dev, pl, ok, m
 
@@ -95,16 +96,18 @@ def test_split_path(setup):
 
 
 def test_large_batch_across_chunk_boundary(setup):
-    """The bench's call: device-resident m and c (fthe_encrypt_u64_dev), one full chunk
-    plus 4,096 more; 4,096 sampled ciphertexts on both sides of the boundary."""
+    """The bench's call: device-resident m and c (fthe_encrypt_u64_dev), one full launch
+    plus 4,096 more; 4,096 sampled ciphertexts on both sides of the boundary, 3,072 around the
+    engine's chunk_lanes() (inside the first launch)."""
     import torch
     dev, pl, ok, m = setup
-    cnt = CHUNK + 4096
+    cnt = ENC_CHUNK + 4096
     md = torch.from_numpy(m[:cnt].view(np.int64)).to("cuda:0")
     cd = torch.empty((cnt, 2 * pl.n_words), dtype=torch.int32, device="cuda:0")
     pl.encrypt_u64_dev(md, cd, seed=SEED + 3)
     dev.sync()
-    idx = np.concatenate([np.arange(0, 512), np.arange(CHUNK - 1536, CHUNK + 1536), np.arange(cnt - 512, cnt)])
+    idx = np.concatenate([np.arange(0, 512), np.arange(CHUNK - 1536, CHUNK + 1536),
+                          np.arange(ENC_CHUNK - 1536, ENC_CHUNK + 1536), np.arange(cnt - 512, cnt)])
     c = cd[torch.from_numpy(idx).to("cuda:0")].cpu().numpy().view(np.uint32)
     _check(pl, ok, m[idx], c, SEED + 3, idx)
     # and the whole batch decrypts (CRT decrypt, the same key)

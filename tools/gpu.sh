@@ -9,7 +9,7 @@
 #   bench:ARGS     python bench.py ARGS (comma-separated, e.g. bench:--steps,3)
 #   trace          the bench's timed region under rocprofv3 --kernel-trace --stats
 #   pmc:W          separate PMC passes (one counter group per run, never with tracing) over workload W:
-#                    enc  the bench's encrypt at 262,144 pairs (fthe_padic_m37 + s74 tails)
+#                    enc  the bench's encrypt at 393,216 pairs: one full 786,432-lane launch per prime (fthe_padic_m37 + s74 tails)
 #                    add  one device-resident P-2048 add of 1M distinct ciphertext pairs (fthe_addb_q152)
 #                    addsame  the same with x = y (each row read once for both operands: counter calibration)
 #                    kway three 8-party merges of 1,048,576 bins
@@ -32,7 +32,7 @@ pmc_pass() {  # workload tag counters...
   local w=$1 tag=$2; shift 2
   local cmd
   case $w in
-    enc)  cmd="python3 bench.py --pairs 262144 --steps 1 --warmup 0 --no-cpu --no-secondary";;
+    enc)  cmd="python3 bench.py --pairs 393216 --steps 1 --warmup 0 --no-cpu --no-secondary";;
     add)  cmd="python3 tools/prof_ops.py --n 1048576 --ops add";;
     addsame) cmd="python3 tools/prof_ops.py --n 1048576 --ops addsame";;
     kway) cmd="python3 tools/prof_ops.py --n 1048576 --ops kway";;
