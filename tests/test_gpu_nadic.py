@@ -149,6 +149,12 @@ def test_chunk_boundary_and_public_only_key(keys):
     assert launches == 2
     idx = np.r_[0:64, 98304 - 64:98304 + 64, cnt - 64:cnt]
     assert np.array_equal(cp[idx], pm.encrypt_u64(m[idx], r=raw[idx], public=True))
+    # and against the reference's formula PowerMod(g, m, n^2) PowerMod(r, n, n^2) (paillier.cpp:134-137), not
+    # only against the other kernel: the 256 sampled ciphertexts on both sides of the launch boundary
+    n2 = n * n
+    got = pyoracle.words_to_ints(cp[idx])
+    for j, i in enumerate(idx):
+        assert got[j] == (1 + int(m[i]) * n) * pow(rs[i], n, n2) % n2, int(i)
     assert np.array_equal(pa.decrypt_u64(cp), m)
 
 
