@@ -1455,6 +1455,10 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     if (nb && L % kNbPerWg) return FTHE_ERR_ARG;          // the kernel covers whole workgroups of the slots
     unsigned blocks = nb ? (unsigned)((live + kNbPerWg - 1) / kNbPerWg)
                          : (unsigned)((live * kVariants[vi].lanes + 255) / 256);
+    if (nb) {                     // persistent: at most one workgroup per CU, batches from its LDS counter
+        blocks = std::min(blocks, (unsigned)c->n_cu);
+        args.pad = blocks;
+    }
     if (dyn) {
         if (!c->d_jobctr) HIPOK(hipMalloc(&c->d_jobctr, 256 * sizeof(uint32_t)));
         blocks = std::min(blocks, 2u * (unsigned)c->n_cu);          // 249 VGPRs: two waves per SIMD

@@ -86,7 +86,8 @@ assert IMG_BYTES % 16 == 0 and WAVE_AREA % 16 == 0 and (QROW // 4) % 32 == 4
 
 
 def lds_bytes(waves=WAVES):
-    return IMG_BYTES + waves * WAVE_AREA
+    """the image, the wave areas and the workgroup's batch counter (one dword, 16-byte slot)"""
+    return IMG_BYTES + waves * WAVE_AREA + 16
 
 
 assert lds_bytes() <= 160 * 1024
@@ -114,6 +115,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     DBG = set(os.environ.get("FTHE_GEN_NADICB_DBG", "").split(","))
     DPP = "row_mask:0xf bank_mask:0xf"
     LDSB = lds_bytes(waves)
+    LDS_CNT = LDSB - 16                 # the workgroup's batch counter
     # ---- VGPRs ---------------------------------------------------------------------------------------------
     V_LANE = 0                        # lane (0..63) * 4 after the prologue (tid at entry)
     V_ROW, V_LDSI, V_LDSW, V_SH = 1, 2, 3, 4     # (g, k) slot code; A column base; lane k's row base; 2 k
@@ -157,9 +159,10 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     # s[0:1] kernarg, s2 wg id, s[4:5] slots, s[6:7] prog, s[8:9] ctx, s10 limb stride, s11 slot stride,
     # s[14:15] op / arg, s[16:17] address scratch, s18 trip counter, s19 SQR counter, lane masks s[20:21] quad
     # lane 3, s[22:23] lane 0, s[24:25] lane 1, s[26:27] lane 2, s[28:29] lanes 0-1, s30 = 256, s31 = 65536,
-    # s32 = 2^24, s33 = 0x80808080, s[34:35] saved exec, s36 ctx lo + N_OFF
+    # s32 = 2^24, s33 = 0x80808080, s[34:35] saved exec, s36 ctx lo + N_OFF, s[40:41] the program's first op,
+    # s42 workgroups launched, s43 batches of 16 ciphertexts, s44 scratch
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
-    NSGPR = 40
+    NSGPR = 46
 
     o = []
     e = o.append
@@ -200,13 +203,21 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'  ds_write_b128 v{V_LDSI}, v[{X0B}:{X0B + 3}]')
         if part:
             e('  s_mov_b64 exec, s[34:35]')
+    e(f'  v_cmp_eq_u32_e32 vcc, 0, v{V_LANE}')                            # thread 0: batch counter = 0
+    e('  s_and_saveexec_b64 s[34:35], vcc')
+    e(f'  v_mov_b32_e32 v{V_TMP}, {hex(LDS_CNT)}')
+    e(f'  v_mov_b32_e32 v{V_TMP + 1}, 0')
+    e(f'  ds_write_b32 v{V_TMP}, v{V_TMP + 1}')
+    e('  s_mov_b64 exec, s[34:35]')
+    e('  s_load_dwordx2 s[42:43], s[0:1], 0x20')                         # live ciphertexts, workgroups launched
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
+    e('  s_add_u32 s44, s42, 15')
+    e('  s_lshr_b32 s44, s44, 4')                                         # batches of 16 ciphertexts
+    e('  s_mov_b32 s42, s43')
+    e('  s_mov_b32 s43, s44')
+    e('  s_mov_b64 s[40:41], s[6:7]')
     # ---- per-lane constants ----------------------------------------------------------------------------------
-    # ROW = g*512 + k*128 = wg*(16 waves ciphertexts)*512 + tid*128
-    e(f'  s_mul_i32 s14, s2, {CT_PER_WAVE * waves * 512}')
-    e(f'  v_lshlrev_b32_e32 v{V_ROW}, 7, v{V_LANE}')
-    e(f'  v_add_u32_e32 v{V_ROW}, s14, v{V_ROW}')
     e(f'  v_lshrrev_b32_e32 v{V_TMP}, 6, v{V_LANE}')                    # wave
     e(f'  v_mul_u32_u24_e32 v{V_TMP}, {WAVE_AREA}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_TMP}, {IMG_BYTES}, v{V_TMP}')              # wave area base
@@ -245,10 +256,29 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_add_u32_e32 v{V_G}, v{V_G}, v{V_A2X}')                    # + the wave's area
     e(f'  v_add_u32_e32 v{V_B}, v{V_B}, v{V_A2X}')
     e(f'  v_lshlrev_b32_e32 v{V_SH}, 1, v{V_SH}')                      # 2 k
-    e(f'  v_lshlrev_b32_e32 v{V_LANE}, 2, v{V_LANE}')                  # lane * 4 (unused now; kept)
+    e(f'  v_lshlrev_b32_e32 v{V_LANE}, 7, v{V_LANE}')                  # lane * 128: ROW = g*512 + k*128
     e('  s_add_u32 s36, s8, ' + hex(N_OFF))
     e('  s_addc_u32 s37, s9, 0')
 
+    # ---- persistent waves: workgroup wg owns the batches wg, wg + nwg, ... of 16 ciphertexts; its waves draw
+    #      them from the LDS counter (a wave the SIMD's arbiter favours runs more of them, as fthe_addb_q152),
+    #      and run the whole program on each (the END op draws the next) ----------------------------------------
+    e('.Lnext_batch:')
+    e('  s_mov_b64 exec, 1')
+    e(f'  v_mov_b32_e32 v{V_TMP}, {hex(LDS_CNT)}')
+    e(f'  v_mov_b32_e32 v{V_TMP + 1}, 1')
+    e(f'  ds_add_rtn_u32 v{V_TMP}, v{V_TMP}, v{V_TMP + 1}')
+    e('  s_waitcnt lgkmcnt(0)')
+    e('  s_mov_b64 exec, -1')
+    e('  s_nop 1')
+    e(f'  v_readfirstlane_b32 s44, v{V_TMP}')
+    e('  s_mul_i32 s44, s44, s42')
+    e('  s_add_u32 s44, s44, s2')                                          # batch
+    e('  s_cmp_ge_u32 s44, s43')
+    e('  s_cbranch_scc1 .Lend')
+    e('  s_lshl_b32 s44, s44, 13')                                         # 16 ciphertexts x 512
+    e(f'  v_add_u32_e32 v{V_ROW}, s44, v{V_LANE}')
+    e('  s_mov_b64 s[6:7], s[40:41]')
     e('.Lprog:')
     e('  s_load_dwordx2 s[14:15], s[6:7], 0x0')
     e('  s_add_u32 s6, s6, 8')
@@ -257,7 +287,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     for code, lab in ((1, '.Lloadx'), (2, '.Lstorex'), (3, '.Lsqr'), (4, '.Lmul'), (20, '.Lcanon')):
         e(f'  s_cmp_eq_u32 s14, {code}')
         e(f'  s_cbranch_scc1 {lab}')
-    e('  s_branch .Lend')
+    e('  s_branch .Lnext_batch')
 
     # ---- slot access: limb j of this lane's quarter of digit d at slot limb d*S + k*Q + j ---------------
     def slot_addr():
@@ -421,11 +451,20 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     def emit_product(sq):
         lab = '.Lprod_sq' if sq else '.Lprod_mul'
 
+        # the retired column's low 27 bits go to the lane below by one v_and_b32 with DPP into a fixed pair per
+        # window whose high dword stays 0 (lane 3 masked to 0), and the next step's multiply-add into that
+        # column takes the pair as its addend: no fresh ring column to clear (as fthe_addb_q152); lane 0's
+        # product limb is stored unmasked and masked when to_dwords reads it back
+        HO = {T1B: 146, T2B: 148}            # in the Barretts' DQ registers (dead in the product pass)
+        VMK = 150
+
+        def top(tb, u, j):
+            return pair(HO[tb]) if j == Q - 1 else T(tb, u + j)
+
         def split(tb, u, t):
             """the lowest column: hi -> the lane's next column, lo (lane 0: the product limb) kept in place"""
             e(f'  v_lshrrev_b64 {t}, {B}, {T(tb, u)}')
             e(f'  v_lshl_add_u64 {T(tb, u + 1)}, {t}, 0, {T(tb, u + 1)}')
-            e(f'  v_and_b32_e32 {Tlo(tb, u)}, {hex(MASK)}, {Tlo(tb, u)}')
 
         def retire(tb, u, row):
             """lane 0's lo is the product limb: written to A-column row `row` (its multiplier is consumed)"""
@@ -433,14 +472,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  ds_write_b32 v{V_LDSI}, {Tlo(tb, u)} offset:{row * RB}')
             e('  s_mov_b64 exec, -1')
 
-        def zero_lane0(tb, u):
-            e(f'  v_cndmask_b32_e64 {Tlo(tb, u)}, {Tlo(tb, u)}, 0, s[22:23]')
-
         def handoff(tb, u):
-            """lo to the lane below as its new top column (lane 3 gets lane 0's zero); >= 5 wait states after
-            the EXEC writes of retire() and >= 2 after zero_lane0() (the schedule below keeps MADs between)"""
-            e(f'  v_mov_b32_dpp {Tlo(tb, u + Q)}, {Tlo(tb, u)} quad_perm:[1,2,3,0] {DPP}')
-            e(f'  v_mov_b32_e32 {Thi(tb, u + Q)}, 0')
+            """lo & (2^27 - 1) to the lane below (lane 3: 0) in the window's pair; >= 5 wait states after the
+            EXEC writes of retire() (the schedule below keeps MADs between), after the step's last read of
+            the pair"""
+            e(f'  v_and_b32_dpp v{HO[tb]}, {Tlo(tb, u)}, v{VMK} quad_perm:[1,2,3,0] {DPP}')
 
         def step(u, i, last):
             ai, nai = f"v{V_AI[u % 2]}", f"v{V_AI[(u + 1) % 2]}"
@@ -448,7 +484,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             if sq:
                 e(f'  v_lshlrev_b32_e32 v{V_A2X}, 1, {ai}')
             for j in range(Q):
-                e(f'  v_mad_u64_u32 {T(T1B, u + j)}, vcc, {ai}, {X0(j)}, {T(T1B, u + j)}')
+                e(f'  v_mad_u64_u32 {T(T1B, u + j)}, vcc, {ai}, {X0(j)}, {top(T1B, u, j)}')
                 if j == 2:
                     split(T1B, u, pair(V_TMP))
                 if j == 6 and not last:
@@ -457,13 +493,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                         e(f'  ds_read_b32 {nbi}, v{V_LDSI} offset:{(S + i + 1) * RB}')
                 if j == 8:
                     retire(T1B, u, i)
-                if j == 12:
-                    zero_lane0(T1B, u)
             for j in range(Q):
                 if sq:
-                    e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, v{V_A2X}, {X1(j)}, {T(T2B, u + j)}')
+                    e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, v{V_A2X}, {X1(j)}, {top(T2B, u, j)}')
                 else:
-                    e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, {ai}, {X1(j)}, {T(T2B, u + j)}')
+                    e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, {ai}, {X1(j)}, {top(T2B, u, j)}')
                     e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, {bi}, {X0(j)}, {T(T2B, u + j)}')
                 if j == 0:
                     handoff(T1B, u)
@@ -471,10 +505,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                     split(T2B, u, pair(V_TMP))
                 if j == 8:
                     retire(T2B, u, S + i)
-                if j == 12:
-                    zero_lane0(T2B, u)
-                if j == 16:
-                    handoff(T2B, u)
+            handoff(T2B, u)
             if not last:
                 e('  s_waitcnt lgkmcnt(2)')                      # the prefetch reads (issued before the writes)
 
@@ -482,6 +513,10 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         for k in range(NT):
             e(f'  v_mov_b64_e32 {T(T1B, k)}, 0')
             e(f'  v_mov_b64_e32 {T(T2B, k)}, 0')
+        e(f'  v_mov_b64_e32 {pair(HO[T1B])}, 0')
+        e(f'  v_mov_b64_e32 {pair(HO[T2B])}, 0')
+        e(f'  v_mov_b32_e32 v{VMK}, {hex(MASK)}')
+        e(f'  v_cndmask_b32_e64 v{VMK}, v{VMK}, 0, s[20:21]')
         e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
         if not sq:
             e(f'  ds_read_b32 v{V_BI[0]}, v{V_LDSI} offset:{S * RB}')
@@ -509,8 +544,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         # ---- normalise both windows: positions TL .. TL + 18 -> 19 limbs (z limbs 76 + 19 k + j) --------
         for tb, tag in ((T1B, 'n1'), (T2B, 'n2')):
             e(f'  v_mov_b64_e32 {tmp}, 0')
-            for k in range(Q):
-                e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(tb, TL + k)}')
+            for k in range(Q):                   # the top column is in the window's hand-off pair
+                e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(tb, TL + k) if k < Q - 1 else pair(HO[tb])}')
                 e(f'  v_and_b32_e32 {Tlo(tb, TL + k)}, {hex(MASK)}, v{V_TMP}')
                 e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
             ripple_quad(f'{lab}_{tag}', lambda k, tb=tb: Tlo(tb, TL + k), Q)
@@ -537,6 +572,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  ds_read_b32 v{ZL + k}, v{V_TMP} offset:{(row0 + k) * RB}')
         e('  s_mov_b64 exec, -1')
         e('  s_waitcnt lgkmcnt(0)')
+        for k in range(2 * Q):                         # product limbs were stored with their carries above bit 27
+            e(f'  v_and_b32_e32 v{ZL + k}, {hex(MASK)}, v{ZL + k}')
         U = lambda i: f"v{zb + i}"
         t1, bo = f"v{V_AI[0]}", f"v{V_AI[1]}"
         for i in range(32):

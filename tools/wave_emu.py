@@ -256,6 +256,10 @@ class Wave:
             self.scc = int(self.exec != 0)
         elif op == 's_mul_i32':
             self.sset(a[0], g(a[1]) * g(a[2]))
+        elif op == 's_lshr_b32':
+            r = (g(a[1]) & M32) >> (g(a[2]) & 31)
+            self.sset(a[0], r)
+            self.scc = int(r != 0)
         elif op == 's_lshl_b32':
             r = (g(a[1]) << g(a[2])) & M32
             self.sset(a[0], r)
@@ -650,7 +654,7 @@ def selftest(ntests=16, count0=None):
     print("wave_emu selftest OK")
 
 
-def nadicb_selftest(seed=1, bits=2048, count=16, waves=1):
+def nadicb_selftest(seed=1, bits=2048, count=16, waves=1, batches=1):
     """one wave of fthe_nadic_b76 (a workgroup generated with one wave: 16 ciphertexts): LOADX r; CANON;
     STOREX T; SQR 1; STOREX U (digits up to 3n); SQR 1; MUL U; MUL T; CANON; STOREX OUT -> r^7 mod n^2 as
     canonical digits, against Python integers (r: 0, 1, n - 1, random)"""
@@ -662,8 +666,9 @@ def nadicb_selftest(seed=1, bits=2048, count=16, waves=1):
     rng = random.Random(seed)
     n = nm.rand_n(rng, bits)
     N2 = n * n
-    S, L, B = 152, 16 * waves, 27
-    count = max(count, L) if waves > 1 else count
+    S, L, B = 152, 16 * waves * batches, 27       # batches > 1: the waves draw several (the emulator runs the
+    #                                              first wave to its end, so wave 0 takes them all)
+    count = max(count, L) if waves > 1 or batches > 1 else count
     asm = gb.gen_nadicb('fthe_nadic_b76', waves=waves)
     nv = int(re.search(r'\.amdhsa_next_free_vgpr (\d+)', asm).group(1))
     lds_bytes = int(re.search(r'\.amdhsa_group_segment_fixed_size (\d+)', asm).group(1))
@@ -687,7 +692,8 @@ def nadicb_selftest(seed=1, bits=2048, count=16, waves=1):
     mem.alloc(b''.join(w.to_bytes(4, 'little') for w in prog), PB)
     mem.alloc(bytes(ctx), CB)
     karg = SB.to_bytes(8, 'little') + PB.to_bytes(8, 'little') + CB.to_bytes(8, 'little') + \
-        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + bytes(4 + 128)
+        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + \
+        (1).to_bytes(4, 'little') + bytes(128)
     mem.alloc(karg, KA)
     steps = run_workgroup(asm, lds_bytes, waves, mem, KA, 0, nv)
     bad = 0
@@ -745,7 +751,8 @@ def m37_selftest(seed=1, ab=None, bits=1024):
     mem.alloc(b''.join(w.to_bytes(4, 'little') for w in prog), PB)
     mem.alloc(bytes(ctx), CB)
     karg = SB.to_bytes(8, 'little') + PB.to_bytes(8, 'little') + CB.to_bytes(8, 'little') + \
-        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + bytes(4 + 128)
+        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + \
+        (1).to_bytes(4, 'little') + bytes(128)
     mem.alloc(karg, KA)
     steps = run_workgroup(asm, lds_bytes, 4, mem, KA, 0, nv, finish=(0,))
     bad = 0
