@@ -732,19 +732,18 @@ static bool nadic_ok(const fthe_key *k) {
     return !getenv("FTHE_NO_NADIC") && k->sn2.S == 152 && k->sn2.B == 27 && k->sn2.lanes == 4 &&
            b >= 2042 && b <= 2050;
 }
-// its Montgomery form (fthe_nadic_m76, the default) needs only an odd n with 8 n < R = 2^2052 and n^2 on the
+// its Montgomery form (fthe_nadic_m76, the default below 2041 bits) needs only an odd n with 8 n < R = 2^2052 and n^2 on the
 // s152 slots: every n of 1033..2048 bits (no quotient estimate, so no lower bound of its own)
 static bool nadic_mont_ok(const fthe_key *k) {
     return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_CLASSICAL") && k->sn2.S == 152 && k->sn2.B == 27 &&
            k->sn2.lanes == 4 && mpz_sizeinbase(k->n, 2) <= 2048;
 }
-// its matrix-core Barrett form (fthe_nadic_b76; opt-in, FTHE_NADIC_BARRETT=1 at key set-up): n of 2041..2048 bits,
-// n^2 on the s152 slots.  Bit-exact, but measured slower than the Montgomery form (477k vs 519k public-key
-// encrypts/s, tools/nadicb_ab.py): its VALU products run at the issue rate, its reductions at about half of it
-// (DESIGN.md 8), so fthe_nadic_m76 stays the default
+// its matrix-core Barrett form (fthe_nadic_b76, the default for n of 2041..2048 bits, n^2 on the s152 slots;
+// FTHE_NADIC_MONT=1 at key set-up keeps the Montgomery form): persistent waves and the fixed-pair hand-off made
+// it 2.6% faster than fthe_nadic_m76 (555k vs 541k public-key encrypts/s in one process, tools/nadicb_ab.py,
+// profiles/r04u_nadicb_3op_ab.json)
 static bool nadicb_ok(const fthe_key *k) {
-    const char *b = getenv("FTHE_NADIC_BARRETT");
-    return b && *b == '1' && !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_MONT") && !getenv("FTHE_NADIC_CLASSICAL") &&
+    return !getenv("FTHE_NO_NADIC") && !getenv("FTHE_NADIC_MONT") && !getenv("FTHE_NADIC_CLASSICAL") &&
            k->sn2.S == 152 && k->sn2.B == 27 && k->sn2.lanes == 4 && nadicb::n_ok(k->n);
 }
 static int upload_nadic(DevMod &d, const mpz_t n, const mpz_t n2, Shape slots, bool classical = true) {

@@ -1,7 +1,7 @@
 """The n-adic four-lane kernels behind the public-key encrypt at Paillier-2048 (Party::encrypt_histogram,
-party.h:118-142 -> paillier.cpp:122-139): the Montgomery form fthe_nadic_m76 (the default, n of
-1033..2048 bits), the matrix-core Barrett form fthe_nadic_b76 (gen_nadicb.py, n of 2041..2048 bits, opt-in with
-FTHE_NADIC_BARRETT=1) and the classical fthe_nadic_q76 (FTHE_NADIC_CLASSICAL=1): the
+party.h:118-142 -> paillier.cpp:122-139): the matrix-core Barrett form fthe_nadic_b76 (gen_nadicb.py,
+the default for n of 2041..2048 bits), the Montgomery form fthe_nadic_m76 (n of 1033..2040 bits; FTHE_NADIC_MONT=1
+selects it everywhere) and the classical fthe_nadic_q76 (FTHE_NADIC_CLASSICAL=1): the
 same ciphertexts as each other and as the Montgomery s152 program they replace (FTHE_NO_NADIC=1), every one of
 them equal to the C oracle's (1 + m n) r^n mod n^2 on the sizes tested, for injected r at the extremes and random
 r, u64 and word plaintexts, across a chunk boundary, on a public-only key too, and their launches really run.
@@ -65,14 +65,14 @@ def _variant_launches(dev, fn, variant):
 
 
 def test_three_forms_same_ciphertexts(keys):
-    """fthe_nadic_m76 (Montgomery, the default), fthe_nadic_b76 (FTHE_NADIC_BARRETT=1; tools/nadicb_model.py) and
-    fthe_nadic_q76 (FTHE_NADIC_CLASSICAL=1): identical ciphertexts for injected r at the
+    """fthe_nadic_b76 (matrix-core Barrett, the default at 2048 bits; tools/nadicb_model.py), fthe_nadic_m76
+    (FTHE_NADIC_MONT=1) and fthe_nadic_q76 (FTHE_NADIC_CLASSICAL=1): identical ciphertexts for injected r at the
     extremes (r >= n included) and random, plaintexts up to 2^64 - 1, across a chunk boundary; each form's
     launches are its own kernel; 64 of them against the formula (every one against the oracle below)."""
     dev, pa, pm = keys
     from fedtree_amd.paillier import Paillier
     forms = {}
-    for env, variant in (("FTHE_NADIC_BARRETT", 2276), ("FTHE_NADIC_CLASSICAL", 2076)):
+    for env, variant in (("FTHE_NADIC_MONT", 2176), ("FTHE_NADIC_CLASSICAL", 2076)):
         os.environ[env] = "1"
         try:
             forms[variant] = Paillier.from_primes(pa.p, pa.q, dev)
@@ -86,7 +86,7 @@ def test_three_forms_same_ciphertexts(keys):
     m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)
     m[:3] = [0, 2**64 - 1, 1]
     rw = pyoracle.ints_to_words(rs, pa.n_words)
-    cb, lb = _variant_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True), 2176)
+    cb, lb = _variant_launches(dev, lambda: pa.encrypt_u64(m, r=rw, public=True), 2276)
     assert lb >= 2
     for variant, pl in forms.items():
         cv, lv = _variant_launches(dev, lambda: pl.encrypt_u64(m, r=rw, public=True), variant)
@@ -177,15 +177,15 @@ def _key_of_bits(rng, nbits):
             return p, q, n
 
 
-# which kernel a party's key of n bits runs: the Montgomery form for n of 1033..2048 bits (n^2 on the s152 slots; no
-# quotient estimate, so no lower bound of its own; with FTHE_NADIC_BARRETT=1 the matrix-core Barrett form takes
-# 2041..2048), below 1033 bits n^2 takes the s74 slots and neither n-adic form (1032: the Montgomery s74 program,
-# 1009..1030: the P-adic one)
-@pytest.mark.parametrize("nbits,variant,barrett", [(2048, 2176, False), (2048, 2276, True), (2045, 2276, True),
-                                                   (2042, 2176, False), (2041, 2276, True), (2040, 2176, True),
-                                                   (2030, 2176, False), (1536, 2176, False), (1033, 2176, False),
-                                                   (1032, None, False)])
-def test_modulus_range_edges(nbits, variant, barrett):
+# which kernel a party's key of n bits runs: the matrix-core Barrett form for n of 2041..2048 bits, the Montgomery
+# form for 1033..2040 (n^2 on the s152 slots; no quotient estimate, so no lower bound of its own; FTHE_NADIC_MONT=1
+# takes 2041..2048 too), below 1033 bits n^2 takes the s74 slots and neither n-adic form (1032: the Montgomery s74
+# program, 1009..1030: the P-adic one)
+@pytest.mark.parametrize("nbits,variant,mont", [(2048, 2276, False), (2048, 2176, True), (2045, 2276, False),
+                                                (2042, 2176, True), (2041, 2276, False), (2040, 2176, False),
+                                                (2030, 2176, False), (1536, 2176, False), (1033, 2176, False),
+                                                (1032, None, False)])
+def test_modulus_range_edges(nbits, variant, mont):
     """every ciphertext of a party's public-key encrypt (600 per size, injected r incl. 1 and n - 1) equals the
     C oracle's full formula PowerMod(g, m, n^2) PowerMod(r, n, n^2) (paillier.cpp:134-137), on the kernel the
     size selects; all decrypt back"""
@@ -193,12 +193,12 @@ def test_modulus_range_edges(nbits, variant, barrett):
     dev = Device(0)
     rng = np.random.default_rng(nbits)
     p, q, n = _key_of_bits(rng, nbits)
-    if barrett:
-        os.environ["FTHE_NADIC_BARRETT"] = "1"
+    if mont:
+        os.environ["FTHE_NADIC_MONT"] = "1"
     try:
         pl = Paillier.from_public(n, dev)
     finally:
-        os.environ.pop("FTHE_NADIC_BARRETT", None)
+        os.environ.pop("FTHE_NADIC_MONT", None)
     cnt = 600
     rs = [1, n - 1] + [int.from_bytes(rng.bytes(260), "little") % (n - 1) + 1 for _ in range(cnt - 2)]
     m = rng.integers(0, 2**64 - 1, cnt, dtype=np.uint64)

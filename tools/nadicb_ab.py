@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the Paillier-2048 public-key encrypt: the matrix-core Barrett n-adic kernel fthe_nadic_b76
-(FTHE_NADIC_BARRETT=1 at key set-up) vs the Montgomery form fthe_nadic_m76 (the default), same primes and plaintexts,
+(the default at 2041..2048 bits) vs the Montgomery form fthe_nadic_m76 (FTHE_NADIC_MONT=1 at key set-up), same primes and plaintexts,
 device-resident, variants round-robin; bit-identical outputs for injected r (and against the classical form and
 the Montgomery s152 program).  Prints one JSON line.  python tools/nadicb_ab.py [ciphertexts] [reps]"""
 import json
@@ -25,8 +25,8 @@ def key_with(env, pa, dev):
 def main():
     dev = Device(0)
     lib = dev.lib
-    pm = Paillier(dev).keygen(2048, seed=7)
-    pa = key_with("FTHE_NADIC_BARRETT", pm, dev)
+    pa = Paillier(dev).keygen(2048, seed=7)
+    pm = key_with("FTHE_NADIC_MONT", pa, dev)
     cnt = int(sys.argv[1]) if len(sys.argv) > 1 else 393216
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     m = torch.arange(cnt, dtype=torch.int64, device="cuda:0")

@@ -33,7 +33,6 @@ def from_limbs(row):
 def main():
     cnt = int(sys.argv[1]) if len(sys.argv) > 1 else 1536
     dev = Device(0)
-    os.environ["FTHE_NADIC_BARRETT"] = "1"
     pl = Paillier(dev).keygen(2048, seed=7)
     n = pl.modulus
     key = nm.Key(n)
