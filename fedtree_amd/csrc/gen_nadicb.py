@@ -75,11 +75,11 @@ IMG_BYTES = CORR2_OFF + TILES2 * 64
 N_OFF = IMG_BYTES                                     # n limbs (76 x u32) in ctx, not copied to LDS
 CTX_BYTES = N_OFF + 4 * S
 QROW = 400                       # q / r staging row: 80 dwords used; 100 dwords == 4 mod 32 (4-way stores)
-GROW = 304                       # group staging row (one chunk: <= 32 int64 groups + pad; 16-byte aligned rows
-                                 # for the normalisation's ds_read_b128 of two groups)
-QST_OFF = 0                      # staging areas inside the wave area (the A column is dead in the Barretts)
-GST_OFF = 16 * QROW
-WAVE_AREA = max(ROWS * RB, GST_OFF + 16 * GROW)
+GROW = 560                       # group staging row: a product's 68 int64 groups (every chunk at once) + pad;
+                                 # 16-byte aligned rows for the normalisation's ds_read_b128 of two groups
+QST_OFF = 0                      # staging areas inside the wave area (the A column is dead in the Barretts); the
+GST_OFF = 0                      # groups overlap the q staging, which the B operands have left before the MFMAs
+WAVE_AREA = max(ROWS * RB, QST_OFF + 16 * QROW, GST_OFF + 16 * GROW)
 M_A = (0, 1, 2, 3, 12, 13, 14, 15)
 M_B = (4, 5, 6, 7, 8, 9, 10, 11)
 assert IMG_BYTES % 16 == 0 and WAVE_AREA % 16 == 0 and (QROW // 4) % 32 == 4
@@ -111,7 +111,8 @@ def layout_header():
 
 def gen_nadicb(name: str, waves: int = WAVES) -> str:
     # timing-only switches (wrong results; fedtree_amd/build.py never lets FTHE_GEN_* reach the in-tree library):
-    # noprod (no VALU product steps), nobarrett (no reductions), nomfma (no MFMAs), noconv (no z -> dword moves)
+    # noprod (no VALU product steps), nobarrett (no reductions), nomfma (no MFMAs), noconv (no z -> dword moves),
+    # nonorm (no group normalisation)
     DBG = set(os.environ.get("FTHE_GEN_NADICB_DBG", "").split(","))
     DPP = "row_mask:0xf bank_mask:0xf"
     LDSB = lds_bytes(waves)
@@ -229,7 +230,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_add_u32_e32 v{V_QW}, v{V_QW}, v{V_TMP}')                   # staging row of c (QST_OFF = 0)
     e(f'  v_mul_u32_u24_e32 v{V_GR}, {GROW}, v{V_TMP + 1}')
     e(f'  v_add_u32_e32 v{V_GR}, v{V_GR}, v{V_TMP}')
-    e(f'  v_add_u32_e32 v{V_GR}, {GST_OFF}, v{V_GR}')                 # group row of c (norm reads)
+    e(f'  v_add_u32_e32 v{V_GR}, {GST_OFF}, v{V_GR}')                 # group row of c
+    e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_LANE}')                        # k
+    e(f'  v_lshl_add_u32 v{V_GR}, v{V_SH}, 8, v{V_GR}')               # + 256 k: quad lane k's chunk (norm reads)
     e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_LANE}')                        # k (quad lane)
     e(f'  v_mul_u32_u24_e32 v{V_LDSW}, {Q * RB}, v{V_SH}')
     e(f'  v_add_u32_e32 v{V_LDSW}, v{V_LDSW}, v{V_LDSI}')              # area + 4 c + 19 k RB
@@ -659,43 +662,96 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                     e('  s_nop 7')
                     e('  s_nop 7')
                     e('  s_nop 3')
-                    fold_tile(ACC[(n - 1) % 2], 4 * (tiles[n - 1] - t0))
+                    fold_tile(ACC[(n - 1) % 2], 4 * tiles[n - 1])              # group 4 t (every chunk staged)
                     q.append(('w', n - 1))
                     if n + 1 < len(tiles):
                         read_corr(n + 1, tiles[n + 1])
             e('  s_nop 7')
             e('  s_nop 7')
             e('  s_nop 7')
-            fold_tile(ACC[(len(tiles) - 1) % 2], 4 * (tiles[-1] - t0))
-            e('  s_waitcnt lgkmcnt(0)')
-            if j:
-                e('  s_nop 1')
-                e(f'  v_mov_b32_dpp v{V_TMP}, v{CR} quad_perm:[0,0,1,2] {DPP}')
-            e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
-            ng = 4 * len(tiles)
-            cv = f"v{V_TMP}" if j else f"v{CR}"
-            # two groups per ds_read_b128, two buffers: the read of groups g + 2, g + 3 is in flight while
-            # g, g + 1 are normalised (LDS returns in order: lgkmcnt(1) waits for the older read only)
-            def rd(g):
-                e(f'  ds_read_b128 {quad4(GB + 4 * ((g // 2) % 2))}, v{V_GR} offset:{8 * g}')
-            rd(0)
-            if ng > 2:
-                rd(2)
-            for g0 in range(0, ng, 2):
-                e(f'  s_waitcnt lgkmcnt({1 if g0 + 2 < ng else 0})')
-                for g in (g0, g0 + 1):
-                    src = pair(GB + 4 * ((g0 // 2) % 2) + 2 * (g - g0))
-                    if g % 2 == 0:
-                        e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {src}')
-                        cv = f"v{DQ + g + 1}"
-                    else:
-                        e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {src}')
-                        e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
-                        cv = f"v{FV + 1}"
-                if g0 + 4 < ng:
-                    rd(g0 + 4)
-            e(f'  v_mov_b32_e32 v{CR}, {cv}')
-            e('  s_mov_b64 exec, -1')
+            fold_tile(ACC[(len(tiles) - 1) % 2], 4 * tiles[-1])
+        e('  s_waitcnt lgkmcnt(0)')
+        if "nonorm" not in DBG:
+            normalise_chunks()
+
+    def normalise_chunks():
+        """Every chunk at once: quad lane k normalises chunk k's groups (k = 0, 1: 32 groups, k = 2: 4; lane 3 has
+        none) with carry-in 0 -- one chain instead of three after each other -- and then the chunks' carries are
+        delivered: lane k + 1 adds lane k's carry-out to its lowest dword; the signed overflow of that add (rare:
+        |carry| < 2^18 against a uniform dword) ripples through the lane's dwords on a slow path and changes its
+        carry-out, which is delivered the same way until no lane receives one.  CR: every lane's final carry."""
+        sizes = [4 * len(ch) for ch in CHUNKS]
+        assert sizes[:2] == [32, 32] and sizes[2] == 4 and len(sizes) == 3
+        L012, L01 = "s[34:35]", "s[28:29]"
+        e('  s_mov_b32 s34, 0x77777777')
+        e('  s_mov_b32 s35, 0x77777777')
+        e(f'  s_mov_b64 exec, {L012}')
+        e(f'  v_mov_b32_e32 v{CR}, 0')
+        cv = f"v{CR}"
+
+        # two groups per ds_read_b128, two buffers: the read of groups g + 2, g + 3 is in flight while
+        # g, g + 1 are normalised (LDS returns in order: lgkmcnt(1) waits for the older read only)
+        def rd(g):
+            e(f'  ds_read_b128 {quad4(GB + 4 * ((g // 2) % 2))}, v{V_GR} offset:{8 * g}')
+        ng = 32
+        rd(0)
+        rd(2)
+        for g0 in range(0, ng, 2):
+            if g0 == sizes[2]:                           # lane 2's chunk ends: its carry stays in FV + 1
+                e(f'  s_mov_b64 exec, {L01}')
+            e(f'  s_waitcnt lgkmcnt({1 if g0 + 2 < ng else 0})')
+            for g in (g0, g0 + 1):
+                src = pair(GB + 4 * ((g0 // 2) % 2) + 2 * (g - g0))
+                if g % 2 == 0:
+                    e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {src}')
+                    cv = f"v{DQ + g + 1}"
+                else:
+                    e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {src}')
+                    e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
+                    cv = f"v{FV + 1}"
+            if g0 + 4 < ng:
+                rd(g0 + 4)
+        assert cv == f"v{FV + 1}"
+        e(f'  s_mov_b64 exec, {L012}')
+        e(f'  v_mov_b32_e32 v{CR}, {cv}')                 # carry-outs with carry-in 0
+        e('  s_mov_b64 exec, -1')
+        # delivery: DL = the carries (or their changes) still to deliver, lane k -> lane k + 1 (k = 0, 1)
+        DL, X, TP = GB, CR + 1, V_TMP
+        lab = f'.Lcd{len(o)}'
+        e(f'  v_mov_b32_e32 v{DL}, v{CR}')
+        e(f'{lab}_loop:')
+        e('  s_nop 4')                                    # EXEC / VALU writes -> DPP
+        e(f'  v_mov_b32_dpp v{X}, v{DL} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 v{X}, v{X}, 0, s[22:23]')     # lane 0 receives none
+        e(f'  v_cndmask_b32_e64 v{X}, v{X}, 0, s[20:21]')     # lane 3 has no chunk
+        e(f'  v_mov_b32_e32 v{TP}, v{DQ}')
+        e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+        e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{X}, 1, {pair(TP)}')   # lowest dword + carry (signed)
+        e(f'  v_mov_b32_e32 v{DQ}, v{TP}')
+        e(f'  v_mov_b32_e32 v{DL}, 0')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{TP + 1}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        # slow path, the lanes whose add overflowed: the signed overflow P ripples through dwords 1.. (lane 2:
+        # 1..3, then it is lane 2's carry change); lane 1's final P changes its carry, delivered next round
+        e('  s_and_saveexec_b64 s[34:35], vcc')
+        P = X
+        e(f'  v_mov_b32_e32 v{P}, v{TP + 1}')
+        for i in range(1, 32):
+            if i == sizes[2]:
+                e(f'  v_add_u32_e32 v{TP}, v{P}, v{CR}')
+                e(f'  v_cndmask_b32_e64 v{CR}, v{CR}, v{TP}, s[26:27]')   # lane 2: carry += P
+                e(f'  v_cndmask_b32_e64 v{P}, v{P}, 0, s[26:27]')         # and nothing more to ripple
+            e(f'  v_mov_b32_e32 v{TP}, v{DQ + i}')
+            e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+            e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{P}, 1, {pair(TP)}')
+            e(f'  v_mov_b32_e32 v{DQ + i}, v{TP}')
+            e(f'  v_mov_b32_e32 v{P}, v{TP + 1}')
+        e(f'  v_add_u32_e32 v{CR}, v{P}, v{CR}')          # lane 1: carry += P (lane 2: P = 0 here)
+        e(f'  v_mov_b32_e32 v{DL}, v{P}')
+        e('  s_mov_b64 exec, s[34:35]')
+        e(f'  s_branch {lab}_loop')
+        e(f'{lab}_done:')
 
     def stage_q1(zb):
         """q1 = z dwords 63..128 (XORed 0x80808080) -> staging positions 0..65, zero 66..79; B operands.
