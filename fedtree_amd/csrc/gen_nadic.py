@@ -632,6 +632,7 @@ def gen_nadic(S: int, B: int, name: str, mont: bool = False) -> str:
         e(f'  v_mov_b64_e32 v[{HO[TB1]}:{HO[TB1] + 1}], 0')
         e(f'  v_mov_b64_e32 v[{HO[TB2]}:{HO[TB2] + 1}], 0')
         e(f'  v_mov_b32_e32 v{VMK}, {hex(MASK)}')
+
         e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
         if not sq or dbl:
             e(f'  ds_read_b32 v{V_BI[0]}, v{V_LDSI} offset:{S * RB_}')

@@ -484,8 +484,6 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         def step(u, i, last):
             ai, nai = f"v{V_AI[u % 2]}", f"v{V_AI[(u + 1) % 2]}"
             bi, nbi = f"v{V_BI[u % 2]}", f"v{V_BI[(u + 1) % 2]}"
-            if sq:
-                e(f'  v_lshlrev_b32_e32 v{V_A2X}, 1, {ai}')
             for j in range(Q):
                 e(f'  v_mad_u64_u32 {T(T1B, u + j)}, vcc, {ai}, {X0(j)}, {top(T1B, u, j)}')
                 if j == 2:
@@ -497,8 +495,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 if j == 8:
                     retire(T1B, u, i)
             for j in range(Q):
-                if sq:
-                    e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, v{V_A2X}, {X1(j)}, {top(T2B, u, j)}')
+                if sq:                               # x0_i (2 x1): X1 doubled once per squaring
+                    e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, {ai}, {X1(j)}, {top(T2B, u, j)}')
                 else:
                     e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, {ai}, {X1(j)}, {top(T2B, u, j)}')
                     e(f'  v_mad_u64_u32 {T(T2B, u + j)}, vcc, {bi}, {X0(j)}, {T(T2B, u + j)}')
@@ -520,6 +518,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'  v_mov_b64_e32 {pair(HO[T2B])}, 0')
         e(f'  v_mov_b32_e32 v{VMK}, {hex(MASK)}')
         e(f'  v_cndmask_b32_e64 v{VMK}, v{VMK}, 0, s[20:21]')
+        if sq:                                   # window 2 of a squaring is 2 x0 x1: double x1's limbs (< 2^28)
+            for j in range(Q):                   # once instead of 2 x0_i at every step; x1 is dead after the pass
+                e(f'  v_lshlrev_b32_e32 {X1(j)}, 1, {X1(j)}')
         e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
         if not sq:
             e(f'  ds_read_b32 v{V_BI[0]}, v{V_LDSI} offset:{S * RB}')
