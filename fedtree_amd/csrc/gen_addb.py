@@ -368,11 +368,11 @@ def gen_addb(name: str) -> str:
             e(f'  v_lshrrev_b32_e32 {U(i)}, {lo - B * j0}, {src(j0)}')
             for jj in range(j0 + 1, j1 + 1):
                 e(f'  v_lshl_or_b32 {U(i)}, {src(jj)}, {B * jj - lo}, {U(i)}')
-        e(f'  v_sub_u32_e32 {bo}, 31, v{V_SH}')                      # 31 - 2j
-        for i in range(31, 0, -1):
-            e(f'  v_lshrrev_b32_e32 {t1}, {bo}, {U(i - 1)}')
-            e(f'  v_lshrrev_b32_e32 {t1}, 1, {t1}')
-            e(f'  v_lshl_or_b32 {U(i)}, {U(i)}, v{V_SH}, {t1}')
+        e(f'  v_sub_u32_e32 {bo}, 32, v{V_SH}')
+        e(f'  v_and_b32_e32 {bo}, 31, {bo}')                          # 32 - 2j (lane 0: 0)
+        for i in range(31, 0, -1):                     # (U(i) << 2j) | (U(i-1) >> 32 - 2j); lane 0 keeps U(i)
+            e(f'  v_alignbit_b32 {t1}, {U(i)}, {U(i - 1)}, {bo}')
+            e(f'  v_cndmask_b32_e64 {U(i)}, {t1}, {U(i)}, s[22:23]')
         e('  s_nop 1')
         e(f'  v_mov_b32_dpp {t1}, {src(Q - 1)} quad_perm:[0,0,1,2] {DPP}')
         e(f'  v_sub_u32_e32 {bo}, {B}, v{V_SH}')                     # lane 0: shift 27 -> no bits

@@ -266,6 +266,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     # ---- persistent waves: workgroup wg owns the batches wg, wg + nwg, ... of 16 ciphertexts; its waves draw
     #      them from the LDS counter (a wave the SIMD's arbiter favours runs more of them, as fthe_addb_q152),
     #      and run the whole program on each (the END op draws the next) ----------------------------------------
+    e('// @phase batch')
     e('.Lnext_batch:')
     e('  s_mov_b64 exec, 1')
     e(f'  v_mov_b32_e32 v{V_TMP}, {hex(LDS_CNT)}')
@@ -283,6 +284,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_add_u32_e32 v{V_ROW}, s44, v{V_LANE}')
     e('  s_mov_b64 s[6:7], s[40:41]')
     e('.Lprog:')
+    e('// @phase ops')
     e('  s_load_dwordx2 s[14:15], s[6:7], 0x0')
     e('  s_add_u32 s6, s6, 8')
     e('  s_addc_u32 s7, s7, 0')
@@ -511,6 +513,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 e('  s_waitcnt lgkmcnt(2)')                      # the prefetch reads (issued before the writes)
 
         e(f'{lab}:')
+        e('// @phase product')
         for k in range(NT):
             e(f'  v_mov_b64_e32 {T(T1B, k)}, 0')
             e(f'  v_mov_b64_e32 {T(T2B, k)}, 0')
@@ -545,6 +548,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         if "noprod" in DBG:
             e(f'{lab}_skip:')
         e('  s_waitcnt lgkmcnt(0)')
+        e('// @phase window')
         # ---- normalise both windows: positions TL .. TL + 18 -> 19 limbs (z limbs 76 + 19 k + j) --------
         for tb, tag in ((T1B, 'n1'), (T2B, 'n2')):
             e(f'  v_mov_b64_e32 {tmp}, 0')
@@ -553,6 +557,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 e(f'  v_and_b32_e32 {Tlo(tb, TL + k)}, {hex(MASK)}, v{V_TMP}')
                 e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
             ripple_quad(f'{lab}_{tag}', lambda k, tb=tb: Tlo(tb, TL + k), Q)
+        e('// @phase conv')
         # ---- z1, z2 -> dwords Z1, Z2 (quad layout of the add kernel) ----------------------------------------
         for tb, zb, row0, tag in ((T1B, Z1B, 0, 'z1'), (T2B, Z2B, S, 'z2')):
             if "noconv" not in DBG:
@@ -586,11 +591,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  v_lshrrev_b32_e32 {U(i)}, {lo - B * j0}, v{ZL + j0}')
             for jj in range(j0 + 1, j1 + 1):
                 e(f'  v_lshl_or_b32 {U(i)}, v{ZL + jj}, {B * jj - lo}, {U(i)}')
-        e(f'  v_sub_u32_e32 {bo}, 31, v{V_SH}')                      # 31 - 2j
-        for i in range(31, 0, -1):
-            e(f'  v_lshrrev_b32_e32 {t1}, {bo}, {U(i - 1)}')
-            e(f'  v_lshrrev_b32_e32 {t1}, 1, {t1}')
-            e(f'  v_lshl_or_b32 {U(i)}, {U(i)}, v{V_SH}, {t1}')
+        e(f'  v_sub_u32_e32 {bo}, 32, v{V_SH}')
+        e(f'  v_and_b32_e32 {bo}, 31, {bo}')                          # 32 - 2j (lane 0: 0)
+        for i in range(31, 0, -1):                     # (U(i) << 2j) | (U(i-1) >> 32 - 2j); lane 0 keeps U(i)
+            e(f'  v_alignbit_b32 {t1}, {U(i)}, {U(i - 1)}, {bo}')
+            e(f'  v_cndmask_b32_e64 {U(i)}, {t1}, {U(i)}, s[22:23]')
         e('  s_nop 1')
         e(f'  v_mov_b32_dpp {t1}, v{ZL + 2 * Q - 1} quad_perm:[0,0,1,2] {DPP}')
         e(f'  v_sub_u32_e32 {bo}, {B}, v{V_SH}')                     # lane 0: shift 27 -> no bits
@@ -610,6 +615,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{8 * gl}')
 
     def mfma_product(prod):
+        e(f'// @phase mfma{prod}')
         A = V_A1 if prod == 1 else V_A2
         KO = KO1 if prod == 1 else KO2
         act = ACT1 if prod == 1 else ACT2
@@ -681,6 +687,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         delivered: lane k + 1 adds lane k's carry-out to its lowest dword; the signed overflow of that add (rare:
         |carry| < 2^18 against a uniform dword) ripples through the lane's dwords on a slow path and changes its
         carry-out, which is delivered the same way until no lane receives one.  CR: every lane's final carry."""
+        e('// @phase norm')
         sizes = [4 * len(ch) for ch in CHUNKS]
         assert sizes[:2] == [32, 32] and sizes[2] == 4 and len(sizes) == 3
         L012, L01 = "s[34:35]", "s[28:29]"
@@ -758,6 +765,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         """q1 = z dwords 63..128 (XORed 0x80808080) -> staging positions 0..65, zero 66..79; B operands.
         Lane k's local dword i is z dword 32 k + i -> position 32 k - 63 + i: lanes 2, 3 all of theirs (lane 3
         also local 32 = dword 128), lane 1 its local 31 (position 0)."""
+        e('// @phase stage')
         t = DQ                                                   # XORed copies (DQ is free here)
         for i in range(33):
             e(f'  v_xor_b32_e32 v{t + i}, s33, v{zb + i}')
@@ -793,6 +801,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     def stage_q3():
         """q3 dword d = N1 dword d + 1: lane k holds N1 dwords [32 k, 32 k + 32) in DQ -> positions 32 k - 1 + i
         (lane 0 from i = 1); positions 65..79 get lane 2's zeros; XOR 0x80 only on the real bytes (0..64)"""
+        e('// @phase stage')
         e('  s_mov_b64 exec, s[28:29]')                                    # lanes 0, 1: DQ 2..31 real
         for i in range(2, 32):
             e(f'  v_xor_b32_e32 v{DQ + i}, s33, v{DQ + i}')
@@ -882,6 +891,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     def remainder_to_digit(zb, X, tag):
         """r = (z - r2) mod 2^2080 (lane j: dwords [32 j, 32 j + 32), lane 2: dword 64 only) -> staging row
         positions 0..64 -> lane k reads positions [16 k, 16 k + 17), funnel-shifts by k, 19 limbs of 27 bits"""
+        e('// @phase remainder')
         e(f'  v_sub_co_u32_e32 v{zb}, vcc, v{zb}, v{DQ}')
         for i in range(1, 32):
             e(f'  v_subb_co_u32_e32 v{zb + i}, vcc, v{zb + i}, v{DQ + i}, vcc')
@@ -929,6 +939,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     clear_dq()
     mfma_product(1)
     clamp('.Lnoclamp1')
+    e('// @phase q3add')
     # z2 += q3_1: Z2 local i += DQ[i + 1] (i < 31), local 31 += the next lane's DQ[0]
     _dbg_noq3 = os.environ.get("FTHE_GEN_NADICB_DBG") == "noq3"
     if _dbg_noq3:
