@@ -65,7 +65,8 @@ LDS_CNT = LDS_WAVES + WAVES * WAVE_AREA      # the workgroup's batch counter (dw
 LDS_BYTES = LDS_CNT + 16                     # 153,872
 QROW = 656                                   # q staging row: 9 K-blocks of 64 bytes, stride = 4 (mod 32)
                                              # dwords: the quads' staging writes 4-way, not 16-way, per bank
-GROW = 296                                   # group staging row (36 int64 groups + pad: conflict-free)
+GROW = 560                                   # group staging row: two chunks' 64-68 int64 groups + pad (16-byte
+                                             # aligned: the normalisation reads two groups per ds_read_b128)
 KB1, KB2 = 9, 9
 NQ1, NQ3 = 129, 129                          # q1, q3 dwords (rows >= N: q3 < 2^4098)
 MU_SHIFT = 4072 + 4128                       # mu = floor(2^(A + C) / N)
@@ -74,7 +75,7 @@ BIAS_COL, BIAS_DIGIT = 515, -2               # -2^4121 in product 1's correction
 M_A = (0, 1, 2, 3, 12, 13, 14, 15)           # rows whose copies sit in slots 0..7 (ds_read_b128 lane groups)
 M_B = (4, 5, 6, 7, 8, 9, 10, 11)             # slots 8..15
 assert IMG_BYTES % 16 == 0 and WAVE_AREA % 16 == 0 and LDS_BYTES <= 160 * 1024
-assert WAVE_AREA >= max(S * RB, 16 * QROW) and QROW % 16 == 0 and (QROW // 4) % 32 == 4
+assert WAVE_AREA >= max(S * RB, 16 * QROW, 16 * GROW) and QROW % 16 == 0 and (QROW // 4) % 32 == 4
 
 
 def layout_header():
@@ -258,7 +259,9 @@ def gen_addb(name: str) -> str:
     e(f'  v_and_b32_e32 v{V_TMP}, 63, v{V_TID}')
     e(f'  v_lshrrev_b32_e32 v{V_TMP}, 2, v{V_TMP}')                    # c
     e(f'  v_mul_u32_u24_e32 v{V_GR}, {GROW}, v{V_TMP}')
-    e(f'  v_add_u32_e32 v{V_GR}, s15, v{V_GR}')                        # group row c (fold reads)
+    e(f'  v_add_u32_e32 v{V_GR}, s15, v{V_GR}')                        # group row c
+    e(f'  v_and_b32_e32 v{V_TMP + 1}, 1, v{V_TID}')
+    e(f'  v_lshl_add_u32 v{V_GR}, v{V_TMP + 1}, 8, v{V_GR}')          # quad lanes 1, 3: the pair's 2nd chunk
     e(f'  v_mul_u32_u24_e32 v{V_Q3W}, {QROW}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_Q3W}, s15, v{V_Q3W}')                      # staging row c (+ 128 j below)
     e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_TID}')                         # j
@@ -534,7 +537,7 @@ def gen_addb(name: str) -> str:
         corr = 0 if prod == 1 else CORR2_OFF - CORR1_OFF
         e(f'  v_mov_b32_e32 v{CR}, 0')
         for j, tiles in enumerate(CHUNKS):
-            t0 = tiles[0]
+            t0 = CHUNKS[j & ~1][0]                   # groups staged from the pair's first tile
             ops = [(n, t, kb) for n, t in enumerate(tiles) for kb in act[t]]
             q = []                                   # outstanding LDS ops, oldest first (tags)
 
@@ -585,39 +588,84 @@ def gen_addb(name: str) -> str:
             e('  s_nop 7')
             e('  s_nop 7')
             fold_tile(ACC[(len(tiles) - 1) % 2], 4 * (tiles[-1] - t0))
+            if j % 2 == 0:
+                continue                             # the pair's second chunk first
             e('  s_waitcnt lgkmcnt(0)')
-            # carry in: lane j's chunk starts from lane j-1's final carry (lane 0: none)
-            if j:
-                e('  s_nop 1')
-                e(f'  v_mov_b32_dpp v{CR2}, v{CR} quad_perm:[0,0,1,2] {DPP}')
             e('// @phase norm')
-            if "nonorm" in DBG:
-                continue
-            e(f'  s_mov_b64 exec, {LANE_MASK[j]}')
-            ng = 4 * len(tiles)
-            # D_g = low dword of (group g + carry), carry = its high dword (signed): one v_mad_i64_i32 per
-            # group (carry x 1 + group); an even g writes the pair (D_g, D_g+1), D_g+1 holding the carry
-            # until the odd group's result replaces it
-            cv = f"v{CR2}" if j else f"v{CR}"
-            assert DQ % 2 == 0 and ng % 2 == 0
-            for g0 in range(0, ng, 8):
-                for g in range(g0, min(ng, g0 + 8)):
-                    e(f'  ds_read_b64 {pair(GB + 2 * (g - g0))}, v{V_GR} offset:{8 * g}')
-                e('  s_waitcnt lgkmcnt(0)')
-                for g in range(g0, min(ng, g0 + 8)):
-                    if g % 2 == 0:
-                        e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
-                        cv = f"v{DQ + g + 1}"
-                    else:
-                        e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {pair(GB + 2 * (g - g0))}')
-                        e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
-                        cv = f"v{FV + 1}"
-            e(f'  v_mov_b32_e32 v{CR}, {cv}')
-            e('  s_mov_b64 exec, -1')
+            if "nonorm" not in DBG:
+                norm_pair(j - 1, j)
             e(f'// @phase prod{prod}')
 
+    def norm_pair(ja, jb):
+        """Chunks ja, jb = ja + 1 at once: quad lane ja from its carry-in (lane ja - 1's final carry; 0 for chunk
+        0), quad lane jb from 0, one v_mad_i64_i32 chain each (D_g = low dword of group g + carry, carry = its
+        high dword, signed); then lane ja's carry-out is added to lane jb's lowest dword, and the signed overflow
+        of that add, rare, ripples through lane jb's dwords on a slow path into its carry.  CR: the final carries
+        (lane 3's: the clamp's).  Two passes per product instead of four chunk after chunk."""
+        na, nb = 4 * len(CHUNKS[ja]), 4 * len(CHUNKS[jb])
+        assert na == 32 and nb in (32, 36) and DQ % 2 == 0
+        e(f'  s_or_b64 s[16:17], {LANE_MASK[ja]}, {LANE_MASK[jb]}')
+        if ja:
+            e('  s_nop 1')
+            e(f'  v_mov_b32_dpp v{CR2}, v{CR} quad_perm:[0,0,1,2] {DPP}')      # lane ja: lane ja - 1's carry
+        else:
+            e(f'  v_mov_b32_e32 v{CR2}, 0')
+        e(f'  v_cndmask_b32_e64 v{CR2}, v{CR2}, 0, {LANE_MASK[jb]}')          # lane jb: 0
+        e('  s_mov_b64 exec, s[16:17]')
+        cv = f"v{CR2}"
+
+        def rd(g):
+            e(f'  ds_read_b128 v[{GB + 4 * ((g // 2) % 2)}:{GB + 4 * ((g // 2) % 2) + 3}], v{V_GR} offset:{8 * g}')
+        ng = max(na, nb)
+        rd(0)
+        rd(2)
+        for g0 in range(0, ng, 2):
+            if g0 == na and nb > na:                 # lane ja's chunk ends (its carry stays in FV + 1)
+                e(f'  s_mov_b64 exec, {LANE_MASK[jb]}')
+            e(f'  s_waitcnt lgkmcnt({1 if g0 + 2 < ng else 0})')
+            for g in (g0, g0 + 1):
+                src = pair(GB + 4 * ((g0 // 2) % 2) + 2 * (g - g0))
+                if g % 2 == 0:
+                    e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {src}')
+                    cv = f"v{DQ + g + 1}"
+                else:
+                    e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {src}')
+                    e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
+                    cv = f"v{FV + 1}"
+            if g0 + 4 < ng:
+                rd(g0 + 4)
+        assert cv == f"v{FV + 1}"
+        e('  s_mov_b64 exec, s[16:17]')
+        e(f'  v_mov_b32_e32 v{CR}, {cv}')
+        e('  s_mov_b64 exec, -1')
+        # lane ja's carry-out into lane jb's lowest dword
+        X, TP = CR + 1, V_TMP
+        lab = f'.Lnp{len(o)}'
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{X}, v{CR} quad_perm:[0,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 v{X}, 0, v{X}, {LANE_MASK[jb]}')              # lane jb only
+        e(f'  v_mov_b32_e32 v{TP}, v{DQ}')
+        e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+        e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{X}, 1, {pair(TP)}')
+        e(f'  v_mov_b32_e32 v{DQ}, v{TP}')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{TP + 1}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        e('  s_and_saveexec_b64 s[16:17], vcc')                              # slow path: the overflowing lanes
+        e(f'  v_mov_b32_e32 v{X}, v{TP + 1}')
+        for i in range(1, nb):
+            e(f'  v_mov_b32_e32 v{TP}, v{DQ + i}')
+            e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+            e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{X}, 1, {pair(TP)}')
+            e(f'  v_mov_b32_e32 v{DQ + i}, v{TP}')
+            e(f'  v_mov_b32_e32 v{X}, v{TP + 1}')
+        e(f'  v_add_u32_e32 v{CR}, v{X}, v{CR}')
+        e('  s_mov_b64 exec, s[16:17]')
+        e(f'{lab}_done:')
+
     def fold_tile(acc, gl):
-        """acc's 4 int32 rows (output bytes 4h..4h+3 of the tile) -> int64 group -> LDS (group 4 (t - t0) + h)"""
+        """acc's 4 int32 rows (output bytes 4h..4h+3 of the tile) -> int64 group -> LDS (group 4 (t - t0) + h, t0
+        the first tile of the chunk pair)"""
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc}, 1, 0')                # sign-extended row 0
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 1}, s30, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 2}, s31, {pair(PG)}')

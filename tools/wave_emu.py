@@ -256,6 +256,10 @@ class Wave:
             self.scc = int(self.exec != 0)
         elif op == 's_mul_i32':
             self.sset(a[0], g(a[1]) * g(a[2]))
+        elif op == 's_or_b64':
+            r = g(a[1], 2) | g(a[2], 2)
+            self.sset(a[0], r)
+            self.scc = int(r != 0)
         elif op == 's_lshr_b32':
             r = (g(a[1]) & M32) >> (g(a[2]) & 31)
             self.sset(a[0], r)
