@@ -402,6 +402,11 @@ def gen_addb(name: str) -> str:
             e(f'  v_mad_u64_u32 v[{c0}:{c1}], vcc, {vals(k)}, 1, v[{c0}:{c1}]')
             e(f'  v_and_b32_e32 {vals(k)}, {hex((1 << width) - 1)}, v{c0}')
             e(f'  {shr} v[{c0}:{c1}], {width}, v[{c0}:{c1}]')
+            if k == 1 and nv > 2:                # a carry absorbed by limbs 0, 1 everywhere (the usual case):
+                e(f'  v_or_b32_e32 v{a0}, v{c0}, v{c1}')      # no carry-out changes, nothing left to hand on
+                e(f'  v_cmp_ne_u32_e32 vcc, 0, v{a0}')
+                e('  s_nop 4')
+                e(f'  s_cbranch_vccz {lab}_done')
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 
@@ -721,10 +726,15 @@ def gen_addb(name: str) -> str:
         e('  s_nop 4')
         e(f'  s_cbranch_vccz {lab}_done')
         e(f'  v_sub_co_u32_e32 v{R}, vcc, v{R}, v{bin_}')
+        e(f'  v_mov_b32_e32 v{bo}, 0')                                   # the borrows handed on are delivered
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')                               # absorbed by dword 0 everywhere (usual)
+        e('  s_and_saveexec_b64 s[38:39], vcc')                         # the lanes whose dword 0 borrowed
         for i in range(1, 32):
             e(f'  v_subb_co_u32_e64 v{R + i}, vcc, v{R + i}, 0, vcc')
         e(f'  v_cndmask_b32_e64 v{bo}, 0, 1, vcc')
         e(f'  v_subb_co_u32_e64 v{R128_}, vcc, v{R128_}, 0, vcc')
+        e('  s_mov_b64 exec, s[38:39]')
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 

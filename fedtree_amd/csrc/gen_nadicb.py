@@ -354,6 +354,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  v_mad_u64_u32 {tmp}, vcc, {vals(k)}, 1, {tmp}')
             e(f'  v_and_b32_e32 {vals(k)}, {hex((1 << width) - 1)}, v{V_TMP}')
             e(f'  {shr} {tmp}, {width}, {tmp}')
+            if k == 1 and nv > 2:                # a carry absorbed by limbs 0, 1 everywhere (the usual case):
+                e(f'  v_or_b32_e32 v{a0}, v{V_TMP}, v{V_TMP + 1}')   # no carry-out changes, nothing to hand on
+                e(f'  v_cmp_ne_u32_e32 vcc, 0, v{a0}')
+                e('  s_nop 4')
+                e(f'  s_cbranch_vccz {lab}_done')
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 
@@ -864,12 +869,16 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e('  s_nop 4')
         e(f'  s_cbranch_vccz {lab}_done')
         e(f'  v_add_co_u32_e32 v{R}, vcc, v{R}, v{cin}')
+        e(f'  v_mov_b32_e32 v{ci}, 0')                                   # the carries handed on are delivered
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')                               # absorbed by dword 0 everywhere (usual)
+        e('  s_and_saveexec_b64 s[34:35], vcc')                         # the lanes whose dword 0 carried
         for i in range(1, n):
             e(f'  v_addc_co_u32_e32 v{R + i}, vcc, 0, v{R + i}, vcc')
         e(f'  v_cndmask_b32_e64 v{ci}, 0, 1, vcc')
-        e('  s_mov_b64 exec, s[20:21]')
+        e('  s_and_b64 exec, exec, s[20:21]')                            # lane 3: into its top dword
         e(f'  v_add_u32_e32 v{R + n}, v{R + n}, v{ci}')
-        e('  s_mov_b64 exec, -1')
+        e('  s_mov_b64 exec, s[34:35]')
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 
@@ -882,9 +891,14 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e('  s_nop 4')
         e(f'  s_cbranch_vccz {lab}_done')
         e(f'  v_sub_co_u32_e32 v{R}, vcc, v{R}, v{bin_}')
+        e(f'  v_mov_b32_e32 v{bo}, 0')                                   # the borrows handed on are delivered
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')                               # absorbed by dword 0 everywhere (usual)
+        e('  s_and_saveexec_b64 s[34:35], vcc')                         # the lanes whose dword 0 borrowed
         for i in range(1, n):
             e(f'  v_subb_co_u32_e64 v{R + i}, vcc, v{R + i}, 0, vcc')
         e(f'  v_cndmask_b32_e64 v{bo}, 0, 1, vcc')
+        e('  s_mov_b64 exec, s[34:35]')
         e(f'  s_branch {lab}_loop')
         e(f'{lab}_done:')
 
