@@ -75,8 +75,10 @@ IMG_BYTES = CORR2_OFF + TILES2 * 64
 N_OFF = IMG_BYTES                                     # n limbs (76 x u32) in ctx, not copied to LDS
 CTX_BYTES = N_OFF + 4 * S
 QROW = 400                       # q / r staging row: 80 dwords used; 100 dwords == 4 mod 32 (4-way stores)
-GROW = 560                       # group staging row: a product's 68 int64 groups (every chunk at once) + pad;
+GROW = 624                       # group staging row: a product's 68 int64 groups (every chunk at once) + pad;
                                  # 16-byte aligned rows for the normalisation's ds_read_b128 of two groups
+CSTRIDE = 272                    # chunk k's groups at 272 k: with GROW = 624 the normalisation's reads are
+                                 # conflict-free and the folds' writes 2-way (tools/lds_conflicts.py)
 QST_OFF = 0                      # staging areas inside the wave area (the A column is dead in the Barretts); the
 GST_OFF = 0                      # groups overlap the q staging, which the B operands have left before the MFMAs
 WAVE_AREA = max(ROWS * RB, QST_OFF + 16 * QROW, GST_OFF + 16 * GROW)
@@ -232,7 +234,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_add_u32_e32 v{V_GR}, v{V_GR}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_GR}, {GST_OFF}, v{V_GR}')                 # group row of c
     e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_LANE}')                        # k
-    e(f'  v_lshl_add_u32 v{V_GR}, v{V_SH}, 8, v{V_GR}')               # + 256 k: quad lane k's chunk (norm reads)
+    e(f'  v_mul_u32_u24_e32 v{V_TMP + 1}, {CSTRIDE}, v{V_SH}')
+    e(f'  v_add_u32_e32 v{V_GR}, v{V_GR}, v{V_TMP + 1}')               # + CSTRIDE k: quad lane k's chunk (norm reads)
     e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_LANE}')                        # k (quad lane)
     e(f'  v_mul_u32_u24_e32 v{V_LDSW}, {Q * RB}, v{V_SH}')
     e(f'  v_add_u32_e32 v{V_LDSW}, v{V_LDSW}, v{V_LDSI}')              # area + 4 c + 19 k RB
@@ -612,12 +615,17 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         emit_product(sq)
 
     # ---- the two Barrett reductions ------------------------------------------------------------------------
-    def fold_tile(acc, gl):
+    def stage_off(t):
+        """byte offset of tile t's groups in the staging row: chunk k at CSTRIDE k"""
+        k = next(i for i, ch in enumerate(CHUNKS) if t in ch)
+        return CSTRIDE * k + 32 * (t - CHUNKS[k][0])
+
+    def fold_tile(acc, off):
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc}, 1, 0')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 1}, s30, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 2}, s31, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 3}, s32, {pair(PG)}')
-        e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{8 * gl}')
+        e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{off}')
 
     def mfma_product(prod):
         e(f'// @phase mfma{prod}')
@@ -674,14 +682,14 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                     e('  s_nop 7')
                     e('  s_nop 7')
                     e('  s_nop 3')
-                    fold_tile(ACC[(n - 1) % 2], 4 * tiles[n - 1])              # group 4 t (every chunk staged)
+                    fold_tile(ACC[(n - 1) % 2], stage_off(tiles[n - 1]))            # every chunk staged
                     q.append(('w', n - 1))
                     if n + 1 < len(tiles):
                         read_corr(n + 1, tiles[n + 1])
             e('  s_nop 7')
             e('  s_nop 7')
             e('  s_nop 7')
-            fold_tile(ACC[(len(tiles) - 1) % 2], 4 * tiles[-1])
+            fold_tile(ACC[(len(tiles) - 1) % 2], stage_off(tiles[-1]))
         e('  s_waitcnt lgkmcnt(0)')
         if "nonorm" not in DBG:
             normalise_chunks()

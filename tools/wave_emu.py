@@ -525,6 +525,8 @@ class Wave:
                 r = g(l, a[1]) * g(l, a[2])
             elif op == 'v_mul_u32_u24_e32':
                 r = (g(l, a[1]) & 0xFFFFFF) * (g(l, a[2]) & 0xFFFFFF)
+            elif op == 'v_mad_u32_u24':
+                r = (g(l, a[1]) & 0xFFFFFF) * (g(l, a[2]) & 0xFFFFFF) + g(l, a[3])
             elif op == 'v_add3_u32':
                 r = g(l, a[1]) + g(l, a[2]) + g(l, a[3])
             elif op == 'v_lshl_add_u32':
