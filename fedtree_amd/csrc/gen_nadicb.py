@@ -522,6 +522,10 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
 
         e(f'{lab}:')
         e('// @phase product')
+        if "prio" in DBG:                        # timing knobs: the product pass at low / high priority
+            e('  s_setprio 0')
+        if "prioinv" in DBG:
+            e('  s_setprio 3')
         for k in range(NT):
             e(f'  v_mov_b64_e32 {T(T1B, k)}, 0')
             e(f'  v_mov_b64_e32 {T(T2B, k)}, 0')
@@ -557,6 +561,10 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'{lab}_skip:')
         e('  s_waitcnt lgkmcnt(0)')
         e('// @phase window')
+        if "prio" in DBG:
+            e('  s_setprio 3')
+        if "prioinv" in DBG:
+            e('  s_setprio 0')
         # ---- normalise both windows: positions TL .. TL + 18 -> 19 limbs (z limbs 76 + 19 k + j) --------
         for tb, tag in ((T1B, 'n1'), (T2B, 'n2')):
             e(f'  v_mov_b64_e32 {tmp}, 0')
