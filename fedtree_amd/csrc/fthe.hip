@@ -186,6 +186,17 @@ size_t enc_chunk_lanes() {
     return v;
 }
 
+// the parties' public-key encrypt on fthe_nadic_b76 (persistent waves: more batches per wave balance the SIMDs
+// better): lanes per launch, four per ciphertext; FTHE_PUB_CHUNK overrides
+size_t pub_chunk_lanes() {
+    static const size_t v = [] {
+        const char *e = getenv("FTHE_PUB_CHUNK");
+        size_t c = e ? (size_t)strtoull(e, nullptr, 10) : chunk_lanes();
+        return c < 3072 ? (size_t)3072 : c;
+    }();
+    return v;
+}
+
 // window width minimising table + multiplications for an e-bit exponent
 int best_window(size_t ebits) {
     int best = 1; double bc = 1e30;
@@ -1822,7 +1833,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     const int nsl = nslots_for(k);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2,
-                        direct_y && !split && !quad ? enc_chunk_lanes() : 0);
+                        direct_y && !split && !quad ? enc_chunk_lanes() : !crt && k->nadic_b ? pub_chunk_lanes() : 0);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     // Device-drawn randomness under CRT draws y_p, y_q uniform in [1,p), [1,q) and
