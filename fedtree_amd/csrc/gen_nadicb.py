@@ -165,7 +165,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     # s32 = 2^24, s33 = 0x80808080, s[34:35] saved exec, s36 ctx lo + N_OFF, s[40:41] the program's first op,
     # s42 workgroups launched, s43 batches of 16 ciphertexts, s44 scratch
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
-    NSGPR = 46
+    NSGPR = 72 if "stamp" in DBG else 46
 
     o = []
     e = o.append
@@ -215,6 +215,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e('  s_load_dwordx2 s[42:43], s[0:1], 0x20')                         # live ciphertexts, workgroups launched
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
+    e('// @stampinit')
     e('  s_add_u32 s44, s42, 15')
     e('  s_lshr_b32 s44, s44, 4')                                         # batches of 16 ciphertexts
     e('  s_mov_b32 s42, s43')
@@ -597,14 +598,19 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
             e(f'  ds_read_b32 v{ZL + k}, v{V_TMP} offset:{(row0 + k) * RB}')
         e('  s_mov_b64 exec, -1')
         e('  s_waitcnt lgkmcnt(0)')
-        for k in range(2 * Q):                         # product limbs were stored with their carries above bit 27
+        # product limbs were stored with their carries above bit 27: a limb's first use takes bits [s, 27) by
+        # v_bfe_u32, a last use shifts the carries out of the dword; only the limbs that end inside a dword
+        # (and limb 37, whose top bits go to the next lane and dword 128) are masked
+        dw = [(32 * i - B * (32 * i // B), 32 * i // B, min((32 * i + 31) // B, 2 * Q - 1)) for i in range(32)]
+        mid = sorted({jj for i, (s, j0, j1) in enumerate(dw) for jj in range(j0 + 1, j1 + 1)
+                      if B * jj - 32 * i + B < 32} | {2 * Q - 1})
+        for k in mid:
             e(f'  v_and_b32_e32 v{ZL + k}, {hex(MASK)}, v{ZL + k}')
         U = lambda i: f"v{zb + i}"
         t1, bo = f"v{V_AI[0]}", f"v{V_AI[1]}"
-        for i in range(32):
-            lo, hi = 32 * i, 32 * i + 31
-            j0, j1 = lo // B, min(hi // B, 2 * Q - 1)
-            e(f'  v_lshrrev_b32_e32 {U(i)}, {lo - B * j0}, v{ZL + j0}')
+        for i, (s, j0, j1) in enumerate(dw):
+            lo = 32 * i
+            e(f'  v_bfe_u32 {U(i)}, v{ZL + j0}, {s}, {B - s}')
             for jj in range(j0 + 1, j1 + 1):
                 e(f'  v_lshl_or_b32 {U(i)}, v{ZL + jj}, {B * jj - lo}, {U(i)}')
         e(f'  v_sub_u32_e32 {bo}, 32, v{V_SH}')
@@ -783,13 +789,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'{lab}_done:')
 
     def stage_q1(zb):
-        """q1 = z dwords 63..128 (XORed 0x80808080) -> staging positions 0..65, zero 66..79; B operands.
+        """q1 = z dwords 63..128 (raw) -> staging positions 0..65, 0x80 bytes at 66..79; B operands (read_b).
         Lane k's local dword i is z dword 32 k + i -> position 32 k - 63 + i: lanes 2, 3 all of theirs (lane 3
         also local 32 = dword 128), lane 1 its local 31 (position 0)."""
         e('// @phase stage')
-        t = DQ                                                   # XORed copies (DQ is free here)
-        for i in range(33):
-            e(f'  v_xor_b32_e32 v{t + i}, s33, v{zb + i}')
+        t = zb                                                   # raw dwords: the B operands are XORed after the read
         e(f'  v_bfe_u32 v{V_TMP}, v{V_ROW}, 7, 2')
         e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_TMP}')
         e(f'  v_add_u32_e32 v{V_TMP}, v{V_TMP}, v{V_QW}')                 # row + 128 k
@@ -805,15 +809,23 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'  ds_write_b32 v{V_TMP + 1}, v{t + 31} offset:{4 * 31}')
         e('  s_mov_b64 exec, s[20:21]')
         e(f'  ds_write_b32 v{V_TMP + 1}, v{t + 32} offset:{4 * 32}')       # lane 3: dword 128 -> position 65
-        e('  s_mov_b64 exec, s[22:23]')                                    # lane 0: zero positions 66..79
-        e(f'  v_mov_b32_e32 v{V_TMP}, 0')
+        e('  s_mov_b64 exec, s[22:23]')                  # lane 0: positions 66..79 = 0x80 bytes (0 after the XOR)
+        e(f'  v_mov_b32_e32 v{V_TMP}, s33')
         for d in range(NQ1, 16 * KB1):
             e(f'  ds_write_b32 v{V_QW}, v{V_TMP} offset:{4 * d}')
         e('  s_mov_b64 exec, -1')
+        read_b(KB1)
+
+    def read_b(kbs):
+        """the B operands (staged raw) -> registers, XOR 0x80 per byte: u8 -> u8 - 128 as i8 (20 XORs instead of
+        one per staged dword)"""
         e('  s_waitcnt lgkmcnt(0)')
-        for kb in range(KB1):
+        for kb in range(kbs):
             e(f'  ds_read_b128 {quad4(BQ + 4 * kb)}, v{V_B} offset:{64 * kb}')
-        e('  s_waitcnt lgkmcnt(0)')
+        for kb in range(kbs):
+            e(f'  s_waitcnt lgkmcnt({kbs - 1 - kb})')
+            for i in range(4):
+                e(f'  v_xor_b32_e32 v{BQ + 4 * kb + i}, s33, v{BQ + 4 * kb + i}')
 
     def clear_dq():
         for i in range(32):
@@ -821,32 +833,29 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
 
     def stage_q3():
         """q3 dword d = N1 dword d + 1: lane k holds N1 dwords [32 k, 32 k + 32) in DQ -> positions 32 k - 1 + i
-        (lane 0 from i = 1); positions 65..79 get lane 2's zeros; XOR 0x80 only on the real bytes (0..64)"""
+        (lane 0 from i = 1), raw; lane 2 sets positions 65..79 to 0x80 bytes, which read_b's XOR makes 0"""
         e('// @phase stage')
-        e('  s_mov_b64 exec, s[28:29]')                                    # lanes 0, 1: DQ 2..31 real
-        for i in range(2, 32):
-            e(f'  v_xor_b32_e32 v{DQ + i}, s33, v{DQ + i}')
         e('  s_mov_b32 s34, 0x77777777')
         e('  s_mov_b32 s35, 0x77777777')
-        e('  s_mov_b64 exec, s[34:35]')                                    # lanes 0..2: DQ 0, 1
-        e(f'  v_xor_b32_e32 v{DQ}, s33, v{DQ}')
-        e(f'  v_xor_b32_e32 v{DQ + 1}, s33, v{DQ + 1}')
+        e('  s_mov_b64 exec, s[34:35]')                                    # lanes 0..2
         e(f'  v_bfe_u32 v{V_TMP}, v{V_ROW}, 7, 2')
         e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_TMP}')
         e(f'  v_add_u32_e32 v{V_TMP}, v{V_TMP}, v{V_QW}')                 # row + 128 k = position 32 k
         for i in range(1, 31, 2):
             e(f'  ds_write2_b32 v{V_TMP}, v{DQ + i}, v{DQ + i + 1} offset0:{i - 1} offset1:{i}')
         e(f'  ds_write_b32 v{V_TMP}, v{DQ + 31} offset:{4 * 30}')
+        e('  s_mov_b64 exec, s[26:27]')                  # lane 2: positions 65..79 = 0x80 bytes (0 after the XOR)
+        e(f'  v_mov_b32_e32 v{V_TMP + 1}, s33')
+        for d in range(65, 16 * KB2 - 1, 2):
+            e(f'  ds_write2_b32 v{V_TMP}, v{V_TMP + 1}, v{V_TMP + 1} offset0:{d - 64} offset1:{d - 63}')
+        e(f'  ds_write_b32 v{V_TMP}, v{V_TMP + 1} offset:{4 * (16 * KB2 - 1 - 64)}')
         e('  s_mov_b32 s34, 0x66666666')
         e('  s_mov_b32 s35, 0x66666666')
         e('  s_mov_b64 exec, s[34:35]')                                    # lanes 1, 2: N1 dword 32 k -> pos 32 k - 1
         e(f'  v_subrev_u32_e32 v{V_TMP}, 4, v{V_TMP}')
         e(f'  ds_write_b32 v{V_TMP}, v{DQ}')
         e('  s_mov_b64 exec, -1')
-        e('  s_waitcnt lgkmcnt(0)')
-        for kb in range(KB2):
-            e(f'  ds_read_b128 {quad4(BQ + 4 * kb)}, v{V_B} offset:{64 * kb}')
-        e('  s_waitcnt lgkmcnt(0)')
+        read_b(KB2)
 
     def unxor_q3():
         e('  s_mov_b64 exec, s[28:29]')
@@ -1003,12 +1012,60 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e('  s_branch .Lsqr_loop')
 
     e('.Lend:')
+    e('// @stampout')
     e('  s_endpgm')
     e(f'.Lfunc_end_{name}:')
     e(f'  .size {name}, .Lfunc_end_{name}-{name}')
     e('')
+    if "stamp" in DBG:
+        o = stamp_pass(o, waves)
     o.extend(_descriptor(name, LDSB, NVGPR, NSGPR, max_wg=64 * waves).splitlines())
     return "\n".join(o) + "\n"
+
+
+STAMP_PHASES = ['batch', 'ops', 'product', 'window', 'conv', 'stage', 'mfma1', 'norm', 'q3add', 'mfma2', 'remainder']
+
+
+def stamp_pass(o, waves):
+    """timing build (FTHE_GEN_NADICB_DBG=stamp, tools/nadicb_stamps.py): at every `// @phase` marker the
+    s_memtime ticks since the last one go to the accumulator of the phase that ran (s50, runtime: the op loop
+    jumps, so the textual order is not the running order; SGPR-relative s_movrels / s_movreld on M0); after the
+    last batch lane 0 writes 16 dwords per wave at kernarg rows[15] + 64 (waves wg + wave): the 11 sums, the
+    batches, the s_memrealtime of the first and the last stamp, 0, 0"""
+    ids = {ph: i for i, ph in enumerate(STAMP_PHASES)}
+    acc0 = 52
+    out = []
+
+    def stamp(new_id):
+        return ['  s_memtime s[48:49]', '  s_waitcnt lgkmcnt(0)', '  s_sub_u32 s51, s48, s46', '  s_mov_b32 m0, s50',
+                '  s_nop 0', f'  s_movrels_b32 s45, s{acc0}', '  s_add_u32 s51, s51, s45', f'  s_movreld_b32 s{acc0}, s51',
+                f'  s_mov_b32 s50, {new_id}', '  s_mov_b64 s[46:47], s[48:49]']
+    for line in o:
+        if line.startswith('// @phase'):
+            ph = line.split()[2]
+            out += stamp(ids[ph])
+            if ph == 'batch':
+                out.append('  s_add_u32 s64, s64, 1')
+            out.append(line)
+        elif line == '// @stampinit':
+            out += [f'  s_mov_b32 s{acc0 + i}, 0' for i in range(len(STAMP_PHASES))]
+            out += ['  s_mov_b32 s64, 0', f'  s_mov_b32 s50, {ids["batch"]}', '  s_memtime s[46:47]',
+                    '  s_memrealtime s[66:67]', '  s_waitcnt lgkmcnt(0)', '  v_readfirstlane_b32 s65, v0',
+                    '  s_lshr_b32 s65, s65, 6', f'  s_mul_i32 s44, s2, {waves}', '  s_add_u32 s65, s65, s44']
+        elif line == '// @stampout':
+            out += stamp(ids['batch'])
+            out += ['  s_memrealtime s[68:69]', '  s_load_dwordx2 s[70:71], s[0:1], 0xa0', '  s_waitcnt lgkmcnt(0)',
+                    '  s_cmp_eq_u64 s[70:71], 0', '  s_cbranch_scc1 .Lstamp_skip', '  s_mov_b64 exec, 1',
+                    '  s_lshl_b32 s44, s65, 6', '  v_mov_b32_e32 v1, s44']
+            for i in range(len(STAMP_PHASES)):
+                out += [f'  v_mov_b32_e32 v2, s{acc0 + i}', f'  global_store_dword v1, v2, s[70:71] offset:{4 * i}']
+            for i, sg in enumerate(('s64', 's66', 's68')):
+                out += [f'  v_mov_b32_e32 v2, {sg}',
+                        f'  global_store_dword v1, v2, s[70:71] offset:{4 * (len(STAMP_PHASES) + i)}']
+            out += ['  s_waitcnt vmcnt(0)', '.Lstamp_skip:']
+        else:
+            out.append(line)
+    return out
 
 
 if __name__ == "__main__":
