@@ -710,7 +710,8 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
 
     def normalise_chunks():
         """Every chunk at once: quad lane k normalises chunk k's groups (k = 0, 1: 32 groups, k = 2: 4; lane 3 has
-        none) with carry-in 0 -- one chain instead of three after each other -- and then the chunks' carries are
+        none) with carry-in 0 -- one chain instead of three after each other, itself split in two interleaved
+        halves joined like the chunks -- and then the chunks' carries are
         delivered: lane k + 1 adds lane k's carry-out to its lowest dword; the signed overflow of that add (rare:
         |carry| < 2^18 against a uniform dword) ripples through the lane's dwords on a slow path and changes its
         carry-out, which is delivered the same way until no lane receives one.  CR: every lane's final carry."""
@@ -721,34 +722,70 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e('  s_mov_b32 s34, 0x77777777')
         e('  s_mov_b32 s35, 0x77777777')
         e(f'  s_mov_b64 exec, {L012}')
-        e(f'  v_mov_b32_e32 v{CR}, 0')
-        cv = f"v{CR}"
+        # two chains per lane, interleaved: groups 0..15 (A) and 16..31 (B, carry-in 0) -- half the dependent
+        # v_mad_i64_i32 latency; A's carry then goes into B's lowest dword like the chunks' carries between lanes.
+        # Lane 2 (4 groups) runs B's first steps on don't-care rows; its dwords 16..19 are cleared after.
+        H = 16
+        chains = ((0, GB, FV), (H, AOP[0], ACC[0]))      # (first group, read double buffer, odd-step pair)
+        cvs = [None, None]
 
-        # two groups per ds_read_b128, two buffers: the read of groups g + 2, g + 3 is in flight while
-        # g, g + 1 are normalised (LDS returns in order: lgkmcnt(1) waits for the older read only)
-        def rd(g):
-            e(f'  ds_read_b128 {quad4(GB + 4 * ((g // 2) % 2))}, v{V_GR} offset:{8 * g}')
-        ng = 32
-        rd(0)
-        rd(2)
-        for g0 in range(0, ng, 2):
-            if g0 == sizes[2]:                           # lane 2's chunk ends: its carry stays in FV + 1
+        def rd(c, p):                                     # pair p (groups 2 p, 2 p + 1) of chain c
+            g0c, buf, _ = chains[c]
+            e(f'  ds_read_b128 {quad4(buf + 4 * (p % 2))}, v{V_GR} offset:{8 * (g0c + 2 * p)}')
+        npair = H // 2
+        for p in (0, 1):
+            rd(0, p)
+            rd(1, p)
+        for p in range(npair):
+            if 2 * p == sizes[2]:                         # lane 2's chunk ends: its carry stays in FV + 1
                 e(f'  s_mov_b64 exec, {L01}')
-            e(f'  s_waitcnt lgkmcnt({1 if g0 + 2 < ng else 0})')
-            for g in (g0, g0 + 1):
-                src = pair(GB + 4 * ((g0 // 2) % 2) + 2 * (g - g0))
-                if g % 2 == 0:
-                    e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cv}, 1, {src}')
-                    cv = f"v{DQ + g + 1}"
-                else:
-                    e(f'  v_mad_i64_i32 {pair(FV)}, vcc, {cv}, 1, {src}')
-                    e(f'  v_mov_b32_e32 v{DQ + g}, v{FV}')
-                    cv = f"v{FV + 1}"
-            if g0 + 4 < ng:
-                rd(g0 + 4)
-        assert cv == f"v{FV + 1}"
-        e(f'  s_mov_b64 exec, {L012}')
-        e(f'  v_mov_b32_e32 v{CR}, {cv}')                 # carry-outs with carry-in 0
+            e(f'  s_waitcnt lgkmcnt({2 if p + 1 < npair else 0})')
+            for h in (0, 1):                              # even group of A, of B, then the odd groups
+                for c in (0, 1):
+                    g0c, buf, fp = chains[c]
+                    g = g0c + 2 * p + h
+                    src = pair(buf + 4 * (p % 2) + 2 * h)
+                    cin = cvs[c] if cvs[c] else '0'
+                    if h == 0:
+                        e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cin}, 1, {src}' if cvs[c] else
+                          f'  v_mov_b64_e32 {pair(DQ + g)}, {src}')
+                        cvs[c] = f"v{DQ + g + 1}"
+                    else:
+                        e(f'  v_mad_i64_i32 {pair(fp)}, vcc, {cin}, 1, {src}')
+                        cvs[c] = f"v{fp + 1}"
+            for c in (0, 1):
+                g0c, _, fp = chains[c]
+                e(f'  v_mov_b32_e32 v{DQ + g0c + 2 * p + 1}, v{fp}')
+            if p + 2 < npair:
+                rd(0, p + 2)
+                rd(1, p + 2)
+        FB = chains[1][2]
+        assert cvs == [f"v{FV + 1}", f"v{FB + 1}"]
+        # lanes 0, 1: dword 16 += A's carry; the rare signed overflow ripples through dwords 17..31 into B's carry
+        TP = V_TMP
+        lab = f'.Lch{len(o)}'
+        e(f'  v_mov_b32_e32 v{TP}, v{DQ + H}')
+        e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+        e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{FV + 1}, 1, {pair(TP)}')
+        e(f'  v_mov_b32_e32 v{DQ + H}, v{TP}')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{TP + 1}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        e('  s_and_saveexec_b64 s[38:39], vcc')
+        for i in range(H + 1, 2 * H):
+            e(f'  v_mov_b32_e32 v{TP}, v{DQ + i}')
+            e(f'  v_mov_b32_e32 v{FV}, v{TP + 1}')
+            e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+            e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{FV}, 1, {pair(TP)}')
+            e(f'  v_mov_b32_e32 v{DQ + i}, v{TP}')
+        e(f'  v_add_u32_e32 v{FB + 1}, v{TP + 1}, v{FB + 1}')
+        e('  s_mov_b64 exec, s[38:39]')
+        e(f'{lab}_done:')
+        e(f'  v_mov_b32_e32 v{CR}, v{FB + 1}')            # lanes 0, 1: B's carry-out (exec is L01)
+        e('  s_mov_b64 exec, s[26:27]')
+        e(f'  v_mov_b32_e32 v{CR}, v{FV + 1}')            # lane 2: A's (its only chain); its dwords 16..19
+        e(f'  v_mov_b64_e32 {pair(DQ + H)}, 0')           # from B's first steps back to 0 (q3_1 is added to z2
+        e(f'  v_mov_b64_e32 {pair(DQ + H + 2)}, 0')       # dword by dword, lane 2 included)
         e('  s_mov_b64 exec, -1')
         # delivery: DL = the carries (or their changes) still to deliver, lane k -> lane k + 1 (k = 0, 1)
         DL, X, TP = GB, CR + 1, V_TMP
