@@ -37,7 +37,7 @@ from gen_montprog import _descriptor  # noqa: E402
 
 S, Q, B = 76, 19, 27
 MASK = (1 << B) - 1
-WAVES = 12
+WAVES = int(os.environ.get("FTHE_GEN_NADICB_WAVES", "12"))   # timing builds only (FTHE_GEN_*: never in-tree)
 CT_PER_WAVE = 16
 RB = 68                          # A-column row: 16 ciphertexts x 4 B + pad (gen_quad's QUAD_ROWB)
 ROWS = 2 * S                     # rows 0..75: y0 / x0 (then z1's retired limbs), 76..151: y1 (then z2's)
