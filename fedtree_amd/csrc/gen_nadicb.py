@@ -131,11 +131,14 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     # Barrett-phase plan (the product registers are dead): z dwords, MFMA operands, fold / norm scratch
     Z1B, Z2B = 14, 47                 # 33 dwords each (lane 3's dword 128 in local 32)
     BQ = 80                           # B operands, KB x 4 = v80..v99
-    ACC = (100, 104)                  # two accumulator sets
+    ACC = (100, 104)                  # two accumulator sets (the third of the MFMA phase: GB)
     AOP = (108, 112, 116, 120)        # four A-operand buffers (reads two MFMAs ahead, as gen_addb)
     DQ = 124                          # chunk dwords v124..v155 (the carry rides in DQ + g + 1 until g + 1 is done)
     GB = 156                          # group read buffers: 2 x (2 int64) = v156..v163, ds_read_b128 each
     PG = FV = 164                     # int64 pair (the fold's group; the normalisation's odd-group sum)
+    ACCS = ACC + (GB,) if "acc2" not in DBG else ACC   # MFMA accumulator sets (GB is free until the norm)
+    NACC = len(ACCS)
+    XDL_WAIT = 19                     # wait states after an MFMA before a VALU reads its result (as before)
     CR = 166                          # chunk carry
     NVGPR = 168
     assert T2B + 2 * NT <= V_AI[0] and V_A2X < NVGPR
@@ -671,15 +674,28 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 issue(('a', x), f'  ds_read_b128 {quad4(AOP[x % 4])}, v{A} offset:{off}')
 
             def read_corr(n, t):
-                issue(('c', n), f'  ds_read_b128 {quad4(ACC[n % 2])}, v{V_C} offset:{corr + 64 * t}')
+                issue(('c', n), f'  ds_read_b128 {quad4(ACCS[n % NACC])}, v{V_C} offset:{corr + 64 * t}')
 
             # A operands are read three MFMAs ahead into four buffers (the buffer re-filled after MFMA x is MFMA
             # x - 1's, whose operands were read at its issue); tile n - 1 is folded right after tile n's FIRST
             # MFMA (>= 18 wait states after tile n - 1's last: the MFMA and three s_nops), and tile n + 1's
             # corrections (its accumulators' srcC, the set tile n - 1 used) are read then, a whole tile ahead
-            read_corr(0, tiles[0])
-            if len(tiles) > 1:
-                read_corr(1, tiles[1])
+            # three accumulator sets: tile n - 2 is folded right after tile n's first MFMA, so its results have
+            # long been written (tile n - 1's MFMAs and reads in between) and the fold needs no s_nop padding
+            # unless the instructions since its last MFMA number under XDL_WAIT; tile n + 1's corrections (srcC,
+            # the set tile n - 2 used) are read right after that fold
+            last_mfma = {}
+
+            def settle(n):
+                """wait states before a VALU read of tile n's accumulators: one per instruction issued since"""
+                since = sum(1 for ln in o[last_mfma[n] + 1:] if ln.startswith('  '))
+                need = XDL_WAIT - since
+                while need > 0:
+                    e(f'  s_nop {min(need, 8) - 1}')
+                    need -= 8
+
+            for n in range(min(NACC, len(tiles))):
+                read_corr(n, tiles[n])
             for x in range(min(3, len(ops))):
                 read_a(x)
             for x, (n, t, kb) in enumerate(ops):
@@ -688,22 +704,21 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                     wait_for(('c', n))
                 wait_for(('a', x))
                 if "nomfma" not in DBG:
-                    e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACC[n % 2])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
-                      f'{quad4(ACC[n % 2])}')
+                    e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACCS[n % NACC])}, {quad4(AOP[x % 4])}, '
+                      f'{quad4(BQ + 4 * kb)}, {quad4(ACCS[n % NACC])}')
+                last_mfma[n] = len(o) - 1
                 if x + 3 < len(ops):
                     read_a(x + 3)
-                if first and n >= 1:
-                    e('  s_nop 7')
-                    e('  s_nop 7')
-                    e('  s_nop 3')
-                    fold_tile(ACC[(n - 1) % 2], stage_off(tiles[n - 1]))            # every chunk staged
-                    q.append(('w', n - 1))
-                    if n + 1 < len(tiles):
-                        read_corr(n + 1, tiles[n + 1])
-            e('  s_nop 7')
-            e('  s_nop 7')
-            e('  s_nop 7')
-            fold_tile(ACC[(len(tiles) - 1) % 2], stage_off(tiles[-1]))
+                if first and n >= NACC - 1:
+                    m = n - (NACC - 1)
+                    settle(m)
+                    fold_tile(ACCS[m % NACC], stage_off(tiles[m]))              # every chunk staged
+                    q.append(('w', m))
+                    if m + NACC < len(tiles):
+                        read_corr(m + NACC, tiles[m + NACC])
+            for m in range(max(0, len(tiles) - (NACC - 1)), len(tiles)):
+                settle(m)
+                fold_tile(ACCS[m % NACC], stage_off(tiles[m]))
         e('  s_waitcnt lgkmcnt(0)')
         if "nonorm" not in DBG:
             normalise_chunks()
