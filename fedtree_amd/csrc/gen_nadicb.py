@@ -644,12 +644,31 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 3}, s32, {pair(PG)}')
         e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{off}')
 
+    def mfma_consts(prod):
+        """A-copy base register, its K offset, the active K-blocks per tile, the corrections' offset"""
+        return ((V_A1, KO1, ACT1, 0) if prod == 1 else (V_A2, KO2, ACT2, CORR2_OFF - CORR1_OFF))
+
+    def first_reads(prod, issue):
+        """chunk 0's first corrections and A operands: constant image rows, independent of the staging, so the
+        stage issues them ahead of its own writes (preload) and their round trip overlaps the staging's"""
+        A, KO, act, corr = mfma_consts(prod)
+        tiles = CHUNKS[0]
+        ops = [(n, t, kb) for n, t in enumerate(tiles) for kb in act[t]]
+        for n in range(min(NACC, len(tiles))):
+            issue(('c', n), f'  ds_read_b128 {quad4(ACCS[n % NACC])}, v{V_C} offset:{corr + 64 * tiles[n]}')
+        for x in range(min(3, len(ops))):
+            n, t, kb = ops[x]
+            off = KO + 16 * (4 * kb - t)
+            assert 0 <= off and off + 64 <= COPY
+            issue(('a', x), f'  ds_read_b128 {quad4(AOP[x % 4])}, v{A} offset:{off}')
+
+    def preload(prod):
+        if "nopreload" not in DBG:
+            first_reads(prod, lambda tag, ins: e(ins))
+
     def mfma_product(prod):
         e(f'// @phase mfma{prod}')
-        A = V_A1 if prod == 1 else V_A2
-        KO = KO1 if prod == 1 else KO2
-        act = ACT1 if prod == 1 else ACT2
-        corr = 0 if prod == 1 else CORR2_OFF - CORR1_OFF
+        A, KO, act, corr = mfma_consts(prod)
         e(f'  v_mov_b32_e32 v{CR}, 0')
         for j, tiles in enumerate(CHUNKS):
             t0 = tiles[0]
@@ -677,10 +696,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                 issue(('c', n), f'  ds_read_b128 {quad4(ACCS[n % NACC])}, v{V_C} offset:{corr + 64 * t}')
 
             # A operands are read three MFMAs ahead into four buffers (the buffer re-filled after MFMA x is MFMA
-            # x - 1's, whose operands were read at its issue); tile n - 1 is folded right after tile n's FIRST
-            # MFMA (>= 18 wait states after tile n - 1's last: the MFMA and three s_nops), and tile n + 1's
-            # corrections (its accumulators' srcC, the set tile n - 1 used) are read then, a whole tile ahead
-            # three accumulator sets: tile n - 2 is folded right after tile n's first MFMA, so its results have
+            # x - 1's, whose operands were read at its issue).  Three accumulator sets: tile n - 2 is folded right after tile n's first MFMA, so its results have
             # long been written (tile n - 1's MFMAs and reads in between) and the fold needs no s_nop padding
             # unless the instructions since its last MFMA number under XDL_WAIT; tile n + 1's corrections (srcC,
             # the set tile n - 2 used) are read right after that fold
@@ -694,10 +710,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
                     e(f'  s_nop {min(need, 8) - 1}')
                     need -= 8
 
-            for n in range(min(NACC, len(tiles))):
-                read_corr(n, tiles[n])
-            for x in range(min(3, len(ops))):
-                read_a(x)
+            if j > 0 or "nopreload" in DBG:              # chunk 0's arrived with the stage (its lgkmcnt(0))
+                for n in range(min(NACC, len(tiles))):
+                    read_corr(n, tiles[n])
+                for x in range(min(3, len(ops))):
+                    read_a(x)
             for x, (n, t, kb) in enumerate(ops):
                 first = x == 0 or ops[x - 1][0] != n
                 if first:
@@ -845,6 +862,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         Lane k's local dword i is z dword 32 k + i -> position 32 k - 63 + i: lanes 2, 3 all of theirs (lane 3
         also local 32 = dword 128), lane 1 its local 31 (position 0)."""
         e('// @phase stage')
+        preload(1)
         t = zb                                                   # raw dwords: the B operands are XORed after the read
         e(f'  v_bfe_u32 v{V_TMP}, v{V_ROW}, 7, 2')
         e(f'  v_lshlrev_b32_e32 v{V_TMP}, 7, v{V_TMP}')
@@ -887,6 +905,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         """q3 dword d = N1 dword d + 1: lane k holds N1 dwords [32 k, 32 k + 32) in DQ -> positions 32 k - 1 + i
         (lane 0 from i = 1), raw; lane 2 sets positions 65..79 to 0x80 bytes, which read_b's XOR makes 0"""
         e('// @phase stage')
+        preload(2)
         e('  s_mov_b32 s34, 0x77777777')
         e('  s_mov_b32 s35, 0x77777777')
         e('  s_mov_b64 exec, s[34:35]')                                    # lanes 0..2
