@@ -670,8 +670,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e(f'// @phase mfma{prod}')
         A, KO, act, corr = mfma_consts(prod)
         e(f'  v_mov_b32_e32 v{CR}, 0')
-        for j, tiles in enumerate(CHUNKS):
-            t0 = tiles[0]
+        # all 17 tiles as one stream (the folds stage each tile's groups at its chunk's offset): no drain of the
+        # MFMA pipeline and no exposed operand round trip at the chunk boundaries (chunkloop: one loop per chunk)
+        for j, tiles in enumerate(CHUNKS if "chunkloop" in DBG else [tuple(t for ch in CHUNKS for t in ch)]):
             ops = [(n, t, kb) for n, t in enumerate(tiles) for kb in act[t]]
             q = []
 
