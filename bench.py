@@ -228,6 +228,92 @@ def cpu_baseline(a, pl, p1k, m, c, dev):
             "host": hc, "same_key_decrypts_on_gpu": same_key_ok, "ops": ops}
 
 
+def _sig(x, digits=4):
+    """x rounded to `digits` significant digits (floats only)."""
+    if isinstance(x, float) and x == x and x not in (float("inf"), float("-inf")) and x != 0:
+        from math import floor, log10
+        return round(x, max(0, digits - 1 - floor(log10(abs(x)))))
+    return x
+
+
+def _strip(o, drop):
+    if isinstance(o, dict):
+        return {k: _strip(v, drop) for k, v in o.items() if not drop(k)}
+    if isinstance(o, list):
+        return [_strip(v, drop) for v in o]
+    return _sig(o)
+
+
+LINE_MAX = 7000      # the driver keeps the tail of the line (~8.7 KB): the whole record must fit
+
+
+def compact_line(full):
+    """The stdout line: the full record without prose (notes, sources, host details -- DESIGN.md 4 explains the
+    fields) and with the tool outputs reduced to their rates, at most LINE_MAX bytes.  The full record goes to
+    FTHE_BENCH_DETAIL (default gpurun_out/bench_detail.json)."""
+    import re
+    pat = re.compile(r"note|_source$|^source$|^what$|^per_thread_per_s$|^survey_alg|^window_operand|"
+                     r"^kernel_share|^montmuls_per|^launches$|^avg_launch_ms$|_range$|^pmc_calibration$|"
+                     r"^pmc_launch_ms$|^pmc_kernel$|^pmc_algorithmic|^peak_GBps$|^bound$|^products_per_add$")
+    line = _strip(full, lambda k: bool(pat.search(k)))
+    for k, v in full.items():                            # the contract's own fields exactly as measured
+        if not isinstance(v, (dict, list)):
+            line[k] = v
+    line["roofline"] = _strip(full.get("roofline") or {}, lambda k: bool(re.search(r"note|^survey_alg|^window_operand", k)))
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        if k in (full.get("roofline") or {}):
+            line["roofline"][k] = full["roofline"][k]
+    cpu = line.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        host = (full.get("cpu_baseline") or {}).get("host") or {}
+        cpu.pop("host", None)
+        cpu["value"] = full["cpu_baseline"].get("value")
+        cpu["host_model"] = host.get("model")
+        cpu["sample"] = (full["cpu_baseline"].get("sample") or "")[:160]
+        if isinstance(cpu.get("ops"), dict):
+            cpu["ops"] = {k: v.get("per_s", v.get("adds_per_s")) for k, v in cpu["ops"].items() if isinstance(v, dict)}
+    sec = line.get("secondary") or {}
+    hl = sec.get("histogram_loop_unchanged_callers")
+    if isinstance(hl, dict):
+        sec["histogram_loop_unchanged_callers"] = {
+            t: ({"adds_per_s": v.get("ciphertext_adds_per_s"), "vs_reference_add": v.get("vs_reference_add"),
+                 "subs_per_s": (v.get("sub") or {}).get("ciphertext_subs_per_s"),
+                 "vs_reference_sub": (v.get("sub") or {}).get("vs_reference_sub"), "ok": v.get("ok")}
+                if isinstance(v, dict) and "error" not in v else v) for t, v in hl.items()}
+    hm = sec.get("host_marshalling_shards")
+    if isinstance(hm, dict) and isinstance(hm.get("shards"), list):
+        sec["host_marshalling_shards"] = {"round_trip_ok": hm.get("round_trip_ok"), "per_shards": {
+            str(x.get("shards")): [x.get("encrypt_side_per_s"), x.get("decrypt_side_per_s")] for x in hm["shards"]}}
+    ah = sec.get("p2048_add_hbm")
+    if isinstance(ah, dict):
+        sec["p2048_add_hbm"] = {k: ah[k] for k in ("algorithmic_GBps", "pmc_GBps_calibrated", "pmc_VALUBusy",
+                                                   "valu_frac_executed", "matrix_core") if k in ah}
+    for k in ("ghpair_e2e", "ghpair_e2e_sharded"):
+        if isinstance(sec.get(k), dict):
+            sec[k] = {x: sec[k][x] for x in ("encrypts_per_s", "decrypts_per_s", "ok", "shards", "error") if x in sec[k]}
+    if isinstance(sec.get("wire"), dict):
+        sec["wire"] = {k: v for k, v in sec["wire"].items() if k.endswith("_per_s") or k.endswith("_ok")
+                       or k.endswith("_host")}
+    text = json.dumps(line, separators=(",", ":"))
+    for k in ("wire", "host_marshalling_shards", "histogram_loop_unchanged_callers", "p1024_100k_pairs",
+              "fixed_base", "ghpair_operator_add", "concurrent_decrypt_gh"):
+        if len(text) <= LINE_MAX:
+            break
+        sec.pop(k, None)
+        text = json.dumps(line, separators=(",", ":"))
+    return text
+
+
+def write_detail(full):
+    path = os.environ.get("FTHE_BENCH_DETAIL") or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(json.dumps(full) + "\n")
+    except OSError as ex:
+        print(f"[bench] detail record not written: {ex}", file=sys.stderr)
+
+
 def main():
     a = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -398,9 +484,11 @@ def run(a, world):
     elapsed = max(p["elapsed_s"] for p in per_rank)
     enc_total = world * enc_rank
     value = enc_total / elapsed
-    na_rank = min(2 * P, 1 << 23)          # 8M adds per call (1M-add calls of ~1.4 ms disagreed by 10%)
+    # 8M adds per call (1M-add calls of ~1.4 ms disagreed by 10%); at most P, so the operands are always the two
+    # distinct halves c[:na], c[na:2na] (x = y would read half the bytes and inflate the rate)
+    na_rank = min(P, 1 << 23)
     add_out = torch.empty((na_rank, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
-    add_b = c[na_rank:2 * na_rank] if 2 * na_rank <= 2 * P else c[:na_rank]
+    add_b = c[na_rank:2 * na_rank]
 
     def _add_call():
         pl.add_dev(c[:na_rank], add_b, add_out)
@@ -514,12 +602,14 @@ def run(a, world):
     secondary = {}
     p1k_cpu = None
     if rank == 0 and world == 1 and not a.no_secondary:      # N=1 runs only: scaling runs stay lean
-        # CRT decrypt of 1M ciphertexts (config 3's decrypt half), device-resident
-        nd = min(2 * P, 1 << 20)
+        # CRT decrypt of every ciphertext the step produced (configs[2]'s decrypt half: 20M at 10M pairs),
+        # device-resident, one call
+        nd = 2 * P
         low = torch.empty(nd, dtype=torch.int64, device=f"cuda:{local}")
         pl.decrypt_u64_dev(c[:nd], low)
         dev.sync()
         secondary["crt_decrypt_per_s"] = round(nd / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        secondary["crt_decrypt_ciphertexts"] = nd
         ok = torch.equal(low, m[:nd])
         secondary["decrypt_roundtrip_ok"] = bool(ok)
         # opt-in short-plaintext decrypt (plaintext < p, true of every FedTree codec value): p half only
@@ -529,6 +619,7 @@ def run(a, world):
         secondary["decrypt_short_roundtrip_ok"] = bool(torch.equal(low, m[:nd]))
         # the same CRT encrypt with injected r (stage A r^Q mod P, then stage B): the path the golden,
         # random-vs-oracle and configs[1] tests pin bit-exactly; r < 2^(n_bits - 2) < n drawn by torch
+        low = low[:min(2 * P, 1 << 20)]
         nr = min(2 * P, 1 << 20)
         gen = torch.Generator(device=f"cuda:{local}").manual_seed(SEED + 5)
         rinj = torch.randint(-2**31, 2**31 - 1, (nr, pl.n_words), dtype=torch.int32, device=f"cuda:{local}",
@@ -788,13 +879,13 @@ def run(a, world):
                     "(128-bit exponent): 140 gathered products"}
         del cfb, lowfb, pko, kparty
         # ciphertext adds (x*y mod n^2, 4096-bit n^2 on the four-lane kernel), device-resident
-        na = min(2 * P, 1 << 23)                         # 8M adds per timed call (as ciphertext_adds)
+        na = na_rank                                     # 8M adds per timed call, distinct halves (as ciphertext_adds)
         o = torch.empty((na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
-        pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
+        pl.add_dev(c[:na], c[na:2 * na], o)
         dev.sync()
         add_ts = []
         for _ in range(5):                               # the median of 5 timed calls (one call: +-5%)
-            pl.add_dev(c[:na], c[na:2 * na] if 2 * na <= 2 * P else c[:na], o)
+            pl.add_dev(c[:na], c[na:2 * na], o)
             dev.sync()
             add_ts.append(lib.fthe_last_kernel_ms(dev.ctx) * 1e-3)
         add_s = sorted(add_ts)[2]
@@ -839,7 +930,7 @@ def run(a, world):
         # the same adds on Montgomery-resident rows (x R mod n^2, include/fthe.h): one product per add
         # instead of two; rows converted in/out once per chain (conversion not in this rate)
         mr = torch.empty((2 * na, 2 * pl.n_words), dtype=torch.int32, device=f"cuda:{local}")
-        src = c[:2 * na] if 2 * na <= 2 * P else torch.cat([c[:na], c[:na]])
+        src = c[:2 * na]
         pl.to_mont_dev(src, mr)
         pl.add_mont_dev(mr[:na], mr[na:], o)
         dev.sync()
@@ -1015,7 +1106,8 @@ def run(a, world):
             line["rehearsal"] = "FTHE_BENCH_REHEARSE=1: all ranks on cuda:0 over gloo; not a measurement"
         if cpu:
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
-        print(json.dumps(line), flush=True)
+        write_detail(line)
+        print(compact_line(line), flush=True)
     if world > 1:
         dist.barrier()                                 # the other ranks wait for rank 0's CPU stage
         dist.destroy_process_group()

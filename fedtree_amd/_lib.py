@@ -43,6 +43,7 @@ _I = ctypes.c_int
 _PROTOS = {
     "fthe_version": (_I, []),
     "fthe_strerror": (ctypes.c_char_p, [_I]),
+    "fthe_device_count": (_I, []),
     "fthe_ctx_create": (_I, [_I, _PP]),
     "fthe_ctx_destroy": (None, [_P]),
     "fthe_ctx_sync": (_I, [_P]),
@@ -73,6 +74,8 @@ _PROTOS = {
     "fthe_key_public_bases_info": (_I, [_P, _P, _P]),
     "fthe_encrypt_u64_dev": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_encrypt_u64": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _P, _I]),
+    "fthe_encrypt_u64_at_dev": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _U64, _P, _I]),
+    "fthe_encrypt_u64_at": (_I, [_P, _P, _P, _SZ, _P, _I, _U64, _U64, _P, _I]),
     "fthe_encrypt_words_dev": (_I, [_P, _P, _P, _I, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_encrypt_words": (_I, [_P, _P, _P, _I, _SZ, _P, _I, _U64, _P, _I]),
     "fthe_decrypt_dev": (_I, [_P, _P, _P, _SZ, _P, _P]),

@@ -518,6 +518,11 @@ extern "C" const char *fthe_strerror(int s) {
 
 extern "C" int fthe_kernel_limbs(int bits) { return kernel_limbs_for_bits(bits); }
 
+extern "C" int fthe_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0 ? n : 0;
+}
+
 extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
     if (!out) return FTHE_ERR_ARG;
     *out = nullptr;
@@ -1438,8 +1443,10 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
     static_assert(sizeof(args) == 168, "kernarg layout of gen_montprog.py");
     if (nrows > 16) return FTHE_ERR_ARG;
     for (int i = 0; i < nrows; i++) args.rows[i] = rows[i];
-    // timing builds only (FTHE_GEN_M37_AB=stamp, tools/m37_stamps.py): FTHE_STAMP_PTR = a device buffer of
-    // FTHE_STAMP_LAUNCHES x 128 KiB, one 128 KiB record area per launch in turn; other kernels ignore rows[15]
+#ifdef FTHE_STAMP_HOOK
+    // timing builds only (FTHE_GEN_M37_AB=stamp, tools/m37_stamps.py; compiled in for FTHE_BUILD_OUT libraries,
+    // never the in-tree one): FTHE_STAMP_PTR = a device buffer of FTHE_STAMP_LAUNCHES x 128 KiB, one 128 KiB
+    // record area per launch in turn
     static const char *stamp_ptr = getenv("FTHE_STAMP_PTR");
     static std::atomic<unsigned> stamp_launch{0};
     if (stamp_ptr && nrows < 16) {
@@ -1447,6 +1454,7 @@ int launch_montprog(fthe_ctx *c, void *slots, int S, int L, const void *prog, co
         const unsigned i = stamp_launch.fetch_add(1);
         if (i < nl) args.rows[15] = (const char *)(uintptr_t)strtoull(stamp_ptr, nullptr, 0) + (size_t)i * 131072;
     }
+#endif
     size_t sz = sizeof(args);
     void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     // programs without fixed-base table ops (the key's own) may take the MFMA-Barrett P-adic kernel
@@ -1603,12 +1611,13 @@ int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nsl
     if (k->device != c->device) return FTHE_ERR_ARG;
     if (!sh.S) return FTHE_ERR_UNSUPPORTED;
     HIPOK(hipSetDevice(c->device));
-    // L: a multiple of 768 ciphertexts -- the 256-thread glue grids and fthe_nadic_b76's workgroups of 192
-    // ciphertexts both cover the slots exactly
+    // L: a multiple of 256 ciphertexts (the 256-thread glue grids cover the slots exactly), and of 768 on a
+    // shape that may run fthe_nadic_b76, whose workgroups hold 192 ciphertexts (the public-key encrypt mod n^2)
+    const size_t q = (k->nadic_b && sh.S == k->sn2.S && sh.lanes == k->sn2.lanes) ? 768 : 256;
     size_t ch = (chunk ? chunk : chunk_lanes()) / (size_t)sh.lanes;    // same slot footprint per chunk
-    ch = (ch + 767) / 768 * 768;
-    size_t L = std::min(ch, (count + 767) / 768 * 768);
-    if (L == 0) L = 768;
+    ch = (ch + q - 1) / q * q;
+    size_t L = std::min(ch, (count + q - 1) / q * q);
+    if (L == 0) L = q;
     Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = sh.S; Lc.B = sh.B;
     int rc = c->slots.ensure((size_t)nslots * sh.S * L * 4);
     Lc.base = c->slots.p;
@@ -1790,6 +1799,9 @@ struct MsgSrc {
     const uint64_t *m64 = nullptr;
     const uint32_t *mw = nullptr;
     int mww = 0;
+    // index of m[0] in the caller's whole batch: device-drawn randomness (r == NULL) of plaintext i is the
+    // stream element idx0 + i, so the shards of a seeded batch (fthe_encrypt_u64_at) draw what one call would
+    uint64_t idx0 = 0;
     bool null() const { return !m64 && !mw; }
     // plaintexts [off, off + cnt) -> the IN1 slot (radix-2^B limbs); g^m = 1 + m n follows in the programs
     void pack(hipStream_t st, dim3 grid, size_t off, size_t cnt, uint32_t *slot, int S, int L, int B) const {
@@ -1902,9 +1914,9 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
             uint32_t *yp = (uint32_t *)c->scratch.p, *yq = yp + (size_t)L * k->pq_w;
             RngKey rq = rk; rq.nonce ^= kYqStream;                    // an independent stream for y_q
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords, k->pq_w, (int)k->p.bits(),
-                               rk, (uint64_t)off, cnt, yp);
+                               rk, m.idx0 + off, cnt, yp);
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords + k->pq_w, k->pq_w,
-                               (int)k->q.bits(), rq, (uint64_t)off, cnt, yq);
+                               (int)k->q.bits(), rq, m.idx0 + off, cnt, yq);
             m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
             pack_rows(c->stream, yp, k->pq_w, cnt, 0, Lc.slot(SL_T3), S, L, Lc.B);
             pack_rows(c->stream, yq, k->pq_w, cnt, 0, Lc.slot(SL_T4), S, L, Lc.B);
@@ -1969,7 +1981,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         }
         if (!r) {
             hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_nwords, nw, k->n_bits, rk,
-                               (uint64_t)off, cnt, (uint32_t *)c->scratch.p);
+                               m.idx0 + off, cnt, (uint32_t *)c->scratch.p);
             rw = (const uint32_t *)c->scratch.p; rwn = nw;
         }
         m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
@@ -2360,7 +2372,7 @@ static int encrypt_fb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
                                a_words, cnt, nwin, L, bpd, dig_p);
         } else {
             for (int sd = 0; sd < sides; sd++)
-                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, rk, (uint64_t)off, cnt, nwin, L,
+                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, rk, m.idx0 + off, cnt, nwin, L,
                                    bpd, sd, sd ? dig_q : dig_p);
         }
         m.pack(c->stream, Lc.grid(), off, cnt, Lc.slot(SL_IN1), S, L, Lc.B);
@@ -2859,7 +2871,7 @@ static int encrypt_pb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
             } else {
                 RngKey kb = rk;
                 kb.nonce += (uint64_t)(b + 1) << 56;                       // one stream per base
-                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, kb, (uint64_t)off, cnt, B.nwin[b],
+                hipLaunchKernelGGL(k_rng_digits, Lc.grid(), dim3(256), 0, c->stream, kb, m.idx0 + off, cnt, B.nwin[b],
                                    L, 2, 0, dst);
             }
         }
@@ -2924,7 +2936,7 @@ static int encrypt_xb_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, con
                     RngKey kb = rk;
                     kb.nonce += (uint64_t)(3 * side + b + 1) << 56;           // one stream per (prime, base)
                     hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords + side * pw, pw,
-                                       (int)(side ? k->q : k->p).bits(), kb, (uint64_t)off, cnt, ytmp);
+                                       (int)(side ? k->q : k->p).bits(), kb, m.idx0 + off, cnt, ytmp);
                     hipLaunchKernelGGL(k_alpha_digits, Lc.grid(), dim3(256), 0, c->stream, ytmp, pw, pw, cnt, X.nwin,
                                        L, 2, dst);
                 }
@@ -2950,6 +2962,12 @@ extern "C" int fthe_encrypt_u64_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m,
                                     const uint32_t *r, int r_words, uint64_t rng_seed,
                                     uint32_t *out, int flags) {
     MsgSrc ms; ms.m64 = m;
+    return encrypt_impl(k, c, ms, count, r, r_words, rng_seed, out, flags, nullptr);
+}
+
+extern "C" int fthe_encrypt_u64_at_dev(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
+                                       int r_words, uint64_t rng_seed, uint64_t index0, uint32_t *out, int flags) {
+    MsgSrc ms; ms.m64 = m; ms.idx0 = index0;
     return encrypt_impl(k, c, ms, count, r, r_words, rng_seed, out, flags, nullptr);
 }
 
@@ -3843,7 +3861,7 @@ struct HostIO {
 // Host-resident encrypt: inputs staged and outputs drained chunk by chunk through pinned buffers
 // (HostPipe); m is either u64 codec values or general plaintexts of mww words.
 static int encrypt_host(fthe_key *k, fthe_ctx *c, const void *m, int mww, size_t count, const uint32_t *r,
-                        int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
+                        int r_words, uint64_t rng_seed, uint32_t *out, int flags, uint64_t index0 = 0) {
     if (!k || !c || (!m && count) || (!out && count)) return FTHE_ERR_ARG;
     if (mww && (mww < 0 || mww > k->n_words)) return FTHE_ERR_ARG;
     if (r && (r_words <= 0 || r_words > ((flags & FTHE_ENC_FIXED_BASE_EXACT) ? 3 * (k->n_words + 2)
@@ -3860,6 +3878,7 @@ static int encrypt_host(fthe_key *k, fthe_ctx *c, const void *m, int mww, size_t
     pipe.add_out(out, c->io[2].p, cw * 4);
     MsgSrc ms;
     if (mww) { ms.mw = (const uint32_t *)c->io[0].p; ms.mww = mww; } else ms.m64 = (const uint64_t *)c->io[0].p;
+    ms.idx0 = index0;
     if ((rc = encrypt_impl(k, c, ms, count, r ? (const uint32_t *)c->io[1].p : nullptr, r_words,
                            rng_seed, (uint32_t *)c->io[2].p, flags, count ? &pipe : nullptr))) return rc;
     return pipe.finish();
@@ -3868,6 +3887,11 @@ static int encrypt_host(fthe_key *k, fthe_ctx *c, const void *m, int mww, size_t
 extern "C" int fthe_encrypt_u64(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
                                 int r_words, uint64_t rng_seed, uint32_t *out, int flags) {
     return encrypt_host(k, c, m, 0, count, r, r_words, rng_seed, out, flags);
+}
+
+extern "C" int fthe_encrypt_u64_at(fthe_key *k, fthe_ctx *c, const uint64_t *m, size_t count, const uint32_t *r,
+                                   int r_words, uint64_t rng_seed, uint64_t index0, uint32_t *out, int flags) {
+    return encrypt_host(k, c, m, 0, count, r, r_words, rng_seed, out, flags, index0);
 }
 
 extern "C" int fthe_encrypt_words(fthe_key *k, fthe_ctx *c, const uint32_t *m, int m_words, size_t count,

@@ -69,9 +69,9 @@ class ShardedPaillier:
     def encrypt_u64(self, m, seed=0, **modes):
         """modes: public / fixed_base / fixed_base_exact, as Paillier.encrypt_u64."""
         m = np.ascontiguousarray(m, dtype=np.uint64)
-        # distinct per-shard streams; seed 0 keeps the /dev/urandom default
-        parts = self._run(len(m), lambda k, lo, hi: k.encrypt_u64(
-            m[lo:hi], seed=(seed * 1315423911 + lo) if seed else 0, **modes))
+        # one stream for the whole batch, each shard at its own positions (index0 = lo): with a nonzero seed the
+        # shards give exactly the ciphertexts of one call; seed 0 draws each shard's key from /dev/urandom
+        parts = self._run(len(m), lambda k, lo, hi: k.encrypt_u64(m[lo:hi], seed=seed, index0=lo, **modes))
         return np.concatenate(parts) if parts else np.zeros((0, 2 * self.n_words), np.uint32)
 
     def decrypt_u64(self, c, short=False):

@@ -308,8 +308,10 @@ class Paillier:
                    "key_public_bases_info")
         return nb.value, [int(x) for x in ew[:nb.value]]
 
-    def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
+    def encrypt_u64(self, m, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False, index0=0):
         """c = g^m r^n mod n^2 for every m (paillier.cpp:134-137).
+        index0: m is the shard starting at element index0 of a larger batch (fthe_encrypt_u64_at): with a
+           nonzero seed its device-drawn randomness is that of the whole batch's call at those positions.
         r: None -> fresh uniform r per ciphertext from the device CSPRNG;
            else (count, n_words) uint32 words or a list of ints.
         fixed_base: r = h^alpha from the key's fixed-base tables (include/fthe.h);
@@ -338,9 +340,9 @@ class Paillier:
                 r = np.stack([_words(int(x), nw) for x in r]) if cnt else np.zeros((0, nw), np.uint32)
             rw = np.ascontiguousarray(r, dtype=np.uint32).reshape(cnt, -1)
         flags = self._flags(public, fixed_base, fixed_base_exact)
-        _lib.check(self.lib.fthe_encrypt_u64(self._key, self.dev.ctx, _ptr(m), cnt, _ptr(rw),
-                                             rw.shape[1] if rw is not None else 0, int(seed), _ptr(out), flags),
-                   "encrypt")
+        _lib.check(self.lib.fthe_encrypt_u64_at(self._key, self.dev.ctx, _ptr(m), cnt, _ptr(rw),
+                                                rw.shape[1] if rw is not None else 0, int(seed), int(index0),
+                                                _ptr(out), flags), "encrypt")
         return out
 
     def direct_y(self, seed, index0, count):
@@ -464,13 +466,14 @@ class Paillier:
 
     # ---- device-resident batch API (torch tensors on this device) -------------
     @_stream_ordered
-    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False):
+    def encrypt_u64_dev(self, m, out, r=None, seed=0, public=False, fixed_base=False, fixed_base_exact=False,
+                        index0=0):
         flags = self._flags(public, fixed_base, fixed_base_exact)
         rp = ctypes.c_void_p(r.data_ptr()) if r is not None else None
         rw = r.shape[-1] if r is not None else 0
-        _lib.check(self.lib.fthe_encrypt_u64_dev(self._key, self.dev.ctx, ctypes.c_void_p(m.data_ptr()), m.numel(),
-                                                 rp, rw, int(seed), ctypes.c_void_p(out.data_ptr()), flags),
-                   "encrypt_dev")
+        _lib.check(self.lib.fthe_encrypt_u64_at_dev(self._key, self.dev.ctx, ctypes.c_void_p(m.data_ptr()),
+                                                    m.numel(), rp, rw, int(seed), int(index0),
+                                                    ctypes.c_void_p(out.data_ptr()), flags), "encrypt_dev")
         return out
 
     @_stream_ordered

@@ -62,6 +62,10 @@ const char *fthe_strerror(int status);
  * written, so callers see one stream: fthe_ctx_sync / an event on
  * fthe_ctx_stream cover all of it.  Results are bit-identical whichever path
  * a batch size takes. */
+/* Visible gfx950 devices (0 without a GPU or HIP runtime).  The drop-in class shards its batch calls over
+ * them (integration/paillier_hip.h, FTHE_DEVICES), as the 8 GPUs of a node would take Server::encrypt_gh_pairs'
+ * batch (server.h:105-121) in independent contiguous shards. */
+int   fthe_device_count(void);
 int   fthe_ctx_create(int device, fthe_ctx **out);
 void  fthe_ctx_destroy(fthe_ctx *ctx);
 int   fthe_ctx_sync(fthe_ctx *ctx);
@@ -123,6 +127,17 @@ int fthe_encrypt_u64_dev(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t
 int fthe_encrypt_u64(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
                      const uint32_t *r, int r_words, uint64_t rng_seed,
                      uint32_t *c, int flags);
+/* A shard of a larger batch: plaintext i of this call is element index0 + i of the caller's whole batch.
+ * With device randomness (r == NULL) and a nonzero rng_seed, ciphertext i draws the randomness element
+ * index0 + i of that seed's stream, so contiguous shards encrypted on several contexts or devices give
+ * exactly the ciphertexts of one fthe_encrypt_u64 call over the whole batch (the multi-GPU drop-in,
+ * integration/paillier_hip.h).  index0 = 0 is fthe_encrypt_u64[_dev]. */
+int fthe_encrypt_u64_at_dev(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
+                            const uint32_t *r, int r_words, uint64_t rng_seed, uint64_t index0,
+                            uint32_t *c, int flags);
+int fthe_encrypt_u64_at(fthe_key *key, fthe_ctx *ctx, const uint64_t *m, size_t count,
+                        const uint32_t *r, int r_words, uint64_t rng_seed, uint64_t index0,
+                        uint32_t *c, int flags);
 /* General plaintexts (Paillier::encrypt(const ZZ&), paillier.cpp:122-139): m_words little-
  * endian words per plaintext (m_words <= n_words); otherwise as fthe_encrypt_u64.  Any m that
  * fits is encrypted exactly as PowerMod(g, m, n^2) r^n (g^m = 1 + m n mod n^2 for every m). */

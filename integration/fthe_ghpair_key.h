@@ -76,16 +76,47 @@ inline void check(int st, const char *what) {
     throw std::runtime_error(std::string(what) + ": " + fthe_strerror(st));
 #endif
 }
-// One engine context per host thread (the boundary is entered from OpenMP
-// regions, FLtrainer.cpp:275-306); device from FTHE_DEVICE (default 0).
-inline fthe_ctx *thread_ctx() {
-    static thread_local fthe_ctx *c = nullptr;
-    if (!c) {
-        const char *d = std::getenv("FTHE_DEVICE");
-        check(fthe_ctx_create(d ? std::atoi(d) : 0, &c), "fthe_ctx_create");
+// The devices the drop-in's batch calls shard over (integration/paillier_hip.h): FTHE_DEVICES, a comma list
+// ("0,1,2,3"; a device may repeat -- "0,0" runs two shards on device 0, the tests' two-context configuration),
+// else FTHE_DEVICE alone, else every visible device (fthe_device_count).  The first is the primary device: the
+// keys of keygen / operator=, the GHPair operators' engine work and the randomizer pool live there.
+inline std::vector<int> parse_devices(const char *e) {
+    std::vector<int> d;
+    for (const char *p = e; p && *p;) {
+        char *end = nullptr;
+        const long x = std::strtol(p, &end, 10);
+        if (end == p) throw std::runtime_error(std::string("FTHE_DEVICES: not a device list: ") + e);
+        d.push_back((int)x);
+        p = end;
+        while (*p == ',' || *p == ' ') p++;
     }
+    return d;
+}
+inline const std::vector<int> &shard_devices() {
+    static const std::vector<int> v = [] {
+        std::vector<int> d = parse_devices(std::getenv("FTHE_DEVICES"));
+        if (d.empty()) {
+            if (const char *e = std::getenv("FTHE_DEVICE")) d.push_back(std::atoi(e));
+            else for (int i = 0, n = fthe_device_count(); i < n; i++) d.push_back(i);
+        }
+        if (d.empty()) d.push_back(0);          // no device: the first context creation fails loudly
+        return d;
+    }();
+    return v;
+}
+inline int primary_device() { return shard_devices()[0]; }
+// The calling thread's engine context on device d, one per (thread, device), created on first use (the boundary
+// is entered from OpenMP regions, FLtrainer.cpp:275-306; a context serves one host thread at a time).
+inline fthe_ctx *ctx_on(int d) {
+    static thread_local std::vector<std::pair<int, fthe_ctx *>> cs;
+    for (auto &x : cs) if (x.first == d) return x.second;
+    fthe_ctx *c = nullptr;
+    check(fthe_ctx_create(d, &c), "fthe_ctx_create");
+    cs.emplace_back(d, c);
     return c;
 }
+// ... on the primary device.
+inline fthe_ctx *thread_ctx() { return ctx_on(primary_device()); }
 // mpz <-> little-endian u32 words (paillier_gpu.cu:7,18 order: mpz_export / mpz_import with order -1, size 4).
 // On a little-endian host with 64-bit limbs and no nails those words ARE the limbs' bytes, so the batch
 // marshalling copies limbs directly (memcpy + size) instead of GMP's generic word loop, which runs ~1.2M

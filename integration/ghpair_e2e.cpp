@@ -3,10 +3,13 @@
 // (integration/paillier_hip.h; Paillier_GPU::encrypt / decrypt, paillier_gpu.cu:211-313, 448-494), which
 // marshal every ciphertext between mpz_t and engine rows (mpz_import / mpz_export, as the reference does
 // at paillier_gpu.cu:240-258, 299-310) around one engine call with host buffers (PCIe both ways).
-//   ghpair_e2e [bits] [pairs] [reps]      -> one JSON line (best of reps; every plaintext checked)
+//   ghpair_e2e [bits] [pairs] [reps] [devices] -> one JSON line (best of reps; every plaintext checked)
+// devices: the FTHE_DEVICES list the batch calls shard over ("0,1,2,3"; "0,0" = two contexts on device 0), or a
+// count k for devices 0 .. k-1; default: the environment's (FTHE_DEVICES, else every visible GPU).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "paillier_hip.h"
@@ -16,6 +19,16 @@ int main(int argc, char **argv) {
     const size_t N = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 2000000;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 2;
     if (bits <= 0 || N == 0 || reps <= 0) return 2;
+    if (argc > 4) {                                   // before the first engine call reads the device list
+        std::string dl = argv[4];
+        if (dl.find(',') == std::string::npos) {
+            const int k = std::atoi(argv[4]);
+            if (k <= 0) return 2;
+            dl.clear();
+            for (int i = 0; i < k; i++) dl += (i ? "," : "") + std::to_string(i);
+        }
+        setenv("FTHE_DEVICES", dl.c_str(), 1);
+    }
     Paillier_HIP server;
     server.keygen(bits);
     std::vector<float> g0(N), h0(N);
@@ -47,9 +60,11 @@ int main(int argc, char **argv) {
             if (d[i].g != fthe_shim::decode(fthe_shim::encode(g0[i])) || d[i].h != fthe_shim::decode(fthe_shim::encode(h0[i])))
                 bad++;
     }
-    std::printf("{\"bits\": %d, \"pairs\": %zu, \"ciphertexts\": %zu, \"reps\": %d, \"encrypt_s\": %.4f, "
-                "\"decrypt_s\": %.4f, \"encrypts_per_s\": %.0f, \"decrypts_per_s\": %.0f, \"bad\": %d, \"ok\": %s}\n",
-                bits, N, 2 * N, reps, enc_best, dec_best, 2.0 * N / enc_best, 2.0 * N / dec_best, bad,
-                bad ? "false" : "true");
+    std::printf("{\"bits\": %d, \"pairs\": %zu, \"ciphertexts\": %zu, \"reps\": %d, \"shards\": %zu, "
+                "\"encrypt_s\": %.4f, \"decrypt_s\": %.4f, \"encrypts_per_s\": %.0f, \"decrypts_per_s\": %.0f, "
+                "\"bad\": %d, \"ok\": %s}\n",
+                bits, N, 2 * N, reps, fthe_shim::shard_plan(2 * N, fthe_shim::shard_devices().size(),
+                                                             fthe_shim::shard_min_rows()).size(),
+                enc_best, dec_best, 2.0 * N / enc_best, 2.0 * N / dec_best, bad, bad ? "false" : "true");
     return bad ? 1 : 0;
 }

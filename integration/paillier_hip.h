@@ -23,8 +23,13 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <exception>
+#include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -41,9 +46,9 @@ namespace fthe_shim {
 // per ciphertext; at the engine's rates it would otherwise dominate a batch call).  Small batches
 // stay on the calling thread, which may itself be one of FedTree's OpenMP workers.
 template <class F>
-inline void parallel_for(size_t n, F f) {
+inline void parallel_for(size_t n, F f, unsigned cap = 16) {
     const size_t grain = 1 << 16;
-    unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    unsigned nt = std::min<unsigned>(std::max(1u, cap), std::max(1u, std::thread::hardware_concurrency()));
     if (n < 2 * grain || nt < 2) { f(0, n); return; }
     nt = (unsigned)std::min<size_t>(nt, n / grain);
     std::vector<std::thread> th;
@@ -93,15 +98,23 @@ public:
     }
     void release(void *q) {
         if (!q) return;
-        std::lock_guard<std::mutex> lk(m_);
-        auto it = size_.find(q);
-        if (it == size_.end()) return;
-        free_.emplace_back(q, it->second);
-        cached_ += it->second;
-        size_.erase(it);
-        trim(cap_);
+        std::vector<void *> unpin;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            auto it = size_.find(q);
+            if (it == size_.end()) return;
+            free_.emplace_back(q, it->second);
+            cached_ += it->second;
+            size_.erase(it);
+            unpin = trim(cap_);
+        }
+        unpin_all(unpin);
     }
-    void drain(size_t keep) { std::lock_guard<std::mutex> lk(m_); trim(keep); }
+    void drain(size_t keep) {
+        std::vector<void *> unpin;
+        { std::lock_guard<std::mutex> lk(m_); unpin = trim(keep); }
+        unpin_all(unpin);
+    }
     size_t cached_bytes() { std::lock_guard<std::mutex> lk(m_); return cached_; }
 
 private:
@@ -109,15 +122,21 @@ private:
         const char *e = std::getenv("FTHE_SHIM_PINNED_CACHE_MB");
         cap_ = (size_t)(e ? std::atoll(e) : 4096) << 20;
     }
-    void trim(size_t keep) {                              // unpin the largest free buffers first
+    // Takes the largest free buffers out of the pool until at most `keep` bytes stay cached (under m_) and
+    // returns them; the caller unpins them after releasing m_ -- hipHostFree synchronises the device, and
+    // other threads' acquire / release must not wait behind it.
+    std::vector<void *> trim(size_t keep) {
+        std::vector<void *> out;
         while (cached_ > keep && !free_.empty()) {
             auto big = std::max_element(free_.begin(), free_.end(),
                                         [](const auto &a, const auto &b) { return a.second < b.second; });
-            fthe_host_free(big->first);
+            out.push_back(big->first);
             cached_ -= big->second;
             free_.erase(big);
         }
+        return out;
     }
+    static void unpin_all(const std::vector<void *> &v) { for (void *p : v) fthe_host_free(p); }
     std::mutex m_;
     std::vector<std::pair<void *, size_t>> free_;
     std::map<void *, size_t> size_;
@@ -137,6 +156,140 @@ struct Pinned {
 // codec of common.h:81-86 and paillier_gpu.cu:487
 inline uint64_t encode(float_type v) { long l = (long)(v * 1e6); return (uint64_t)l; }
 inline float_type decode(uint64_t m) { long l = (long)m; return (float_type)l / 1e6; }
+
+// ---- multi-device sharding of the batch calls ----------------------------------------------------------------
+// Ciphertexts are independent, so a batch of rows splits into contiguous shards, one per entry of
+// shard_devices() (north_star: batches "shard trivially across the 8 GPUs", per-GPU streams, no collective).
+// shard_plan: [lo, hi) of each shard for `rows` rows over at most `slots` shards of at least `min_rows` rows
+// (fewer shards for a small batch; balanced to +-1 row).  FTHE_SHARD_ROWS sets min_rows (default 8192).
+inline size_t shard_min_rows() {
+    static const size_t v = [] {
+        const char *e = std::getenv("FTHE_SHARD_ROWS");
+        const long long x = e ? std::atoll(e) : 8192;
+        return (size_t)std::max(1LL, x);
+    }();
+    return v;
+}
+inline std::vector<std::pair<size_t, size_t>> shard_plan(size_t rows, size_t slots, size_t min_rows) {
+    const size_t ns = std::max<size_t>(1, std::min(slots, rows / std::max<size_t>(1, min_rows)));
+    std::vector<std::pair<size_t, size_t>> v;
+    for (size_t i = 0; i < ns; i++) v.emplace_back(rows / ns * i + std::min(i, rows % ns),
+                                                     rows / ns * (i + 1) + std::min(i + 1, rows % ns));
+    return v;
+}
+// The same for segmented products: contiguous segment ranges of about equal member counts (ptr: nseg + 1 CSR
+// offsets), so each shard does about the same number of products.
+inline std::vector<std::pair<size_t, size_t>> shard_plan_segments(const int64_t *ptr, size_t nseg, size_t slots,
+                                                                  size_t min_members) {
+    const size_t tot = (size_t)(ptr[nseg] - ptr[0]);
+    const size_t ns = std::max<size_t>(1, std::min({slots, nseg, tot / std::max<size_t>(1, min_members)}));
+    std::vector<std::pair<size_t, size_t>> v;
+    size_t s = 0;
+    for (size_t i = 0; i < ns; i++) {
+        size_t e = s;
+        if (i + 1 == ns) e = nseg;
+        else {
+            const int64_t goal = ptr[0] + (int64_t)(tot * (i + 1) / ns);
+            while (e < nseg && ptr[e] < goal) e++;          // first boundary at or past the goal
+            e = std::max(e, s + 1);
+            e = std::min(e, nseg - (ns - 1 - i));             // leave a segment for every later shard
+        }
+        v.emplace_back(s, e);
+        s = e;
+    }
+    return v;
+}
+// One worker thread per shard slot beyond the first, each with its own engine context on its device (the
+// calling thread runs slot 0 on its own context on the primary device).  Jobs of one slot run in arrival order;
+// concurrent callers (FedTree's OpenMP threads) queue on the workers.  Joined at exit before the HIP runtime
+// tears down (the pool starts after it), like the randomizer pool's worker.
+class ShardPool {
+public:
+    static ShardPool &get() {
+        static ShardPool *p = [] {
+            auto *q = new ShardPool();
+            std::atexit([] { get().stop(); });
+            return q;
+        }();
+        return *p;
+    }
+    // f(slot, ctx) for slots 0 .. n-1 concurrently; returns when all are done, rethrowing the first error.
+    void run(size_t n, const std::function<void(size_t, fthe_ctx *)> &f) {
+        const std::vector<int> &devs = shard_devices();
+        if (n > devs.size()) throw std::runtime_error("ShardPool: more shards than devices");
+        struct Join { std::mutex m; std::condition_variable cv; size_t left; std::vector<std::exception_ptr> err; } j;
+        j.left = n - 1;
+        j.err.resize(n);
+        for (size_t i = 1; i < n; i++)
+            worker(i).push([&j, &f, i, d = devs[i]] {
+                try { f(i, ctx_on(d)); } catch (...) { j.err[i] = std::current_exception(); }
+                std::lock_guard<std::mutex> lk(j.m);
+                if (--j.left == 0) j.cv.notify_all();
+            });
+        try { f(0, ctx_on(devs[0])); } catch (...) { j.err[0] = std::current_exception(); }
+        {
+            std::unique_lock<std::mutex> lk(j.m);
+            j.cv.wait(lk, [&] { return j.left == 0; });
+        }
+        for (auto &e : j.err) if (e) std::rethrow_exception(e);
+    }
+
+private:
+    struct Worker {
+        std::mutex m;
+        std::condition_variable cv;
+        std::deque<std::function<void()>> q;
+        bool stopped = false;
+        std::thread th;
+        void push(std::function<void()> job) {
+            std::lock_guard<std::mutex> lk(m);
+            if (stopped) throw std::runtime_error("ShardPool: stopped");
+            q.push_back(std::move(job));
+            cv.notify_one();
+        }
+        void loop() {
+            for (;;) {
+                std::function<void()> job;
+                {
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [&] { return stopped || !q.empty(); });
+                    if (q.empty()) return;                 // stopped and drained
+                    job = std::move(q.front());
+                    q.pop_front();
+                }
+                job();
+            }
+        }
+    };
+    Worker &worker(size_t i) {
+        std::lock_guard<std::mutex> lk(m_);
+        if (w_.size() <= i) w_.resize(i + 1);
+        if (!w_[i]) {
+            w_[i].reset(new Worker());
+            Worker *w = w_[i].get();
+            w->th = std::thread([w] { w->loop(); });
+        }
+        return *w_[i];
+    }
+    void stop() {
+        std::lock_guard<std::mutex> lk(m_);
+        for (auto &w : w_) {
+            if (!w) continue;
+            { std::lock_guard<std::mutex> wl(w->m); w->stopped = true; w->cv.notify_one(); }
+            if (w->th.joinable()) w->th.join();
+        }
+    }
+    std::mutex m_;
+    std::vector<std::unique_ptr<Worker>> w_;
+};
+// The slot a single-shard call of this thread runs on: consecutive threads take consecutive devices, so
+// FedTree's OpenMP callers with small batches (Party::encrypt_histogram per party, FLtrainer.cpp:275-306)
+// spread over the node's GPUs instead of all landing on the primary one.
+inline size_t home_slot() {
+    static std::atomic<size_t> next{0};
+    static thread_local size_t mine = next.fetch_add(1);
+    return mine % shard_devices().size();
+}
 }  // namespace fthe_shim
 
 class Paillier_HIP {
@@ -226,75 +379,92 @@ public:
     // creation (keygen, key_from_primes, operator=), so there is nothing left to upload.
     void parameters_cpu_to_gpu() {}
 
-    // Paillier_GPU::encrypt(SyncArray<GHPair>&) (paillier_gpu.cu:211-313)
+    // ---- batch calls: sharded over shard_devices() ----------------------------------------------------------
+    // A batch of rows splits into contiguous shards (fthe_shim::shard_plan), one per device of FTHE_DEVICES (else
+    // every visible GPU): the calling thread runs the first, one worker thread per further device the others,
+    // each on its own engine context with this key's replica on that device (key_on), no collective.  Batches
+    // below two shards of FTHE_SHARD_ROWS run whole on the calling thread's home device (fthe_shim::home_slot).
+    // Results do not depend on the sharding: decrypt / add / products are deterministic, and a seeded encrypt
+    // (rng_seed) draws row i's randomness at position i of the whole batch (fthe_encrypt_u64_at).
+    // Deterministic device randomness for the batch encrypts (tests, benchmarks); 0: fresh keys from
+    // /dev/urandom per call and shard, the production setting.
+    uint64_t rng_seed = 0;
+
+    // Paillier_GPU::encrypt(SyncArray<GHPair>&) (paillier_gpu.cu:211-313): rows 0..n-1 are the pairs' g,
+    // rows n..2n-1 their h; each shard marshals, encrypts and unmarshals its own rows.
     void encrypt(SyncArray<GHPair> &message) {
         auto *d = message.host_data();
         size_t n = message.size();
         if (n == 0) return;
-        int nw = fthe_key_n_words(key()), cw = 2 * nw;
+        const int cw = 2 * fthe_key_n_words(key()), flags = eff_flags();
         fthe_shim::Pinned<uint64_t> mb(2 * n);
-        uint64_t *m = mb.get();
-        encode_pairs(d, n, m);
         fthe_shim::Pinned<uint32_t> cb(2 * n * (size_t)cw);
+        uint64_t *m = mb.get();
         uint32_t *c = cb.get();
-        fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m, 2 * n, nullptr, 0, 0, c,
-                                          eff_flags()), "encrypt");
-        rows_to_pairs(d, n, c, cw);
+        for_shards(2 * n, [&](fthe_ctx *ctx, fthe_key *k, size_t lo, size_t hi, unsigned nt) {
+            encode_rows(d, n, lo, hi, m, nt);
+            fthe_shim::check(fthe_encrypt_u64_at(k, ctx, m + lo, hi - lo, nullptr, 0, rng_seed, lo,
+                                                 c + lo * (size_t)cw, flags), "encrypt");
+            rows_to_fields(d, n, lo, hi, c, cw, nt);
+        });
     }
 
-    // The host marshalling of the batch calls, on up to 16 threads (integration/marshal_rate.cpp times it
-    // alone, for 1..8 concurrent shards: the host side of a multi-GPU server).
-    // encrypt: the codec of common.h:81-86 into plaintext words; the 2n result rows (g rows, then h rows)
-    // into the pairs' mpz fields (mpz_import, as paillier_gpu.cu:18).
-    static void encode_pairs(const GHPair *d, size_t n, uint64_t *m) {
-        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
-            for (size_t i = b; i < e; i++) { m[i] = fthe_shim::encode(d[i].g); m[n + i] = fthe_shim::encode(d[i].h); }
-        });
+    // The host marshalling of the batch calls (integration/marshal_rate.cpp times it alone, for 1..8 concurrent
+    // shards: the host side of a multi-GPU server), over rows [lo, hi) of the 2n:
+    // encrypt: the codec of common.h:81-86 into plaintext words; result rows into the pairs' mpz fields
+    // (mpz_import, as paillier_gpu.cu:18).
+    static void encode_rows(const GHPair *d, size_t n, size_t lo, size_t hi, uint64_t *m, unsigned nt = 16) {
+        fthe_shim::parallel_for(hi - lo, [&](size_t b, size_t e) {
+            for (size_t r = lo + b; r < lo + e; r++) m[r] = fthe_shim::encode(r < n ? d[r].g : d[r - n].h);
+        }, nt);
     }
-    static void rows_to_pairs(GHPair *d, size_t n, const uint32_t *c, int cw) {
-        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
-            for (size_t i = b; i < e; i++) {
-                fthe_shim::from_words(d[i].g_enc, &c[i * cw], cw);
-                fthe_shim::from_words(d[i].h_enc, &c[(n + i) * cw], cw);
-            }
-        });
+    static void rows_to_fields(GHPair *d, size_t n, size_t lo, size_t hi, const uint32_t *c, int cw, unsigned nt = 16) {
+        fthe_shim::parallel_for(hi - lo, [&](size_t b, size_t e) {
+            for (size_t r = lo + b; r < lo + e; r++)
+                fthe_shim::from_words(r < n ? d[r].g_enc : d[r - n].h_enc, &c[r * (size_t)cw], cw);
+        }, nt);
     }
     // decrypt: the pairs' mpz fields into rows (mpz_export, paillier_gpu.cu:7; unencrypted pairs: zero rows),
     // then the plaintexts' codec back into g, h
-    static void pairs_to_rows(const GHPair *d, size_t n, uint32_t *c, int cw) {
-        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {      // to_words throws only on oversize input
-            for (size_t i = b; i < e; i++) {
-                if (!d[i].encrypted) {                               // rows of unencrypted pairs: zeros
-                    std::fill(&c[i * cw], &c[(i + 1) * cw], 0u);
-                    std::fill(&c[(n + i) * cw], &c[(n + i + 1) * cw], 0u);
-                    continue;
-                }
-                fthe_shim::to_words(d[i].g_enc, &c[i * cw], cw);
-                fthe_shim::to_words(d[i].h_enc, &c[(n + i) * cw], cw);
+    static void fields_to_rows(const GHPair *d, size_t n, size_t lo, size_t hi, uint32_t *c, int cw, unsigned nt = 16) {
+        fthe_shim::parallel_for(hi - lo, [&](size_t b, size_t e) {  // to_words throws only on oversize input
+            for (size_t r = lo + b; r < lo + e; r++) {
+                const GHPair &p = d[r < n ? r : r - n];
+                if (!p.encrypted) std::fill(&c[r * (size_t)cw], &c[(r + 1) * (size_t)cw], 0u);
+                else fthe_shim::to_words(r < n ? p.g_enc : p.h_enc, &c[r * (size_t)cw], cw);
             }
-        });
+        }, nt);
     }
-    static void decode_pairs(GHPair *d, size_t n, const uint64_t *m) {
-        fthe_shim::parallel_for(n, [&](size_t b, size_t e) {
-            for (size_t i = b; i < e; i++)
-                if (d[i].encrypted) { d[i].g = fthe_shim::decode(m[i]); d[i].h = fthe_shim::decode(m[n + i]); }
-        });
+    static void decode_rows(GHPair *d, size_t n, size_t lo, size_t hi, const uint64_t *m, unsigned nt = 16) {
+        fthe_shim::parallel_for(hi - lo, [&](size_t b, size_t e) {
+            for (size_t r = lo + b; r < lo + e; r++) {
+                GHPair &p = d[r < n ? r : r - n];
+                if (p.encrypted) (r < n ? p.g : p.h) = fthe_shim::decode(m[r]);
+            }
+        }, nt);
     }
+    // whole-batch forms (marshal_rate.cpp)
+    static void encode_pairs(const GHPair *d, size_t n, uint64_t *m) { encode_rows(d, n, 0, 2 * n, m); }
+    static void rows_to_pairs(GHPair *d, size_t n, const uint32_t *c, int cw) { rows_to_fields(d, n, 0, 2 * n, c, cw); }
+    static void pairs_to_rows(const GHPair *d, size_t n, uint32_t *c, int cw) { fields_to_rows(d, n, 0, 2 * n, c, cw); }
+    static void decode_pairs(GHPair *d, size_t n, const uint64_t *m) { decode_rows(d, n, 0, 2 * n, m); }
 
     // Paillier_GPU::decrypt(SyncArray<GHPair>&) (paillier_gpu.cu:448-494)
     void decrypt(SyncArray<GHPair> &message) {
         auto *d = message.host_data();
         size_t n = message.size();
         if (n == 0) return;
-        int nw = fthe_key_n_words(key()), cw = 2 * nw;
+        const int cw = 2 * fthe_key_n_words(key());
         fthe_shim::Pinned<uint32_t> cb(2 * n * (size_t)cw);
-        uint32_t *c = cb.get();
-        pairs_to_rows(d, n, c, cw);
         fthe_shim::Pinned<uint64_t> mb(2 * n);
+        uint32_t *c = cb.get();
         uint64_t *m = mb.get();
-        fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(key(), fthe_shim::thread_ctx(), c,
-                                                                         2 * n, m, nullptr), "decrypt");
-        decode_pairs(d, n, m);
+        for_shards(2 * n, [&](fthe_ctx *ctx, fthe_key *k, size_t lo, size_t hi, unsigned nt) {
+            fields_to_rows(d, n, lo, hi, c, cw, nt);
+            fthe_shim::check((dec_short ? fthe_decrypt_short : fthe_decrypt)(k, ctx, c + lo * (size_t)cw, hi - lo,
+                                                                             m + lo, nullptr), "decrypt");
+            decode_rows(d, n, lo, hi, m, nt);
+        });
     }
 
     // Paillier_GPU::decrypt(GHPair&) (paillier_gpu.cu:497-542)
@@ -313,22 +483,23 @@ public:
     }
 
     // Paillier_GPU::add / mul (paillier_gpu.cu:57-68): single values, alias-safe, into an initialised
-    // result -- add on the host (one product, as the reference), mul through the key's shared queue.
+    // result -- both on the host (one product, and a 64-bit-exponent mpz_powm, as the reference GPU build).
     // Batch callers should use the helpers below or fthe_add / fthe_reduce_kway directly.
     void add(mpz_t &result, mpz_t &x, mpz_t &y) { paillier_cpu.add(result, x, y); }
     void mul(mpz_t result, mpz_t &x, mpz_t &y) { paillier_cpu.mul_into(result, x, y); }
 
     // ---- batch helpers for FedTree's HE call sites (not Paillier_GPU members) ----
-    // Each replaces a loop of per-pair GHPair operators (CPU GMP, ~11.5 us per add) with one engine call.
+    // Each replaces a loop of per-pair GHPair operators (CPU GMP, ~11.5 us per add) with one sharded engine call.
     // Unencrypted operands are encrypted first, as the operators promote them (common.h:156-160).
 
     // Histogram of one node (hist_tree_builder.cpp:565-595): hist[cut_col_ptr[f] + b] accumulates gh[i]
     // for each instance i whose feature f has bin b = dense_bin_id[i * n_col + f] (b == max_num_bin: a
     // missing value, skipped), in instance order: one segmented product over g and h
-    // (fthe_reduce_segments).  hist holds cut_col_ptr[n_col] entries; bins without instances are left
-    // untouched (unencrypted zero, like the reference's).  A populated bin is the product of its members;
-    // zero_first also folds a fresh Enc(0) into every populated bin, the reference's exact sequence (its
-    // first += promotes the unencrypted zero accumulator, common.h:156-160).
+    // (fthe_reduce_segments), sharded by bins of about equal member counts.  hist holds cut_col_ptr[n_col]
+    // entries; bins without instances are left untouched (unencrypted zero, like the reference's).  A
+    // populated bin is the product of its members; zero_first also folds a fresh Enc(0) into every populated
+    // bin, the reference's exact sequence (its first += promotes the unencrypted zero accumulator,
+    // common.h:156-160).
     void histogram(SyncArray<GHPair> &gh, const unsigned char *dense_bin_id, const int *cut_col_ptr, int n_col,
                    int max_num_bin, SyncArray<GHPair> &hist, bool zero_first = false) {
         const size_t n = gh.size(), nb = (size_t)cut_col_ptr[n_col];
@@ -351,20 +522,18 @@ public:
         for (int64_t t = 0; t < tot; t++) idx[tot + t] = idx[t] + (int64_t)n;
         const int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> x = rows(gh), out(2 * nb * (size_t)cw);
-        fthe_shim::check(fthe_reduce_segments(key(), fthe_shim::thread_ctx(), x.data(), 2 * n, ptr.data(), idx.data(),
-                                              2 * nb, out.data()), "histogram");
+        segments_rows(x.data(), 2 * n, ptr.data(), idx.data(), 2 * nb, out.data());
         if (zero_first) {                                        // Enc(0) * prod, populated bins only
             std::vector<size_t> pop;
             for (size_t s = 0; s < nb; s++) if (ptr[s + 1] > ptr[s]) pop.push_back(s);
             const size_t np = pop.size();
             std::vector<uint64_t> zero(2 * np, 0);
             std::vector<uint32_t> ez(2 * np * (size_t)cw), a(2 * np * (size_t)cw);
-            fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), zero.data(), 2 * np, nullptr, 0, 0,
-                                              ez.data(), eff_flags()), "histogram");
+            encrypt_rows(zero.data(), 2 * np, ez.data());
             for (size_t j = 0; j < np; j++)
                 for (int pl = 0; pl < 2; pl++)
                     std::copy(&out[(pl * nb + pop[j]) * cw], &out[(pl * nb + pop[j] + 1) * cw], &a[(pl * np + j) * cw]);
-            fthe_shim::check(fthe_add(key(), fthe_shim::thread_ctx(), a.data(), ez.data(), 2 * np, a.data()), "histogram");
+            add_rows(a.data(), ez.data(), 2 * np, a.data());
             for (size_t j = 0; j < np; j++)
                 for (int pl = 0; pl < 2; pl++)
                     std::copy(&a[(pl * np + j) * cw], &a[(pl * np + j + 1) * cw], &out[(pl * nb + pop[j]) * cw]);
@@ -377,8 +546,8 @@ public:
     }
 
     // k-party merge (hist_tree_builder.cpp:1015-1058): out[b] = prod_j parties[j][b] as one k-way product
-    // (fthe_reduce_kway).  zero_first: Enc(0) * prod_j ..., the reference's exact sequence (its zero
-    // accumulator's first += encrypts 0) at the price of one fresh encryption per entry;
+    // (fthe_reduce_kway), sharded by bins.  zero_first: Enc(0) * prod_j ..., the reference's exact sequence
+    // (its zero accumulator's first += encrypts 0) at the price of one fresh encryption per entry;
     // without it the plaintexts are the same and only the randomness differs.
     void merge(const std::vector<SyncArray<GHPair> *> &parties, SyncArray<GHPair> &out, bool zero_first = false) {
         const size_t z = zero_first ? 1 : 0, k = parties.size() + z, nb = out.size();
@@ -389,14 +558,13 @@ public:
         std::vector<uint32_t> x(k * 2 * nb * (size_t)cw), o(2 * nb * (size_t)cw);
         if (zero_first) {
             std::vector<uint64_t> zero(2 * nb, 0);
-            fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), zero.data(), 2 * nb, nullptr, 0, 0,
-                                              x.data(), eff_flags()), "merge");
+            encrypt_rows(zero.data(), 2 * nb, x.data());
         }
         for (size_t j = z; j < k; j++) {
             std::vector<uint32_t> r = rows(*parties[j - z]);
             std::copy(r.begin(), r.end(), x.begin() + j * 2 * nb * (size_t)cw);
         }
-        fthe_shim::check(fthe_reduce_kway(key(), fthe_shim::thread_ctx(), x.data(), (int)k, 2 * nb, o.data()), "merge");
+        kway_rows(x.data(), k, 2 * nb, o.data());
         auto *d = out.host_data();
         fthe_shim::parallel_for(nb, [&](size_t b, size_t e) {
             for (size_t i = b; i < e; i++) set_enc(d[i], &o[i * cw], &o[(nb + i) * cw], cw);
@@ -405,7 +573,7 @@ public:
 
     // Per-feature prefix sums of a histogram (inclusive_scan_by_key, hist_tree_builder.cpp:695-708), in
     // place: hist[t] = sum of hist[cut_col_ptr[f] .. t] within feature f, one segmented scan (g and h
-    // planes as segments of their own, fthe_scan_segments).
+    // planes as segments of their own, fthe_scan_segments), sharded by features.
     void prefix(SyncArray<GHPair> &hist, const int *cut_col_ptr, int n_col) {
         const size_t nb = (size_t)cut_col_ptr[n_col];
         if (hist.size() < nb) throw std::runtime_error("prefix: hist smaller than cut_col_ptr[n_col]");
@@ -414,8 +582,15 @@ public:
         for (int f = 0; f <= n_col; f++) seg[f] = cut_col_ptr[f];
         for (int f = 1; f <= n_col; f++) seg[n_col + f] = (int64_t)nb + cut_col_ptr[f];
         std::vector<uint32_t> x = rows_n(hist, nb), o(2 * nb * (size_t)cw);
-        fthe_shim::check(fthe_scan_segments(key(), fthe_shim::thread_ctx(), x.data(), seg.data(), 2 * (size_t)n_col,
-                                            o.data()), "prefix");
+        const size_t ns = 2 * (size_t)n_col;
+        auto plan = fthe_shim::shard_plan_segments(seg.data(), ns, fthe_shim::shard_devices().size(),
+                                                   fthe_shim::shard_min_rows());
+        run_plan(plan, [&](fthe_ctx *ctx, fthe_key *kk, size_t s0, size_t s1, unsigned) {
+            std::vector<int64_t> ls(seg.begin() + s0, seg.begin() + s1 + 1);
+            for (auto &v : ls) v -= seg[s0];
+            fthe_shim::check(fthe_scan_segments(kk, ctx, x.data() + seg[s0] * cw, ls.data(), s1 - s0,
+                                                o.data() + seg[s0] * cw), "prefix");
+        });
         auto *d = hist.host_data();
         fthe_shim::parallel_for(nb, [&](size_t lo, size_t hi) {
             for (size_t i = lo; i < hi; i++) set_enc(d[i], &o[i * cw], &o[(nb + i) * cw], cw);
@@ -429,11 +604,91 @@ public:
         if (b.size() != n || out.size() != n) throw std::runtime_error("subtract: sizes differ");
         const int cw = 2 * fthe_key_n_words(key());
         std::vector<uint32_t> xa = rows(a), xb = rows(b), o(2 * n * (size_t)cw);
-        fthe_shim::check(fthe_sub(key(), fthe_shim::thread_ctx(), xa.data(), xb.data(), 2 * n, o.data()), "subtract");
+        for_shards(2 * n, [&](fthe_ctx *ctx, fthe_key *k, size_t lo, size_t hi, unsigned) {
+            fthe_shim::check(fthe_sub(k, ctx, xa.data() + lo * cw, xb.data() + lo * cw, hi - lo, o.data() + lo * cw),
+                             "subtract");
+        });
         auto *d = out.host_data();
         fthe_shim::parallel_for(n, [&](size_t lo, size_t hi) {
             for (size_t i = lo; i < hi; i++) set_enc(d[i], &o[i * cw], &o[(n + i) * cw], cw);
         });
+    }
+
+    // ---- sharded engine calls on host rows (the helpers above; public for callers with rows in hand) ----
+    // c[i] = Enc(m[i]) (fthe_encrypt_u64_at with this object's enc_mode and rng_seed)
+    void encrypt_rows(const uint64_t *m, size_t count, uint32_t *c) {
+        const int cw = 2 * fthe_key_n_words(key()), flags = eff_flags();
+        for_shards(count, [&](fthe_ctx *ctx, fthe_key *k, size_t lo, size_t hi, unsigned) {
+            fthe_shim::check(fthe_encrypt_u64_at(k, ctx, m + lo, hi - lo, nullptr, 0, rng_seed, lo, c + lo * cw, flags),
+                             "encrypt");
+        });
+    }
+    // out[i] = a[i] b[i] mod n^2 (fthe_add; alias-safe)
+    void add_rows(const uint32_t *a, const uint32_t *b, size_t count, uint32_t *out) {
+        const int cw = 2 * fthe_key_n_words(key());
+        for_shards(count, [&](fthe_ctx *ctx, fthe_key *k, size_t lo, size_t hi, unsigned) {
+            fthe_shim::check(fthe_add(k, ctx, a + lo * cw, b + lo * cw, hi - lo, out + lo * cw), "add");
+        });
+    }
+    // out[i] = prod_j x[j * count + i] mod n^2 (fthe_reduce_kway); each shard gathers its k column blocks
+    void kway_rows(const uint32_t *x, size_t k, size_t count, uint32_t *out) {
+        const size_t cw = 2 * (size_t)fthe_key_n_words(key());
+        auto plan = fthe_shim::shard_plan(count, fthe_shim::shard_devices().size(), fthe_shim::shard_min_rows());
+        run_plan(plan, [&](fthe_ctx *ctx, fthe_key *kk, size_t lo, size_t hi, unsigned) {
+            const size_t cnt = hi - lo;
+            const uint32_t *src = x;
+            std::vector<uint32_t> local;
+            if (cnt != count) {                                  // this shard's rows of every party
+                local.resize(k * cnt * cw);
+                for (size_t j = 0; j < k; j++)
+                    std::copy(x + (j * count + lo) * cw, x + (j * count + hi) * cw, local.begin() + j * cnt * cw);
+                src = local.data();
+            }
+            fthe_shim::check(fthe_reduce_kway(kk, ctx, src, (int)k, cnt, out + lo * cw), "merge");
+        });
+    }
+    // out[s] = prod_{t in [ptr[s], ptr[s+1])} x[idx[t]] mod n^2 (fthe_reduce_segments; ptr[0] == 0): each shard
+    // takes a range of segments of about equal member counts, with all of x (the members are gathered by idx)
+    void segments_rows(const uint32_t *x, size_t count, const int64_t *ptr, const int64_t *idx, size_t nseg,
+                       uint32_t *out) {
+        const size_t cw = 2 * (size_t)fthe_key_n_words(key());
+        if (!nseg) return;
+        auto plan = fthe_shim::shard_plan_segments(ptr, nseg, fthe_shim::shard_devices().size(),
+                                                   fthe_shim::shard_min_rows());
+        run_plan(plan, [&](fthe_ctx *ctx, fthe_key *kk, size_t s0, size_t s1, unsigned) {
+            std::vector<int64_t> lp(ptr + s0, ptr + s1 + 1);
+            for (auto &v : lp) v -= ptr[s0];
+            fthe_shim::check(fthe_reduce_segments(kk, ctx, x, count, lp.data(), idx + ptr[s0], s1 - s0, out + s0 * cw),
+                             "histogram");
+        });
+    }
+
+    // This key on the device of context c: the key itself on the primary device, else its replica there, made on
+    // first use from p, q (key holder) or n and the published bases (public key) -- the same n, the same results.
+    fthe_key *key_on(fthe_ctx *c) {
+        const int dv = fthe_ctx_device(c);
+        fthe_key *k0 = key();
+        if (dv == fthe_shim::primary_device()) return k0;
+        std::lock_guard<std::mutex> lk(rep_mu_);
+        for (auto &r : replicas_) if (r.first == dv) return r.second.get();
+        const int nw = fthe_key_n_words(k0);
+        fthe_key *k = nullptr;
+        if (fthe_key_has_private(k0)) {
+            const int hw = (nw + 1) / 2;
+            std::vector<uint32_t> p(hw), q(hw);
+            fthe_shim::check(fthe_key_export(k0, nullptr, nullptr, nullptr, p.data(), q.data()), "export");
+            fthe_shim::check(fthe_key_from_primes(c, p.data(), q.data(), hw, &k), "key replica");
+        } else {
+            std::vector<uint32_t> n(nw);
+            fthe_shim::check(fthe_key_export(k0, n.data(), nullptr, nullptr, nullptr, nullptr), "export");
+            fthe_shim::check(fthe_key_from_n(c, n.data(), nw, &k), "key replica");
+        }
+        fthe_key_ref ref = fthe_key_adopt(k);
+        if (nbases_ && !fthe_key_has_private(k0))              // a party's published-bases tables (operator=)
+            fthe_shim::check(fthe_key_set_public_bases(k, c, bases_.data(), nbases_, base_bits_.data()),
+                             "set_public_bases");
+        replicas_.emplace_back(dv, ref);
+        return k;
     }
 
     uint32_t key_length;
@@ -447,6 +702,8 @@ public:
 
 private:
     fthe_key_ref key_;
+    std::mutex rep_mu_;
+    std::vector<std::pair<int, fthe_key_ref>> replicas_;   // (device, key) beyond the primary device
     std::vector<uint32_t> bases_;          // published fixed-base bases (nbases_ x 2 n_words words)
     std::vector<int> base_bits_;           // and the bits of each base's exponent
     int nbases_ = 0;
@@ -467,13 +724,36 @@ private:
         }
         return FTHE_ENC_DEFAULT;
     }
+    // f(ctx, key, lo, hi, marshalling threads) for each range of a plan: one range on the calling thread's home
+    // device, several on the shard pool (each range on its slot's device, with this key's replica there)
+    template <class F>
+    void run_plan(const std::vector<std::pair<size_t, size_t>> &plan, F f) {
+        if (plan.empty()) return;
+        const std::vector<int> &devs = fthe_shim::shard_devices();
+        if (plan.size() == 1) {
+            fthe_ctx *c = fthe_shim::ctx_on(devs[fthe_shim::home_slot()]);
+            f(c, key_on(c), plan[0].first, plan[0].second, 16u);
+            return;
+        }
+        const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned nt = std::max(1u, std::min(16u, hc / (unsigned)plan.size()));
+        fthe_shim::ShardPool::get().run(plan.size(), [&](size_t i, fthe_ctx *c) {
+            f(c, key_on(c), plan[i].first, plan[i].second, nt);
+        });
+    }
+    template <class F>
+    void for_shards(size_t rows, F f) {
+        run_plan(fthe_shim::shard_plan(rows, fthe_shim::shard_devices().size(), fthe_shim::shard_min_rows()), f);
+    }
     void reset_bases() { bases_.clear(); base_bits_.clear(); nbases_ = 0; }
+    void reset_replicas() { std::lock_guard<std::mutex> lk(rep_mu_); replicas_.clear(); }
     fthe_shim::KeyCell *owned_cell_ = nullptr;   // the cell whose randomizer pool this object keeps alive
     void disown() {
         if (owned_cell_) owned_cell_->release();
         owned_cell_ = nullptr;
     }
     void adopt(const fthe_key_ref &k) {
+        reset_replicas();
         key_ = k;
         paillier_cpu.bind(k, key_length);
         fthe_shim::KeyCell *c = paillier_cpu.cell();
@@ -508,8 +788,7 @@ private:
                 m[np + j] = fthe_shim::encode(d[plain[j]].h);
             }
             std::vector<uint32_t> c(2 * np * (size_t)cw);
-            fthe_shim::check(fthe_encrypt_u64(key(), fthe_shim::thread_ctx(), m.data(), 2 * np, nullptr, 0, 0, c.data(),
-                                              eff_flags()), "encrypt");
+            encrypt_rows(m.data(), 2 * np, c.data());
             for (size_t j = 0; j < np; j++) {
                 std::copy(&c[j * cw], &c[(j + 1) * cw], &x[plain[j] * cw]);
                 std::copy(&c[(np + j) * cw], &c[(np + j + 1) * cw], &x[(n + plain[j]) * cw]);
@@ -528,6 +807,7 @@ private:
     // public part of paillier_cpu and re-uploads it, paillier_gpu.h:32-37) and the published bases.
     void copy_public(const Paillier_HIP &o) {
         reset_bases();
+        reset_replicas();
         key_.reset();
         paillier_cpu = Paillier_HIP_Pub();
         if (!o.key_) { disown(); return; }

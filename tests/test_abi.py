@@ -55,6 +55,8 @@ def test_null_arguments_rejected():
     assert lib.fthe_ctx_create(0, None) == _lib.FTHE_ERR_ARG
     assert lib.fthe_key_generate(None, 1024, 0, None) == _lib.FTHE_ERR_ARG
     assert lib.fthe_encrypt_u64_dev(None, None, None, 0, None, 0, 0, None, 0) == _lib.FTHE_ERR_ARG
+    assert lib.fthe_encrypt_u64_at_dev(None, None, None, 0, None, 0, 0, 5, None, 0) == _lib.FTHE_ERR_ARG
+    assert lib.fthe_encrypt_u64_at(None, None, None, 0, None, 0, 0, 5, None, 0) == _lib.FTHE_ERR_ARG
     assert lib.fthe_decrypt_dev(None, None, None, 0, None, None) == _lib.FTHE_ERR_ARG
     assert lib.fthe_decrypt_shared(None, None, 0, None, None, 0) == _lib.FTHE_ERR_ARG
     assert lib.fthe_encrypt_shared(None, None, 0, None, 0) == _lib.FTHE_ERR_ARG
@@ -69,6 +71,7 @@ def test_no_gpu_fails_loudly():
     lib = _lib.load()
     ctx = ctypes.c_void_p()
     assert lib.fthe_ctx_create(0, ctypes.byref(ctx)) == _lib.FTHE_ERR_HIP
+    assert lib.fthe_device_count() == 0                      # the drop-in then has no shard to run on
     from fedtree_amd.paillier import Device
     with pytest.raises(_lib.FtheError):
         Device(0)

@@ -59,3 +59,28 @@ def test_failing_rank_fails_the_launch():
     and exits with rank 1's status instead of hanging."""
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--dry-run"], {"FTHE_BENCH_FAIL_RANK": "1"})
     assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+
+
+def test_compact_line_fits_the_driver_record():
+    """The stdout line drops prose and tool detail (written to FTHE_BENCH_DETAIL instead) and fits LINE_MAX bytes,
+    so the driver's kept tail holds the whole record -- with the aggregate ciphertext adds/s, the parties'
+    public-key encrypts/s and the CRT decrypts/s, checked on round 4's full 14 KB line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    full = json.loads(open(os.path.join(ROOT, "profiles", "r04ze_bench.json")).read().strip().splitlines()[-1])
+    assert len(json.dumps(full)) > 12000
+    text = bench.compact_line(full)
+    assert len(text) <= bench.LINE_MAX
+    line = json.loads(text)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert line[k] == full[k], k
+    assert line["ciphertext_adds"]["aggregate_adds_per_s"] == full["ciphertext_adds"]["aggregate_adds_per_s"]
+    assert line["secondary"]["public_encrypt_per_s"] == full["secondary"]["public_encrypt_per_s"]
+    assert line["secondary"]["crt_decrypt_per_s"] == full["secondary"]["crt_decrypt_per_s"]
+    r, fr = line["roofline"], full["roofline"]
+    assert (r["bound"], r["achieved"], r["peak"], r["unit"], r["frac"]) == \
+        (fr["bound"], fr["achieved"], fr["peak"], fr["unit"], fr["frac"])
+    cb = line["cpu_baseline"]
+    assert cb["value"] == full["cpu_baseline"]["value"] and cb["cores"] and cb["kind"] and cb["sample"]
+    assert "note" not in text

@@ -55,7 +55,11 @@ def test_use_hip_selects_the_engine_class_and_batch_branches(tmp_path):
     par = _cpp(d / FILES[1], "USE_HIP")
     assert "Paillier_HIP paillier;" in srv and "Paillier_HIP paillier;" in par
     assert "Paillier paillier;" not in srv and "Paillier_GPU paillier;" not in srv
-    for call in ("paillier.keygen();", "paillier.decrypt(gh);", "paillier.decrypt(encrypted);",
+    # homo_init(keylength) keeps FLParam.key_length (server.h:64-65 of the CPU build, NTL semantics: n of
+    # key_length bits, parser.cpp:50), not the USE_CUDA branch's argument-less keygen()
+    assert "paillier.keygen(keylength);" in srv and "paillier.keygen();" not in srv
+    assert re.search(r"void keygen\(int keyLength\)", open(os.path.join(ROOT, "integration", "paillier_hip.h")).read())
+    for call in ("paillier.decrypt(gh);", "paillier.decrypt(encrypted);",
                  "paillier.encrypt(raw);", "raw_data[i].paillier = paillier.paillier_cpu;"):
         assert call in srv, call
     assert "paillier.encrypt(hist);" in par and "hist_data[i].paillier = paillier.paillier_cpu;" in par

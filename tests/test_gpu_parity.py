@@ -305,6 +305,9 @@ def test_sharded_two_contexts(dev, coracle):
     m = np.random.default_rng(8).integers(0, 2**64, 10_001, dtype=np.uint64)
     c = sp.encrypt_u64(m, seed=4)
     assert c.shape == (len(m), 2 * pl.n_words)
+    # a seeded batch draws per position (fthe_encrypt_u64_at): the shards give the one-context ciphertexts
+    assert np.array_equal(c, pl.encrypt_u64(m, seed=4))
+    assert np.array_equal(sp.encrypt_u64(m[:999], seed=4, public=True), pl.encrypt_u64(m[:999], seed=4, public=True))
     assert np.array_equal(sp.decrypt_u64(c), m)
     assert np.array_equal(pl.decrypt_u64(c), m)
     s = sp.add_batch(c, c[::-1].copy())
@@ -317,6 +320,9 @@ def test_sharded_two_contexts(dev, coracle):
     cp = pub.encrypt_u64(m, seed=6, fixed_base_exact=True)
     assert np.array_equal(pl.decrypt_u64(cp), m)
     assert np.array_equal(pub.encrypt_u64(m, seed=6, fixed_base_exact=True), cp)
+    one = pl.public()
+    one.set_public_bases(pl.public_bases(seed=2))
+    assert np.array_equal(one.encrypt_u64(m, seed=6, fixed_base_exact=True), cp)
 
 
 # ---------------------------------------------------------------- segmented product / histogram

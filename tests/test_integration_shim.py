@@ -40,6 +40,8 @@ def test_shim_compiles_and_links(tmp_path):
     _build(str(tmp_path / "host_ops_test"), "host_ops_test.cpp", extra=("-fopenmp",))
     _build(str(tmp_path / "pool_test"), "pool_test.cpp", extra=("-fopenmp",))
     _build(str(tmp_path / "shim_refkeylen"), extra=("-DFTHE_REFERENCE_GPU_KEYLEN",))
+    _build(str(tmp_path / "multidev_test"), "multidev_test.cpp")
+    _build(str(tmp_path / "ghpair_e2e"), "ghpair_e2e.cpp", extra=("-fopenmp",))
 
 
 def test_default_key_length_is_2048_unless_reference_keylen_requested(tmp_path):
@@ -298,3 +300,68 @@ def test_marshalling_round_trip_and_shards(tmp_path):
     for bits in ("1024", "2016"):                                  # other row widths (edge rows self-checked)
         r = subprocess.run([exe, bits, "777", "1", "1"], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0 and json.loads(r.stdout.strip().splitlines()[-1])["round_trip_ok"], r.stderr
+
+
+def test_shard_plan_arithmetic(tmp_path):
+    """The drop-in's shard arithmetic (fthe_shim::shard_plan / shard_plan_segments, no GPU): configs[4]'s 80M
+    pairs (160M rows) over 8 devices are 8 contiguous shards of 20M rows; random sizes are covered contiguously,
+    balanced to +-1 row with at least FTHE_SHARD_ROWS per shard; segment plans of random and skewed CSRs are
+    contiguous, non-empty and balanced by member count."""
+    import json
+    exe = str(tmp_path / "multidev_test")
+    _build(exe, "multidev_test.cpp")
+    r = subprocess.run([exe, "plan"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["plan_ok"] and out["config4_shard_rows"] == 20_000_000
+
+
+def test_device_list_parsing(tmp_path):
+    """FTHE_DEVICES is parsed before any engine call (no GPU): a list, repeats allowed; garbage is an error."""
+    src = tmp_path / "dl.cpp"
+    src.write_text('#include "paillier_hip.h"\n#include <cstdio>\nint main(int c, char **v) {\n'
+                   '  for (int d : fthe_shim::parse_devices(v[1])) std::printf("%d ", d);\n  return 0; }\n')
+    exe = str(tmp_path / "dl")
+    _build(exe, str(src))
+    for arg, want in (("0,1,2,3", "0 1 2 3"), ("0,0", "0 0"), ("5", "5"), ("1, 3", "1 3")):
+        r = subprocess.run([exe, arg], capture_output=True, text=True, timeout=30)
+        assert r.returncode == 0 and r.stdout.strip() == want, (arg, r.stdout, r.stderr)
+    r = subprocess.run([exe, "a,b"], capture_output=True, text=True, timeout=30)
+    assert r.returncode != 0 and "not a device list" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ref_gmp_L2048.json"])
+def test_sharded_drop_in_identical_to_one_context(tmp_path, name):
+    """Paillier_HIP's batch calls sharded over two and three contexts on device 0 (FTHE_DEVICES=0,0 / 0,0,0, small
+    FTHE_SHARD_ROWS so 3,000 pairs split) give byte-identical ciphertexts to the one-context run for the seeded
+    key holder's and party's encrypts (default and published-bases exact), the zero-first histogram, the zero-first
+    3-party merge, subtract, prefix and the large merge / subtract; every decrypt is checked against the codec
+    values (server.h:58-135, party.h:118-142, paillier_gpu.cu:211-313, 448-494)."""
+    g = load_golden(name)
+    p, q = golden_key(g)
+    exe = str(tmp_path / "multidev_test")
+    _build(exe, "multidev_test.cpp")
+    outs = {}
+    for devs in ("0", "0,0", "0,0,0"):
+        env = dict(os.environ, FTHE_DEVICES=devs, FTHE_SHARD_ROWS="256")
+        r = subprocess.run([exe, "run", f"{p:x}", f"{q:x}", "3000"], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0 and "multidev OK" in r.stdout, devs + ": " + r.stdout[-3000:] + r.stderr[-3000:]
+        lines = r.stdout.strip().splitlines()
+        assert f"devices {len(devs.split(','))}" in lines
+        outs[devs] = [ln for ln in lines if not ln.startswith("devices")]
+    assert outs["0,0"] == outs["0"] and outs["0,0,0"] == outs["0"], outs
+
+
+@pytest.mark.gpu
+def test_ghpair_e2e_two_shards(tmp_path):
+    """ghpair_e2e (Server::encrypt_gh_pairs / decrypt_gh_pairs at FedTree's types) with its batch split over two
+    contexts on device 0: every plaintext round-trips."""
+    import json
+    exe = str(tmp_path / "ghpair_e2e")
+    _build(exe, "ghpair_e2e.cpp", extra=("-fopenmp",))
+    r = subprocess.run([exe, "2048", "20000", "1", "0,0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"] and out["shards"] == 2
