@@ -152,6 +152,17 @@ size_t dec_split_lanes() {
     return v;
 }
 
+// Large CRT encrypts / decrypts with both halves on two streams as well (each chunk's p and q launches share the
+// chip, so one launch's tail of finishing waves overlaps the other's instead of idling SIMDs); 0 keeps the halves
+// in turn on one stream.  FTHE_SPLIT_ALL overrides (A/B).
+bool split_all() {
+    static const bool v = [] {
+        const char *e = getenv("FTHE_SPLIT_ALL");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
 // Decrypts of at most this many ciphertexts take the four-lane s80 kernel (Paillier-2048 keys);
 // FTHE_DEC_QUAD overrides, 0 turns it off (A/B).
 size_t dec_quad_max() {
@@ -1841,11 +1852,13 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     // and smaller ones both halves on the four-lane s80 kernel (as decrypt_impl)
     // (one chunk by construction: FTHE_CHUNK below the quad limit sends the batch down the other paths)
     const bool quad = direct_y && k->slat.S && count > 0 && count <= dec_quad_max() && count <= chunk_lanes();
-    const bool split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    const bool small_split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    const bool big_split = !quad && !small_split && direct_y && vi >= 0 && split_all();
+    const bool split = small_split || big_split;
     const int nsl = nslots_for(k);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2,
-                        direct_y && !split && !quad ? enc_chunk_lanes() : !crt && k->nadic_b ? pub_chunk_lanes() : 0);
+                        direct_y && !small_split && !quad ? enc_chunk_lanes() : !crt && k->nadic_b ? pub_chunk_lanes() : 0);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     // Device-drawn randomness under CRT draws y_p, y_q uniform in [1,p), [1,q) and
@@ -2991,7 +3004,8 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
     // hand c^(P-1) mod P^2 back to the s74 layout for the unchanged L-function / CRT tail.
     const int vi = variant_index(k->spq.S);
     const bool quad = k->slat.S && count > 0 && count <= dec_quad_max() && count <= chunk_lanes();
-    const bool split = !quad && !short_pt && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    const bool split = !quad && !short_pt && vi >= 0 &&
+                       (count * (size_t)kVariants[vi].lanes <= dec_split_lanes() || split_all());
     const int nsl = nslots_for(k);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, k->spq);

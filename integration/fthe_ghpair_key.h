@@ -18,8 +18,9 @@
 //              the key holder's CRT path or the public formula) on a background thread, so a
 //              promotion (common.h:156-160) costs one host product instead of an
 //              exponentiation.  Every pooled rho is used exactly once.
-//   mul     -> fthe_scalar_mul_u64_shared (64 squarings of 4096 bits; concurrent callers merged into
-//              one launch), fthe_scalar_mul_words for exponents above 64 bits.
+//   mul     -> a host mpz_powm for exponents of at most 64 bits (operator-'s 2^64 - 1), as the reference GPU
+//              build's Paillier_GPU::mul (paillier_gpu.cu:65-67); FTHE_SHIM_MUL_ENGINE=1 sends them to
+//              fthe_scalar_mul_u64_shared instead (A/B); fthe_scalar_mul_words for exponents above 64 bits.
 // The batch call sites go to the engine directly (Paillier_HIP's helpers, include/fthe.h).
 //
 // Copies are free of atomics: a key is an interned, immutable host cell (n, n^2, g limbs; the pool),

@@ -98,7 +98,7 @@ int main(int argc, char **argv) {
     Paillier_HIP server;                                     // Server::paillier, the key holder
     server.key_from_primes(p, q);
     server.rng_seed = 1234;
-    server.publish_bases();
+    server.publish_bases(77);                               // deterministic bases: runs comparable
     Paillier_HIP party;                                      // Party::paillier (Server::send_key, operator=)
     party = server;
     party.rng_seed = 5678;

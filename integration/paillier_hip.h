@@ -344,12 +344,13 @@ public:
     // Parties that receive this key by operator= build their tables from them, and their
     // encrypt() with enc_mode = FixedBaseExact (Party::encrypt_histogram) then draws r^n from the
     // tables (within 3 * 2^-64 of the reference's distribution).  Not in the reference.
-    void publish_bases() {
+    // seed 0 (production): the bases' generators from /dev/urandom; nonzero: deterministic (tests).
+    void publish_bases(uint64_t seed = 0) {
         int nb = 0;
-        fthe_shim::check(fthe_key_public_bases(key(), 0, nullptr, &nb, nullptr), "public_bases");
+        fthe_shim::check(fthe_key_public_bases(key(), seed, nullptr, &nb, nullptr), "public_bases");
         bases_.assign((size_t)nb * 2 * fthe_key_n_words(key()), 0);
         base_bits_.assign(nb, 0);
-        fthe_shim::check(fthe_key_public_bases(key(), 0, bases_.data(), &nb, base_bits_.data()), "public_bases");
+        fthe_shim::check(fthe_key_public_bases(key(), seed, bases_.data(), &nb, base_bits_.data()), "public_bases");
         nbases_ = nb;
     }
 
