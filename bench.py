@@ -473,6 +473,8 @@ def run(a, world):
     _lib.check(lib.fthe_prof_read(dev.ctx, ctypes.byref(kms), ctypes.byref(launches), ctypes.byref(lane_mm),
                                   ctypes.byref(lanes), ctypes.byref(ems), ctypes.byref(elaunch),
                                   ctypes.byref(amacs)))
+    busy, ebusy = ctypes.c_double(), ctypes.c_double()
+    _lib.check(lib.fthe_prof_busy(dev.ctx, ctypes.byref(busy), ctypes.byref(ebusy)), "prof_busy")
     lib.fthe_prof_enable(dev.ctx, 0)
     enc_rank = 2 * P * a.steps
     ident.update({"elapsed_s": round(elapsed_rank, 4), "encrypts_per_s": round(enc_rank / elapsed_rank, 1)})
@@ -503,15 +505,22 @@ def run(a, world):
     # executed algorithm, accumulated per launch by the engine: W(s) = 2 s^2 + s per Montgomery
     # product on s = 32-bit words of the modulus (SURVEY.md 8(d) unit), and the P-adic kernel's
     # own count per squaring / product mod P^2 (fthe.hip padic_alg: digit products + Barretts).
+    # the p and q launches of a chunk run side by side on the engine's two compute streams (fthe.hip split_all):
+    # kernel time is the union of the launch intervals (fthe_prof_busy), not their sum, which counts the shared
+    # time twice; per launch, avg_expo_launch_ms is that union over the launches (the effective time per launch)
+    # and avg_expo_launch_ms_in_flight the HIP-event duration of one launch beside its partner (what rocprof's
+    # kernel trace reports per dispatch)
     alg_macs = amacs.value
-    k_s = kms.value * 1e-3
+    k_s = busy.value * 1e-3
     achieved = alg_macs / k_s / 1e12
     roof = {"bound": "valu", "kernel": "", "achieved": round(achieved, 3),
             "peak": round(PEAK_MAC_S / 1e12, 3), "unit": "TMAC/s", "frac": round(achieved * 1e12 / PEAK_MAC_S, 4),
             "traffic": None,
-            "launches": int(launches.value), "avg_launch_ms": round(kms.value / max(1, launches.value), 3),
+            "launches": int(launches.value), "avg_launch_ms": round(busy.value / max(1, launches.value), 3),
             "expo_launches": int(elaunch.value),
-            "avg_expo_launch_ms": round(ems.value / max(1, elaunch.value), 3),
+            "avg_expo_launch_ms": round(ebusy.value / max(1, elaunch.value), 3),
+            "avg_expo_launch_ms_in_flight": round(ems.value / max(1, elaunch.value), 3),
+            "expo_launches_overlap": round(ems.value / max(1e-9, ebusy.value), 3),
             "avg_expo_launch_ms_by_kernel": {},
             "alg_macs_per_encrypt": round(alg_macs / enc_rank),
             "survey_alg_macs_per_crt_encrypt_direct": ALG_MACS_PER_CRT_ENC,
@@ -567,7 +576,8 @@ def run(a, world):
         roof["traffic"] = pmc.get("enc", {}).get(expo_kernel, {}).get("hbm_bytes_per_launch")
         roof["traffic_source"] = f"profiles/{PMC_FILE} ({expo_kernel} full-chunk launch)"
         ek = pmc.get("enc", {}).get(expo_kernel, {})
-        kms_expo = roof["avg_expo_launch_ms_by_kernel"].get(expo_kernel) or roof["avg_expo_launch_ms"]
+        # the effective time per launch (the union), as the counters are per launch over the whole chip
+        kms_expo = roof["avg_expo_launch_ms"]
         simd_cycles = 1024 * 2.4e9 * kms_expo * 1e-3     # every SIMD's cycles over the live launch time
         if ek.get("SQ_INSTS_VALU") and kms_expo:
             # executed issue: the kernel's VALU wave-instructions (PMC, per launch) x 4 cycles (a wave64

@@ -125,6 +125,7 @@ _PROTOS = {
     "fthe_prof_variant": (_I, [_P, _I, _P, _P]),
     "fthe_prof_exec_macs": (_I, [_P, _P]),
     "fthe_prof_read": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "fthe_prof_busy": (_I, [_P, _P, _P]),
 }
 
 

@@ -482,6 +482,10 @@ int    fthe_prof_enable(fthe_ctx *ctx, int on);
 int    fthe_prof_read(fthe_ctx *ctx, double *kernel_ms, double *launches,
                       double *lane_montmuls, double *lanes,
                       double *expo_ms, double *expo_launches, double *alg_macs);
+/* The union of the launch intervals of the last fthe_prof_read window (time with at least one launch running,
+ * all launches / exponentiation launches): launches on the context's two compute streams overlap when a large
+ * CRT encrypt or decrypt runs its p and q halves side by side, so summed durations then count that time twice. */
+int    fthe_prof_busy(fthe_ctx *ctx, double *busy_ms, double *expo_busy_ms);
 /* Per kernel variant (limb count S: 37, 74, 152, 80; 1037 = the P-adic kernel mod
  * p^2 / q^2) exponentiation-launch time and count of the last fthe_prof_read window. */
 int    fthe_prof_variant(fthe_ctx *ctx, int S, double *expo_ms, double *expo_launches);

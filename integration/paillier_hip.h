@@ -666,10 +666,12 @@ public:
 
     // This key on the device of context c: the key itself on the primary device, else its replica there, made on
     // first use from p, q (key holder) or n and the published bases (public key) -- the same n, the same results.
+    // FTHE_SHIM_REPLICATE=1 (tests): replicas on the primary device too, so a one-GPU box runs the replica path.
     fthe_key *key_on(fthe_ctx *c) {
+        static const bool force = [] { const char *e = std::getenv("FTHE_SHIM_REPLICATE"); return e && *e == '1'; }();
         const int dv = fthe_ctx_device(c);
         fthe_key *k0 = key();
-        if (dv == fthe_shim::primary_device()) return k0;
+        if (dv == fthe_shim::primary_device() && !force) return k0;
         std::lock_guard<std::mutex> lk(rep_mu_);
         for (auto &r : replicas_) if (r.first == dv) return r.second.get();
         const int nw = fthe_key_n_words(k0);

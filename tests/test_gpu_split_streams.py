@@ -68,3 +68,39 @@ def test_split_injected_r_golden(dev):
     assert np.array_equal(pl.decrypt_u64(cts), want)
     for i in range(3):
         assert pl.decrypt_u64(cts[i:i + 1])[0] == want[i]
+
+
+_SPLIT_ALL_PROBE = r'''
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from conftest import golden_key, load_golden
+from fedtree_amd.paillier import Device, Paillier
+p, q = golden_key(load_golden("ref_gmp_L2048.json"))
+pl = Paillier.from_primes(p, q, Device(0))
+m = np.random.default_rng(5).integers(0, 2**64, int(sys.argv[2]), dtype=np.uint64)
+c = pl.encrypt_u64(m, seed=91)
+ok = bool(np.array_equal(pl.decrypt_u64(c), m))
+print(hashlib.sha256(c.tobytes()).hexdigest(), ok)
+'''
+
+
+def test_split_all_large_calls_bit_identical(tmp_path):
+    """Large CRT encrypts and decrypts run each chunk's p and q halves side by side on two streams (fthe.hip
+    split_all, the default); FTHE_SPLIT_ALL=0 runs them in turn on one stream.  Two chunks of 786,432 lanes and a
+    partial third: the seeded ciphertexts are byte-identical both ways and decrypt to their plaintexts."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = tmp_path / "probe.py"
+    probe.write_text(_SPLIT_ALL_PROBE)
+    outs = []
+    for v in ("0", "1"):
+        r = subprocess.run([sys.executable, str(probe), root, str(2 * 786432 + 5000)], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ, FTHE_SPLIT_ALL=v))
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(r.stdout.split())
+    assert outs[0][1] == "True" and outs[1][1] == "True"
+    assert outs[0][0] == outs[1][0]

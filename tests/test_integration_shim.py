@@ -343,8 +343,10 @@ def test_sharded_drop_in_identical_to_one_context(tmp_path, name):
     exe = str(tmp_path / "multidev_test")
     _build(exe, "multidev_test.cpp")
     outs = {}
-    for devs in ("0", "0,0", "0,0,0"):
-        env = dict(os.environ, FTHE_DEVICES=devs, FTHE_SHARD_ROWS="256")
+    for devs, rep in (("0", "0"), ("0,0", "1"), ("0,0,0", "0")):
+        # "0,0" also with FTHE_SHIM_REPLICATE=1: every shard on a key replica (from p, q for the key holder, from n
+        # and the published bases for the party), the path of a second physical GPU
+        env = dict(os.environ, FTHE_DEVICES=devs, FTHE_SHARD_ROWS="256", FTHE_SHIM_REPLICATE=rep)
         r = subprocess.run([exe, "run", f"{p:x}", f"{q:x}", "3000"], capture_output=True, text=True, timeout=300,
                            env=env)
         assert r.returncode == 0 and "multidev OK" in r.stdout, devs + ": " + r.stdout[-3000:] + r.stderr[-3000:]
@@ -352,6 +354,19 @@ def test_sharded_drop_in_identical_to_one_context(tmp_path, name):
         assert f"devices {len(devs.split(','))}" in lines
         outs[devs] = [ln for ln in lines if not ln.startswith("devices")]
     assert outs["0,0"] == outs["0"] and outs["0,0,0"] == outs["0"], outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", ["2", "100000"])
+def test_shim_concurrent_threads_sharded(tmp_path, rows):
+    """16 host threads on one key with the batch calls sharded over three contexts (FTHE_DEVICES=0,0,0): batches of
+    6 rows split into 3 shards that queue on the shard workers (FTHE_SHARD_ROWS=2), or run whole on each thread's
+    home slot (100000); every result checked (the OpenMP call pattern of FLtrainer.cpp:275-306, 758-764)."""
+    exe = str(tmp_path / "concurrency_test")
+    _build(exe, "concurrency_test.cpp")
+    env = dict(os.environ, FTHE_DEVICES="0,0,0", FTHE_SHARD_ROWS=rows, FTHE_SHIM_REPLICATE="1")
+    r = subprocess.run([exe, "1024", "16", "12", "default"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "concurrency OK" in r.stdout, r.stdout + r.stderr
 
 
 @pytest.mark.gpu
