@@ -8,9 +8,12 @@ One quad of lanes per ciphertext (lane j of the quad owns limbs [38j, 38j+38) of
 per wave, 12 waves per workgroup (one workgroup per CU: its LDS holds the key's constant images once).
 
   1. rows -> limbs (the row I/O of gen_montprog.gen_quad); y's limbs become the wave's A column in LDS.
-  2. z = x y on the VALU: 152 operand-scanning steps, 38 v_mad_u64_u32 per lane per step into a ring of
-     64-bit columns; the lowest column of lane 0 retires as limb z_i (written back into the A column row i,
-     whose a_i was consumed the step before) -- the Montgomery step of gen_quad without its q N half.
+  2. z = x y on the VALU by one level of Karatsuba on 76-limb halves (section 2K; "nokara" keeps the plain
+     152-step scan): P1 = (xL + xH)(yL + yH), P0 = xL yL, P2 = xH yH, each 76 operand-scanning steps of 19
+     v_mad_u64_u32 per lane into a ring of 64-bit columns -- 4,332 MADs per lane instead of 5,776 -- the lowest
+     column of lane 0 retiring as a limb (P0 / P2: into the A column row whose multiplier was consumed the step
+     before; P1: into registers), then z = P0 + (P1 - P0 - P2) B^76 + P2 B^152 in signed limbs, normalised
+     across lanes and blocks: 5% more adds/s (profiles/r05e_addb_kara_ab.jsonl, r05f_addb_libs_ab.jsonl).
   3. The window (z >> 4104) is normalised; z >> 4104 and z mod 2^4104 become dwords in the quad layout
      (lane j: dwords [32j, 32j+32)); q1 = z >> 4072 = [bits 4072..4103, (z >> 4104)] goes to a staging row
      per ciphertext, bytes fed as b ^ 0x80 (= b - 128, signed), padded with zero (fed 0) bytes.
@@ -112,6 +115,9 @@ def gen_addb(name: str) -> str:
     # nocanon (no conditional subtractions); stamp: per-phase s_memtime cycle sums per wave, written after the
     # launch's output rows (tools/addb_stamps.py; the stamps' lgkmcnt(0) drains cost some overlap)
     DBG = set(os.environ.get("FTHE_GEN_ADDB_DBG", "").split(","))
+    # the product z = x y as one level of Karatsuba (three 76 x 76-limb products, section 2K below) instead of
+    # 152 x 152 operand scanning; "nokara" keeps the latter (a correct schedule, for the A/B)
+    KARA = "nokara" not in DBG
     o = []
     e = o.append
     DPP = "row_mask:0xf bank_mask:0xf"
@@ -382,13 +388,17 @@ def gen_addb(name: str) -> str:
         e(f'  v_lshrrev_b32_e32 {t1}, {bo}, {t1}')
         e(f'  v_lshl_or_b32 {U(0)}, {U(0)}, v{V_SH}, {t1}')
 
-    def ripple_quad(lab, vals, nv, carry, signed=False, width=B, t=(V_TMP + 0, None)):
+    def ripple_quad(lab, vals, nv, carry, signed=False, width=B, t=(V_TMP + 0, None), top=None):
         """vals(k) (k < nv) limbs of `width` bits, a pending 64-bit carry-out in `carry` (per lane): the
-        carries move to the next lane's limb 0 (lane 0 gets none) and ripple until none is left."""
+        carries move to the next lane's limb 0 (lane 0 gets none) and ripple until none is left.  top: a
+        register that collects quad lane 3's carries-out (< 2^32; otherwise they are dropped)."""
         shr = 'v_ashrrev_i64' if signed else 'v_lshrrev_b64'
         c0, c1 = carry
         a0, a1 = V_AI
         e(f'{lab}_loop:')
+        if top is not None:
+            e(f'  v_cndmask_b32_e64 v{a0}, 0, v{c0}, s[20:21]')
+            e(f'  v_add_u32_e32 v{top}, v{top}, v{a0}')
         e('  s_nop 1')
         e(f'  v_mov_b32_dpp v{a0}, v{c0} quad_perm:[0,0,1,2] {DPP}')
         e(f'  v_mov_b32_dpp v{a1}, v{c1} quad_perm:[0,0,1,2] {DPP}')
@@ -429,71 +439,268 @@ def gen_addb(name: str) -> str:
     convert_row(W0, X)
     e('  s_waitcnt lgkmcnt(0)')
 
-    e('// @phase product')
-    e(f'  v_mov_b64_e32 {pair(HO)}, 0')
-    e(f'  v_mov_b32_e32 v{VMASK}, {hex(MASK)}')
-    e(f'  v_cndmask_b32_e64 v{VMASK}, v{VMASK}, 0, s[20:21]')
-    if "prio" in DBG:
-        e('  s_setprio 0')
-    if "prioinv" in DBG:
-        e('  s_setprio 3')
-    # ---- 2. z = x y: 152 steps; step i reads a_i (prefetched), adds a_i X into the window, retires the
-    #         lowest column: its carry stays in the lane's next column, its low 27 bits go one lane down (the
-    #         top column of lane j-1: one v_and_b32 with DPP into the hand-off pair, lane 3 receiving 0, that
-    #         the next step's top multiply-add takes as its addend, so the ring needs no fresh column), and
-    #         lane 0's -- the product limb z_i, written unmasked and masked when read back -- into A-column
-    #         row i.  Three VALU instructions per step beside the 38 multiply-adds. -------------------------
-    for k in range(NT):
-        e(f'  v_mov_b64_e32 {T(k)}, 0')
-    e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
-    e('  s_waitcnt lgkmcnt(0)')
+    def classic_product():
+        e('// @phase product')
+        e(f'  v_mov_b64_e32 {pair(HO)}, 0')
+        e(f'  v_mov_b32_e32 v{VMASK}, {hex(MASK)}')
+        e(f'  v_cndmask_b32_e64 v{VMASK}, v{VMASK}, 0, s[20:21]')
+        if "prio" in DBG:
+            e('  s_setprio 0')
+        if "prioinv" in DBG:
+            e('  s_setprio 3')
+        # ---- 2. z = x y: 152 steps; step i reads a_i (prefetched), adds a_i X into the window, retires the
+        #         lowest column: its carry stays in the lane's next column, its low 27 bits go one lane down (the
+        #         top column of lane j-1: one v_and_b32 with DPP into the hand-off pair, lane 3 receiving 0, that
+        #         the next step's top multiply-add takes as its addend, so the ring needs no fresh column), and
+        #         lane 0's -- the product limb z_i, written unmasked and masked when read back -- into A-column
+        #         row i.  Three VALU instructions per step beside the 38 multiply-adds. -------------------------
+        for k in range(NT):
+            e(f'  v_mov_b64_e32 {T(k)}, 0')
+        e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
+        e('  s_waitcnt lgkmcnt(0)')
 
-    def step(u, row, prefetch):
+        def step(u, row, prefetch):
+            ai, nai = f"v{V_AI[u % 2]}", f"v{V_AI[(u + 1) % 2]}"
+            for k in range(Q):
+                if "noprod" not in DBG:
+                    src2 = pair(HO) if k == Q - 1 else T(u + k)   # T(u + Q - 1): the slot of the retired T(u - 1)
+                    e(f'  v_mad_u64_u32 {T(u + k)}, vcc, {ai}, {X(k)}, {src2}')
+                if k == 2:
+                    e(f'  v_lshrrev_b64 {tmp}, {B}, {T(u)}')
+                if k == 5:
+                    e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
+                if k == 10 and prefetch is not None:
+                    e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{prefetch * RB}')
+                if k == 12:                              # after the read: the step's wait leaves the write out
+                    e('  s_mov_b64 exec, s[22:23]')
+                    e(f'  ds_write_b32 v{V_LDSI}, {Tlo(u)} offset:{row * RB}')
+                    e('  s_mov_b64 exec, -1')
+            e(f'  v_and_b32_dpp v{HO}, {Tlo(u)}, v{VMASK} quad_perm:[1,2,3,0] {DPP}')
+            if prefetch is not None:
+                e('  s_waitcnt lgkmcnt(1)')
+
+        NTRIP, TL = S // NT, S % NT
+        assert NT % 2 == 0 and TL == 0
+        e(f'  s_mov_b32 s18, {NTRIP}')
+        e('.Ltrip:')
+        for u in range(NT):
+            step(u, u, u + 1)
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(NT * RB)}, v{V_LDSI}')
+        e('  s_sub_u32 s18, s18, 1')
+        e('  s_cmp_lg_u32 s18, 0')
+        e('  s_cbranch_scc1 .Ltrip')
+        for u in range(TL):
+            step(u, u, u + 1 if u + 1 < TL else None)
+        e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB)}, v{V_LDSI}')
+
+        e('// @phase window')
+        if "prio" in DBG:
+            e('  s_setprio 3')
+        if "prioinv" in DBG:
+            e('  s_setprio 0')
+        # ---- 3. window -> W limbs (X), W -> dwords WD; z mod 2^4104 limbs (LDS) -> dwords ZL ---------------
+        e(f'  v_mov_b64_e32 {tmp}, 0')
+        for k in range(Q):                            # columns 152 + k: T(k), the top one in the hand-off pair
+            e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TL + k) if k < Q - 1 else pair(HO)}')
+            e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
+            e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+        ripple_quad('.Lrw', X, Q, (V_TMP, V_TMP + 1))
+
+    # ---- 2K. z = x y by one level of Karatsuba on 76-limb halves (KARA): x = xL + xH B^76, y = yL + yH B^76,
+    #          P1 = (xL + xH)(yL + yH), P0 = xL yL, P2 = xH yH, z = P0 + (P1 - P0 - P2) B^76 + P2 B^152.  Each is a
+    #          76-step operand scan over a 76-limb window of 19 limbs per quad lane (the step of section 2 with
+    #          19 instead of 38 multiply-adds): 3 x 76 x 19 = 4,332 MADs per lane against 152 x 38 = 5,776.  The
+    #          multipliers come from the A column (rows 0..75 yL, 76..151 yH; P1 adds the two rows); P1 runs first
+    #          and keeps its retired limbs in registers, P0 and P2 retire theirs into their consumed rows, so the
+    #          A column ends as (P0 low, P2 low).  The combination is signed limb arithmetic, normalised as one
+    #          228-limb number (blocks 1..3 of z; block 0 is P0 low) with carries across lanes and blocks. -----
+    Q2 = Q // 2                                   # 19 window limbs per lane
+    # the multiplier prefetch after the step's ninth multiply-add (timing knob pfN: after the first measured no
+    # faster, profiles/r05f_addb_libs_ab.jsonl)
+    KARA_PF = next((int(t[2:]) for t in DBG if t.startswith('pf') and t[2:].isdigit()), 8)
+    HALF = S // 2                                 # 76
+    XW = {"L": 46, "H": 65, "S": 84}              # 19-limb windows of xL, xH, xL + xH (later P0 / P2 / P1 high)
+    HO2 = 104                                     # hand-off pair v[104:105] (v105 stays 0)
+    P1L, P1TOP = 146, 165                         # P1's retired limbs (lane k: limbs 19 k + p), lane 3: limb 152
+    BI = (125, 126)                               # P1: the yH multiplier's double buffer
+    RT = 127                                      # P1: the retired limb broadcast over the quad
+    VZ = 128                                      # A-column base of lane j's 19-limb blocks: area + 4c + 19 j RB
+    CB = (129, 130, 131)                          # combination: carries of blocks 1..3
+    CI = (132, 133, 134)                          # their carries-in
+    RO = (135, 136, 137)                          # rotated carries
+
+    def T2(k):
+        k %= Q2
+        return f"v[{XB + 2 * k}:{XB + 2 * k + 1}]"
+
+    def T2lo(k):
+        return f"v{XB + 2 * (k % Q2)}"
+
+    def W_(nm):
+        return lambda k: f"v{XW[nm] + k}"
+
+    def kara_step(mode, u, W):
+        """step u (0..37 of a two-trip loop body) of pass `mode`: multiplier rows u (+76: yH); P1 adds the yL
+        and yH limbs, P0 / P2 retire lane 0's column into rows u / 76 + u, P1 into register u mod 19 of the
+        quad lane (2 trip + u div 19) (mask s[38:39], shifted per trip)"""
         ai, nai = f"v{V_AI[u % 2]}", f"v{V_AI[(u + 1) % 2]}"
-        for k in range(Q):
+        bi, nbi = f"v{BI[u % 2]}", f"v{BI[(u + 1) % 2]}"
+        if mode == "P1":
+            e(f'  v_add_u32_e32 {ai}, {ai}, {bi}')              # yL_i + yH_i (< 2^28)
+        for k in range(Q2):
             if "noprod" not in DBG:
-                src2 = pair(HO) if k == Q - 1 else T(u + k)   # T(u + Q - 1): the slot of the retired T(u - 1)
-                e(f'  v_mad_u64_u32 {T(u + k)}, vcc, {ai}, {X(k)}, {src2}')
+                src2 = pair(HO2) if k == Q2 - 1 else T2(u + k)
+                e(f'  v_mad_u64_u32 {T2(u + k)}, vcc, {ai}, {W(k)}, {src2}')
             if k == 2:
-                e(f'  v_lshrrev_b64 {tmp}, {B}, {T(u)}')
+                e(f'  v_lshrrev_b64 {tmp}, {B}, {T2(u)}')
             if k == 5:
-                e(f'  v_lshl_add_u64 {T(u + 1)}, {tmp}, 0, {T(u + 1)}')
-            if k == 10 and prefetch is not None:
-                e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{prefetch * RB}')
-            if k == 12:                              # after the read: the step's wait leaves the write out
+                e(f'  v_lshl_add_u64 {T2(u + 1)}, {tmp}, 0, {T2(u + 1)}')
+            if k == KARA_PF:                          # prefetch the next step's multiplier(s)
+                if mode in ("P1", "P0"):
+                    e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(u + 1) * RB}')
+                if mode == "P1":
+                    e(f'  ds_read_b32 {nbi}, v{V_LDSI} offset:{(HALF + u + 1) * RB}')
+                if mode == "P2":
+                    e(f'  ds_read_b32 {nai}, v{V_LDSI} offset:{(HALF + u + 1) * RB}')
+            if k == 12 and mode in ("P0", "P2"):      # after the read: the step's wait leaves the write out
                 e('  s_mov_b64 exec, s[22:23]')
-                e(f'  ds_write_b32 v{V_LDSI}, {Tlo(u)} offset:{row * RB}')
+                e(f'  ds_write_b32 v{V_LDSI}, {T2lo(u)} offset:{(u if mode == "P0" else HALF + u) * RB}')
                 e('  s_mov_b64 exec, -1')
-        e(f'  v_and_b32_dpp v{HO}, {Tlo(u)}, v{VMASK} quad_perm:[1,2,3,0] {DPP}')
-        if prefetch is not None:
-            e('  s_waitcnt lgkmcnt(1)')
+            if k == 13 and mode == "P1":
+                e(f'  v_mov_b32_dpp v{RT}, {T2lo(u)} quad_perm:[0,0,0,0] {DPP}')
+            if k == 16 and mode == "P1":
+                e(f'  v_cndmask_b32_e64 v{P1L + u % Q2}, v{P1L + u % Q2}, v{RT}, s[38:39]')
+        e(f'  v_and_b32_dpp v{HO2}, {T2lo(u)}, v{VMASK} quad_perm:[1,2,3,0] {DPP}')
+        if mode == "P1" and u % Q2 == Q2 - 1:
+            e('  s_lshl_b64 s[38:39], s[38:39], 1')          # the next trip's quad lane
+        e(f'  s_waitcnt lgkmcnt({0 if mode == "P1" else 1})')
 
-    NTRIP, TL = S // NT, S % NT
-    assert NT % 2 == 0 and TL == 0
-    e(f'  s_mov_b32 s18, {NTRIP}')
-    e('.Ltrip:')
-    for u in range(NT):
-        step(u, u, u + 1)
-    e(f'  v_add_u32_e32 v{V_LDSI}, {hex(NT * RB)}, v{V_LDSI}')
-    e('  s_sub_u32 s18, s18, 1')
-    e('  s_cmp_lg_u32 s18, 0')
-    e('  s_cbranch_scc1 .Ltrip')
-    for u in range(TL):
-        step(u, u, u + 1 if u + 1 < TL else None)
-    e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(NTRIP * NT * RB)}, v{V_LDSI}')
+    def kara_pass(mode, W, out, top=None):
+        """one 76 x 76 product over window W; its top 76 (+1) limbs normalised into out(k) (19 per lane)"""
+        lab = f'.Lk{mode}'
+        for k in range(Q2):
+            e(f'  v_mov_b64_e32 {T2(k)}, 0')
+        e(f'  v_mov_b64_e32 {pair(HO2)}, 0')
+        if mode in ("P1", "P0"):
+            e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI}')
+        if mode == "P1":
+            e(f'  ds_read_b32 v{BI[0]}, v{V_LDSI} offset:{HALF * RB}')
+            e('  s_mov_b64 s[38:39], s[22:23]')                  # trip 0: quad lane 0
+        if mode == "P2":
+            e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI} offset:{HALF * RB}')
+        e('  s_waitcnt lgkmcnt(0)')
+        e('  s_mov_b32 s18, 2')
+        e(f'{lab}_trip:')
+        for u in range(2 * Q2):
+            kara_step(mode, u, W)
+        e(f'  v_add_u32_e32 v{V_LDSI}, {hex(2 * Q2 * RB)}, v{V_LDSI}')
+        e('  s_sub_u32 s18, s18, 1')
+        e('  s_cmp_lg_u32 s18, 0')
+        e(f'  s_cbranch_scc1 {lab}_trip')
+        e(f'  v_subrev_u32_e32 v{V_LDSI}, {hex(HALF * RB)}, v{V_LDSI}')
+        # the window: columns 76 + k of the lane's 19 (the top one in the hand-off pair), normalised
+        e(f'  v_mov_b64_e32 {tmp}, 0')
+        for k in range(Q2):
+            e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T2(k) if k < Q2 - 1 else pair(HO2)}')
+            e(f'  v_and_b32_e32 {out(k)}, {hex(MASK)}, v{V_TMP}')
+            e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
+        ripple_quad(f'{lab}_rw', out, Q2, (V_TMP, V_TMP + 1), top=top)
 
-    e('// @phase window')
-    if "prio" in DBG:
-        e('  s_setprio 3')
-    if "prioinv" in DBG:
-        e('  s_setprio 0')
-    # ---- 3. window -> W limbs (X), W -> dwords WD; z mod 2^4104 limbs (LDS) -> dwords ZL ---------------
-    e(f'  v_mov_b64_e32 {tmp}, 0')
-    for k in range(Q):                            # columns 152 + k: T(k), the top one in the hand-off pair
-        e(f'  v_lshl_add_u64 {tmp}, {tmp}, 0, {T(TL + k) if k < Q - 1 else pair(HO)}')
-        e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, v{V_TMP}')
-        e(f'  v_lshrrev_b64 {tmp}, {B}, {tmp}')
-    ripple_quad('.Lrw', X, Q, (V_TMP, V_TMP + 1))
+    def kara_product():
+        e('// @phase product')
+        e(f'  v_mov_b32_e32 v{VMASK}, {hex(MASK)}')
+        e(f'  v_cndmask_b32_e64 v{VMASK}, v{VMASK}, 0, s[20:21]')
+        # the windows: lane j of xL holds limbs 19 j .. 19 j + 18, i.e. limbs 19 (j & 1) + p of quad lane j >> 1's
+        # 38 (xH: of quad lane 2 + (j >> 1)); xS = xL + xH limb by limb (28 bits)
+        e('  s_or_b64 s[16:17], s[24:25], s[20:21]')                # quad lanes 1, 3
+        ta, tb = f"v{V_AI[0]}", f"v{V_AI[1]}"
+        for p in range(Q2):
+            for nm, qp in (("L", "[0,0,1,1]"), ("H", "[2,2,3,3]")):
+                e(f'  v_mov_b32_dpp {ta}, {X(p)} quad_perm:{qp} {DPP}')
+                e(f'  v_mov_b32_dpp {tb}, {X(Q2 + p)} quad_perm:{qp} {DPP}')
+                e(f'  v_cndmask_b32_e64 v{XW[nm] + p}, {ta}, {tb}, s[16:17]')
+            e(f'  v_add_u32_e32 v{XW["S"] + p}, v{XW["L"] + p}, v{XW["H"] + p}')
+        e(f'  v_mov_b32_e32 v{P1TOP}, 0')
+        kara_pass("P1", W_("S"), W_("S"), top=P1TOP)                # P1 high -> the xS registers
+        kara_pass("P0", W_("L"), W_("L"))                           # P0 high -> xL's
+        kara_pass("P2", W_("H"), W_("H"))                           # P2 high -> xH's
+        e('// @phase window')
+        # z1 (limbs 76 + 19 j + p) = P0H + P1L - P0L - P2L, z2 (152 + ...) = P2L + P1H - P0H - P2H,
+        # z3 (228 + ...) = P2H (+ P1's limb 152 at z limb 228); P0L / P2L are A-column rows 19 j + p / 76 + 19 j + p
+        e(f'  v_add_u32_e32 v{VZ}, v{V_LDSI}, v{V_ZR}')
+        e(f'  v_lshrrev_b32_e32 v{VZ}, 1, v{VZ}')                    # area + 4c + 19 j RB
+        R0, R2 = XB, XB + Q2                                        # the ring is dead
+        for p in range(Q2):
+            e(f'  ds_read_b32 v{R0 + p}, v{VZ} offset:{p * RB}')
+            e(f'  ds_read_b32 v{R2 + p}, v{VZ} offset:{(HALF + p) * RB}')
+        e('  s_waitcnt lgkmcnt(0)')
+        P0H, P1H, P2H = XW["L"], XW["S"], XW["H"]
+        for p in range(Q2):
+            e(f'  v_and_b32_e32 v{R0 + p}, {hex(MASK)}, v{R0 + p}')
+            e(f'  v_and_b32_e32 v{R2 + p}, {hex(MASK)}, v{R2 + p}')
+            e(f'  v_and_b32_e32 v{P1L + p}, {hex(MASK)}, v{P1L + p}')
+            e(f'  v_add_u32_e32 v{P1L + p}, v{P1L + p}, v{P0H + p}')
+            e(f'  v_sub_u32_e32 v{P1L + p}, v{P1L + p}, v{R0 + p}')
+            e(f'  v_sub_u32_e32 v{P1L + p}, v{P1L + p}, v{R2 + p}')       # z1
+            e(f'  v_add_u32_e32 v{P1H + p}, v{P1H + p}, v{R2 + p}')
+            e(f'  v_sub_u32_e32 v{P1H + p}, v{P1H + p}, v{P0H + p}')
+            e(f'  v_sub_u32_e32 v{P1H + p}, v{P1H + p}, v{P2H + p}')       # z2
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{RT}, v{P1TOP} quad_perm:[3,3,3,3] {DPP}')   # P1's limb 152 -> z3 limb 0 of lane 0
+        e(f'  v_cndmask_b32_e64 v{RT}, 0, v{RT}, s[22:23]')
+        e(f'  v_add_u32_e32 v{P2H}, v{P2H}, v{RT}')
+        blocks = (P1L, P1H, P2H)                                    # z1, z2, z3: signed limbs
+        for b, base in enumerate(blocks):                           # each lane's segments, carries out
+            for p in range(Q2):
+                if p:
+                    e(f'  v_add_u32_e32 v{base + p}, v{base + p}, v{CB[b]}')
+                e(f'  v_ashrrev_i32_e32 v{CB[b]}, {B}, v{base + p}')
+                e(f'  v_and_b32_e32 v{base + p}, {hex(MASK)}, v{base + p}')
+        # carries across segments: block b, lane j -> lane j + 1; lane 3 -> block b + 1, lane 0 (z < B^304: the top
+        # segment's carry is 0 at the end); repeated until no segment receives a carry
+        lab = f'.Lkc{len(o)}'
+        e(f'{lab}_loop:')
+        e('  s_nop 1')
+        for b in range(3):
+            e(f'  v_mov_b32_dpp v{RO[b]}, v{CB[b]} quad_perm:[3,0,1,2] {DPP}')
+        e(f'  v_cndmask_b32_e64 v{CI[0]}, v{RO[0]}, 0, s[22:23]')
+        e(f'  v_cndmask_b32_e64 v{CI[1]}, v{RO[1]}, v{RO[0]}, s[22:23]')
+        e(f'  v_cndmask_b32_e64 v{CI[2]}, v{RO[2]}, v{RO[1]}, s[22:23]')
+        e(f'  v_or3_b32 v{RT}, v{CI[0]}, v{CI[1]}, v{CI[2]}')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{RT}')
+        e('  s_nop 4')
+        e(f'  s_cbranch_vccz {lab}_done')
+        for b in range(3):
+            e(f'  v_mov_b32_e32 v{CB[b]}, v{CI[b]}')
+        for p in range(Q2):
+            for b, base in enumerate(blocks):
+                e(f'  v_add_u32_e32 v{base + p}, v{base + p}, v{CB[b]}')
+                e(f'  v_ashrrev_i32_e32 v{CB[b]}, {B}, v{base + p}')
+                e(f'  v_and_b32_e32 v{base + p}, {hex(MASK)}, v{base + p}')
+            if p == 1:                                # absorbed by limbs 0, 1 everywhere (the usual case)
+                e(f'  v_or3_b32 v{RT}, v{CB[0]}, v{CB[1]}, v{CB[2]}')
+                e(f'  v_cmp_ne_u32_e32 vcc, 0, v{RT}')
+                e('  s_nop 4')
+                e(f'  s_cbranch_vccz {lab}_done')
+        e(f'  s_branch {lab}_loop')
+        e(f'{lab}_done:')
+        # z1 -> A-column rows 76 + 19 j + p (rows 0..151 = z mod 2^4104 as limbs, read below as before)
+        for p in range(Q2):
+            e(f'  ds_write_b32 v{VZ}, v{P1L + p} offset:{(HALF + p) * RB}')
+        # z >> 4104 = (z2, z3) -> X: lane j holds limbs 38 j + k, i.e. segment 2 j + (k >= 19) of blocks 2, 3
+        ta, tb = f"v{V_AI[0]}", f"v{V_AI[1]}"
+        e('  s_or_b64 s[16:17], s[22:23], s[24:25]')                # quad lanes 0, 1
+        for k in range(Q2):
+            for half, qp in ((0, "[0,2,0,2]"), (1, "[1,3,1,3]")):
+                e(f'  v_mov_b32_dpp {ta}, v{P1H + k} quad_perm:{qp} {DPP}')
+                e(f'  v_mov_b32_dpp {tb}, v{P2H + k} quad_perm:{qp} {DPP}')
+                e(f'  v_cndmask_b32_e64 {X(Q2 * half + k)}, {tb}, {ta}, s[16:17]')   # lanes 0, 1: block 2
+        e('  s_waitcnt lgkmcnt(0)')
+
+    if KARA:
+        kara_product()
+    else:
+        classic_product()
     limbs_to_words(X, lambda i: f"v{WD + i}", f"v{ZL128}", f"v{V_AI[0]}")
     for k in range(Q):
         e(f'  ds_read_b32 {X(k)}, v{V_ZR} offset:{k * RB}')

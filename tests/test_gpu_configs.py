@@ -92,6 +92,15 @@ def test_config2_p2048_10M_pairs_roundtrip(dev, coracle):
     assert [pyoracle.from_words(d) for d in dec] == [int(v) for v in m_host[idx.cpu().numpy()]]
     # fresh randomness: no repeated ciphertext among equal plaintexts of the sample
     assert len({s.tobytes() for s in sample}) == len(sample)
+    # the timed path itself, bit for bit across the whole batch: 64 ciphertexts on each side of every 786,432-lane
+    # launch boundary (the p and q halves of each chunk on two streams) and the batch's first and last 64, each
+    # against the C oracle's full-PowerMod encrypt(m, r) with r rebuilt from the drawn (y_p, y_q)
+    from test_gpu_direct_y import ENC_CHUNK, _check
+    n = 2 * pairs
+    edges = [0] + list(range(ENC_CHUNK, n, ENC_CHUNK)) + [n]
+    idx = np.unique(np.concatenate([np.arange(max(0, b - 64), min(n, b + 64)) for b in edges]))
+    rows = c[torch.from_numpy(idx).to("cuda:0")].cpu().numpy().view(np.uint32)
+    _check(pl, ok, m_host[idx], rows, 77, idx)
 
 
 def test_config3_p2048_8party_merge_full_size(dev):

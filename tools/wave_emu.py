@@ -264,6 +264,10 @@ class Wave:
             r = (g(a[1]) & M32) >> (g(a[2]) & 31)
             self.sset(a[0], r)
             self.scc = int(r != 0)
+        elif op == 's_lshl_b64':
+            r = (g(a[1], 2) << (g(a[2]) & 63)) & M64
+            self.sset(a[0], r)
+            self.scc = int(r != 0)
         elif op == 's_lshl_b32':
             r = (g(a[1]) << g(a[2])) & M32
             self.sset(a[0], r)
@@ -422,6 +426,10 @@ class Wave:
                 lo = (s0 >> (32 * sel[0])) & M32
                 hi = (s1 >> (32 * sel[1])) & M32
                 self.vset(l, a[0], lo | hi << 32)
+            return
+        if op == 'v_or3_b32':
+            for l in lanes:
+                self.vset(l, a[0], (g(l, a[1]) | g(l, a[2]) | g(l, a[3])) & M32)
             return
         if op == 'v_bitop3_b32':                   # bit i = table[src0_i << 2 | src1_i << 1 | src2_i]
             tbl = int(a[4].split(':')[1], 0)
