@@ -908,9 +908,10 @@ def run(a, world):
         kname = "fthe_addb_q152" if "fthe_addb_q152" in padd else "fthe_montprog_s152"
         pk = padd.get(kname, {})
         rate = na / add_s
-        # fthe_addb_q152 (gen_addb.py): z = x y on the VALU, 152 x 152 radix-2^27 v_mad_u64_u32 per add; both
+        # fthe_addb_q152 (gen_addb.py): z = x y on the VALU by one level of Karatsuba on 76-limb halves,
+        # 3 x 76 x 76 radix-2^27 v_mad_u64_u32 per add (152 x 152 in the "nokara" generator variant); both
         # Barrett products (q1 mu, q3 n^2) on the i8 matrix cores, 338 v_mfma_i32_16x16x64_i8 per 16 adds
-        valu_macs = 152 * 152
+        valu_macs = 3 * 76 * 76
         i8_macs = 338 * 16 * 16 * 64 / 16
         i8_peak = 1024 * 2.4e9 * (32 * 32 * 32 * 2) / 32
         secondary["p2048_add_hbm"] = {"algorithmic_GBps": round(na * 1536 / add_s / 1e9, 1),
