@@ -73,6 +73,15 @@ LDSX = "ldsx" in AB
 # pairs packed into the tile's first 8 accumulator registers, 2 dwordx4 per half through LDS for 8 swaps
 LDSXA = LDSX and "ldsxa" in AB
 LDSX_BYTES = 5 * 1024           # per wave: 5 K-blocks x 64 lanes x 16 B
+# kara: a squaring's cross term V = 2 x0 x1 by one level of Karatsuba on the halves x = xL + xH b^19 (19 / 18
+# limbs): 2 P0 = 2 xL yL and 2 P2 = 2 xH yH normalised first (P0 into V[0..18] and C, P2 complemented into
+# V[38..73]), then the middle columns of (x0L + x0H)(2 x1L + 2 x1H) - 2 P0 - 2 P2 added at b^19 with a biased
+# carry, and the carry rippled through V[57..73] beside x0^2's multiply-adds: 1,046 instead of 1,369
+# multiply-adds per squaring, 4,076 instead of 4,102 VALU (see kara_cross below).  Measured +0.5%: 133.8-134.1 vs
+# 134.5-134.9 ms per 786,432 lanes, 67.8-68.4 vs 68.0-68.5 per 393,216 (profiles/r05i_m37_kara_ab.jsonl) -- the
+# MAD cycles saved mostly reappear as exposed latency of the matrix phases; nokara keeps the plain product (A/B)
+KARA = "nokara" not in AB
+assert not (KARA and LDSX)
 assert not (LDSX and (PP or SPILL))
 LDS_BYTES = TILE_BYTES + (4 * SPILL_BYTES if SPILL else 0) + (4 * LDSX_BYTES if LDSX else 0)
 S1_LO = 112                     # product-1 columns S1_LO .. S1_LO + 159
@@ -131,6 +140,8 @@ def gen_padic_mfma(name: str) -> str:
     SLO, SHI = 74, 76                            # LDSX: EXEC masks of lanes 0-31 / 32-63
     if LDSX:
         NSGPR = SHI + 2
+    if KARA:                                     # s76..s78: 2, 3, 4 x mask
+        NSGPR = 79
     POW = lambda sh: f"s{SPOW + sh // 4}"
     NEG = lambda sh: f"s{SNEG + sh // 4}"
     NP = lambda j: f"s{SNP + j}"
@@ -165,20 +176,37 @@ def gen_padic_mfma(name: str) -> str:
         return out
 
     # ---- column engine (product scanning, two adjacent columns side by side) --------------------
-    def columns(cols, signed=False):
+    def columns(cols, signed=False, carry_in=False, bg=()):
+        """product scanning over cols (dicts): 'terms' [(a, b)] multiply-adds, 'dbl' (column x 2), 'sq' (one
+        more x*x after the doubling), 'out' (the limb register), 'px' (flip pattern of a pre-XORed limb), 'cpl'
+        (store mask - limb), 'last' (no mask, no carry), 'addend' (a register pair with a zero high dword: the
+        first multiply-add's addend), 'pre' (instructions that must precede the column's first multiply-add:
+        emitted during the previous group's multiply-adds).  carry_in: the carry register holds column 0's
+        carry.  bg: independent instructions spread over the multiply-adds (one per two while no tail is
+        pending), the rest emitted at the end."""
         mad = 'v_mad_i64_i32' if signed else 'v_mad_u64_u32'
         shr = 'v_ashrrev_i64' if signed else 'v_lshrrev_b64'
         pending = []
+        bgq = list(bg)
 
         def flush(n):
             for _ in range(min(n, len(pending))):
                 e(pending.pop(0))
 
+        def tick():
+            if pending:
+                flush(1)
+            elif bgq:
+                e(bgq.pop(0))
+
         def tail_of(ci, col, a0, lo0, used):
             t = []
-            first = ci == 0
+            first = ci == 0 and not carry_in
             if not used:
-                t.append(f'  v_mov_b64_e32 {a0}, {"0" if first else carry}')
+                if col.get('addend'):
+                    t.append(f'  v_lshl_add_u64 {a0}, {col["addend"]}, 0, {"0" if first else carry}')
+                else:
+                    t.append(f'  v_mov_b64_e32 {a0}, {"0" if first else carry}')
             elif col.get('dbl'):
                 t.append(f'  v_lshl_add_u64 {a0}, {a0}, 1, {"0" if first else carry}')
             elif not first:
@@ -188,7 +216,13 @@ def gen_padic_mfma(name: str) -> str:
                 t.append(f'  {mad} {a0}, vcc, {x}, {x}, {a0}')
             if col.get('out') is not None:
                 px = col.get('px')
-                if col.get('last'):
+                if col.get('cpl'):                           # mask - limb (the top limb: < 2^28 asserted by
+                    assert not px                            # the model, so the XOR is the same)
+                    if col.get('last'):
+                        t.append(f'  v_xor_b32_e32 {col["out"]}, {SMASK}, {lo0}')
+                    else:
+                        t.append(f'  v_bitop3_b32 {col["out"]}, {lo0}, {SMASK}, {lo0} bitop3:0xc')
+                elif col.get('last'):
                     if px:
                         t.append(f'  v_xor_b32_e32 {col["out"]}, {px}, {lo0}')
                     else:
@@ -201,27 +235,34 @@ def gen_padic_mfma(name: str) -> str:
                 t.append(f'  {shr} {carry}, {B}, {a0}')
             return t
 
+        for ci in range(min(NCOL, len(cols))):
+            for ins in cols[ci].get('pre', ()):
+                e(ins)
         for gi in range(0, len(cols), NCOL):
             s = (gi // NCOL) % 2
             members = list(range(gi, min(gi + NCOL, len(cols))))
-            seqs = [(acc(s, m), cols[ci]['terms']) for m, ci in enumerate(members)]
+            seqs = [(acc(s, m), cols[ci]['terms'], cols[ci].get('addend')) for m, ci in enumerate(members)]
             used = [False] * len(seqs)
+            for ci in range(gi + NCOL, min(gi + 2 * NCOL, len(cols))):
+                pending += list(cols[ci].get('pre', ()))
             n = 0
             for t in range(max(len(q[1]) for q in seqs)):
-                for k, (ac, terms) in enumerate(seqs):
+                for k, (ac, terms, add) in enumerate(seqs):
                     if t < len(terms):
                         a_, b_ = terms[t]
-                        e(f'  {mad} {ac}, vcc, {a_}, {b_}, {ac if used[k] else "0"}')
+                        e(f'  {mad} {ac}, vcc, {a_}, {b_}, {ac if used[k] else (add or "0")}')
                         used[k] = True
                         n += 1
                         if n % 2 == 0:
-                            flush(1)
+                            tick()
             flush(len(pending))
             tail = []
             for m, ci in enumerate(members):
                 tail += tail_of(ci, cols[ci], acc(s, m), acclo(s, m), used[m])
             pending = tail
         flush(len(pending))
+        for ins in bgq:
+            e(ins)
 
     def product_cols(a, b, n_out, outs, a2=None, b2=None):
         cols = []
@@ -253,6 +294,7 @@ def gen_padic_mfma(name: str) -> str:
     CACC2 = (pair(XA + 32), pair(XA + 34))      # chunk sums, alternating by chunk parity: v[52:53], v[54:55]
     CCARRY = pair(XA + 38)                      # chunk carry v[58:59]
     SMASK = "s35"                               # 0x0fffffff (v_bfi_b32 operand)
+    S2MASK, S3MASK, S4MASK = "s76", "s77", "s78"  # KARA: 2, 3, 4 x 0x0fffffff
 
     def orpack(limbs, shift_bits, ndw, xor_masks, lead_one=False, norm0=False, pre=()):
         """normalised 28-bit limbs (limb t at bit 28 t + shift_bits) -> dwords D[0..ndw-1] XOR xor_masks[w],
@@ -696,6 +738,9 @@ def gen_padic_mfma(name: str) -> str:
     for i in range(7):
         e(f'  s_mov_b32 s{SNEG + i}, {hex((-(1 << (4 * i))) & 0xFFFFFFFF)}')
     e(f'  s_mov_b32 s35, {hex(MASK)}')
+    if KARA:
+        for r_, m_ in ((S2MASK, 2), (S3MASK, 3), (S4MASK, 4)):
+            e(f'  s_mov_b32 {r_}, {hex(m_ * MASK)}')
     if PREXOR:
         for v_, val in zip(PATV, PATVAL):
             e(f'  v_mov_b32_e32 v{v_}, {hex(val)}')
@@ -809,19 +854,91 @@ def gen_padic_mfma(name: str) -> str:
     store_limbs(X0 + X1)
     e('  s_branch .Lprog')
 
+    def kara_cross():
+        """V = 2 x0 x1 (74 limbs, the upper 37 pre-XORed) by one level of Karatsuba; returns the ripple of the
+        final carry through V[57..73] as independent instructions for x0^2's column pass.  Halves: x = xL + xH
+        b^19, xL = limbs 0..18, xH = limbs 19..36.  Temporaries in T (free until x0^2): S0 = x0L + x0H (T[0..17],
+        S0_18 = x0_18), S1 = 2 (x1L + x1H) (T[18..36]), C = limbs 19..37 of 2 P0 (T[37..55]); the middle
+        columns' addends in v2 / v4 over permanently zero v3 / v5.
+          1. 2 P0 = 2 x0L x1L: limbs 0..18 -> V[0..18], 19..37 -> C (limb 37 < 2^29, unmasked);
+          2. 2 P2 = 2 x0H x1H: limbs 0..35 -> V[38..73] as mask - limb (complemented);
+          3. column k = 0..37 of S0 S1 (at most 2^63.1: unsigned) plus t'_k = L_k - P0_k - P2_k + 3 mask, where
+             L_k is the limb of 2 P0 + 2 P2 b^38 at position k + 19 and P0_k, P2_k the limbs subtracted (t'_k in
+             [0, 2^30): the first multiply-add's addend), plus the carry, which starts at 3: with t' biased by
+             3 mask = 3 (2^28 - 1) every column value is the true one plus 3 2^28 >= 0 (the true one >= -2^29 - 2),
+             so its limb is exact and its carry the true one plus 3; limb -> V[k + 19];
+          4. V[57..73] += the final carry (>= 0, minus the bias 3), complemented limbs restored."""
+        S0 = T[:18] + [X0[18]]
+        S1 = T[18:37]
+        C = T[37:56]
+        TPL, TPH = ("v2", "v4"), ("v3", "v5")
+        bg = []
+        for i in range(18):
+            bg.append(f'  v_add_u32_e32 {S0[i]}, {X0[i]}, {X0[19 + i]}')
+            bg.append(f'  v_add_lshl_u32 {S1[i]}, {X1[i]}, {X1[19 + i]}, 1')
+        bg.append(f'  v_lshlrev_b32_e32 {S1[18]}, 1, {X1[18]}')
+        bg += [f'  v_mov_b32_e32 {h}, 0' for h in TPH]
+        cols = []
+        for c in range(38):                                     # 2 P0
+            terms = [(X0[i], X1[c - i]) for i in range(19) if 0 <= c - i < 19]
+            cols.append({'terms': terms, 'dbl': True, 'out': V[c] if c < 19 else C[c - 19], 'last': c == 37})
+        columns(cols, bg=bg)
+        cols = []
+        for c in range(36):                                     # 2 P2, complemented
+            terms = [(X0[19 + i], X1[19 + c - i]) for i in range(18) if 0 <= c - i < 18]
+            cols.append({'terms': terms, 'dbl': True, 'out': V[38 + c], 'cpl': True, 'last': c == 35})
+        columns(cols)
+        e(f'  v_mov_b64_e32 {carry}, 3')
+        cols = []
+        for k in range(38):                                     # middle columns at b^19
+            tl = TPL[k % 2]
+            if k <= 18:                                         # C_k - P0_k + (mask - P2_k) + 2 mask
+                pre = [f'  v_sub_u32_e32 {tl}, {C[k]}, {V[k]}',
+                       f'  v_add3_u32 {tl}, {tl}, {V[38 + k]}, {S2MASK}']
+            elif k <= 35:                                       # P2c_k - P2c_(k-19) - C_(k-19) + 3 mask
+                pre = [f'  v_sub_u32_e32 {tl}, {V[38 + k]}, {V[k + 19]}',
+                       f'  v_sub_u32_e32 {tl}, {tl}, {C[k - 19]}',
+                       f'  v_add_u32_e32 {tl}, {S3MASK}, {tl}']
+            else:                                               # P2_36 = P2_37 = 0: 4 mask - P2c - C
+                pre = [f'  v_sub_u32_e32 {tl}, {S4MASK}, {V[k + 19]}',
+                       f'  v_sub_u32_e32 {tl}, {tl}, {C[k - 19]}']
+            terms = [(S0[i], S1[k - i]) for i in range(19) if 0 <= k - i < 19]
+            col = {'terms': terms, 'out': V[k + 19], 'addend': f'v[{tl[1:]}:{int(tl[1:]) + 1}]', 'pre': pre}
+            if PREXOR and k + 19 >= K:
+                col['px'] = pat(k + 19 - (K - 1))
+            cols.append(col)
+        columns(cols, carry_in=True)
+        # 4. ripple: v = (mask ^ P2c_19) + carry - 3, then limb / carry through V[73] (v2 value, v3 carry)
+        e(f'  v_xad_u32 v2, {V[57]}, {SMASK}, v{CARRY}')
+        rip = ['  v_add_u32_e32 v2, -3, v2']
+        for j in range(57, 2 * K):
+            px = pat(j - (K - 1)) if PREXOR else None
+            if j == 2 * K - 1:
+                rip.append(f'  v_xor_b32_e32 {V[j]}, {px}, v2' if px else f'  v_mov_b32_e32 {V[j]}, v2')
+                break
+            rip.append(f'  v_bitop3_b32 {V[j]}, v2, {SMASK}, {px} bitop3:0x6a' if px
+                       else f'  v_and_b32_e32 {V[j]}, {hex(MASK)}, v2')
+            rip.append('  v_lshrrev_b32_e32 v3, 28, v2')
+            rip.append(f'  v_xad_u32 v2, {V[j + 1]}, {SMASK}, v3')
+        return rip
+
     # SQR: V = 2 x0 x1, T = x0^2, reduce
     e('.Lsqr:')
     e('  s_mov_b32 s19, s15')
     e('.Lsqr_loop:')
     e('  s_cmp_eq_u32 s19, 0')
     e('  s_cbranch_scc1 .Lprog')
-    cols = []
-    for c in range(2 * K):
-        terms = [(X0[i], X1[c - i]) for i in range(K) if 0 <= c - i < K]
-        cols.append({'terms': terms, 'dbl': True, 'out': V[c], 'last': c == 2 * K - 1})
-        if PREXOR and c >= K:
-            cols[-1]['px'] = pat(c - (K - 1))
-    columns(cols)
+    rip = []
+    if KARA:
+        rip = kara_cross()
+    else:
+        cols = []
+        for c in range(2 * K):
+            terms = [(X0[i], X1[c - i]) for i in range(K) if 0 <= c - i < K]
+            cols.append({'terms': terms, 'dbl': True, 'out': V[c], 'last': c == 2 * K - 1})
+            if PREXOR and c >= K:
+                cols[-1]['px'] = pat(c - (K - 1))
+        columns(cols)
     cols = []
     for c in range(2 * K):
         terms = [(X0[i], X0[c - i]) for i in range(K) if i < c - i < K]
@@ -836,7 +953,7 @@ def gen_padic_mfma(name: str) -> str:
         elif sq:
             col['terms'] = [(sq, sq)]
         cols.append(col)
-    columns(cols)
+    columns(cols, bg=rip)
     phase()
     call('.Lreduce')
     phase()

@@ -541,6 +541,8 @@ class Wave:
                 r = (g(l, a[1]) << (g(l, a[2]) & 31)) + g(l, a[3])
             elif op == 'v_lshl_or_b32':
                 r = ((g(l, a[1]) << (g(l, a[2]) & 31)) | g(l, a[3]))
+            elif op == 'v_add_lshl_u32':
+                r = ((g(l, a[1]) + g(l, a[2])) & M32) << (g(l, a[3]) & 31)
             elif op == 'v_bfe_u32':
                 off, w = g(l, a[2]) & 31, g(l, a[3]) & 31
                 r = (g(l, a[1]) >> off) & ((1 << w) - 1)
@@ -779,6 +781,83 @@ def m37_selftest(seed=1, ab=None, bits=1024):
             if bad <= 3:
                 print(f"  lane {g_}: got {got:#x}\n   want {pow(xs[g_], 3, P2):#x}")
     print(f"m37 ({ab or 'default'}): 64 lanes, {bad} mismatches, {steps} wave-instructions emulated")
+    return bad
+
+
+def m37_digits_selftest(seed=1, ab=None, bits=1030):
+    """wave 0 of fthe_padic_m37 on crafted digit pairs (LOADX raw digits; SQR 1; SQR 1; STOREP): the squaring's
+    cross term at the extremes the kernel admits -- every limb < 2^28 and each digit < 5P, incl. digits whose
+    low 36 limbs are all 2^28 - 1 (the largest Karatsuba half sums and column sums), zero halves, one-limb
+    digits and random ones -- against (x0 + x1 P)^4 mod P^2 in Python integers"""
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
+    sys.path.insert(0, here)
+    import importlib
+    import gen_padic_mfma as gm
+    saved = os.environ.get("FTHE_GEN_M37_AB")
+    if ab is not None:
+        os.environ["FTHE_GEN_M37_AB"] = ab
+    try:
+        gm = importlib.reload(gm)
+        asm = gm.gen_padic_mfma('fthe_padic_m37')
+    finally:
+        if saved is None:
+            os.environ.pop("FTHE_GEN_M37_AB", None)
+        else:
+            os.environ["FTHE_GEN_M37_AB"] = saved
+        importlib.reload(gm)
+    import padic_mfma_model as mm
+    rng = random.Random(seed)
+    P = rng.getrandbits(bits) | (1 << (bits - 1)) | (1 << (bits - 2)) | 1
+    P2 = P * P
+    K, S, L, B = 37, 74, 256, 28
+    MASK = (1 << B) - 1
+    top = 5 * P - 1                                              # the largest digit
+    allones = (1 << (B * (K - 1))) - 1                           # limbs 0..35 = 2^28 - 1
+    big = allones + (((top - allones) >> (B * (K - 1))) << (B * (K - 1)))
+    assert big <= top
+    low19 = (1 << (B * 19)) - 1                                  # xL all ones, xH 0
+    high18 = big - (big & low19)                                 # xL 0, xH max
+    special = [big, 0, 1, low19, high18, top, P - 1, (1 << (B * 19)), MASK, big ^ (MASK << (B * 18))]
+    pairs = [(a, b) for a in special for b in special][:40]
+    while len(pairs) < 64:
+        pairs.append((rng.randrange(5 * P), rng.randrange(5 * P)))
+    nv = int(re.search(r'\.amdhsa_next_free_vgpr (\d+)', asm).group(1))
+    lds_bytes = int(re.search(r'\.amdhsa_group_segment_fixed_size (\d+)', asm).group(1))
+    ctx = bytearray(gm.TILE_OFF + gm.TILE_BYTES)
+    for j in range(K):
+        ctx[4 * j:4 * j + 4] = ((-((P >> (B * j)) & MASK)) & M32).to_bytes(4, 'little')
+    img = mm.MfmaKey(P).tile_image()
+    ctx[gm.TILE_OFF:gm.TILE_OFF + len(img)] = img
+    IN, OUT = 0, 1
+    slots = bytearray(2 * S * L * 4)
+    for g_, (x0, x1) in enumerate(pairs):
+        for k in range(K):
+            for d, x in ((0, x0), (K, x1)):
+                off = (IN * S + d + k) * L * 4 + 4 * g_
+                slots[off:off + 4] = ((x >> (B * k)) & MASK).to_bytes(4, 'little')
+    prog = [1, IN, 3, 2, 23, OUT, 0, 0]
+    mem = Mem()
+    SB, PB, CB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000
+    mem.alloc(slots, SB)
+    mem.alloc(b''.join(w.to_bytes(4, 'little') for w in prog), PB)
+    mem.alloc(bytes(ctx), CB)
+    karg = SB.to_bytes(8, 'little') + PB.to_bytes(8, 'little') + CB.to_bytes(8, 'little') + \
+        (L * 4).to_bytes(4, 'little') + (S * L * 4).to_bytes(4, 'little') + L.to_bytes(4, 'little') + \
+        (1).to_bytes(4, 'little') + bytes(128)
+    mem.alloc(karg, KA)
+    steps = run_workgroup(asm, lds_bytes, 4, mem, KA, 0, nv, finish=(0,))
+    bad = 0
+    for g_, (x0, x1) in enumerate(pairs):
+        got = 0
+        for k in reversed(range(S)):
+            got = (got << B) + mem.read(SB + (OUT * S + k) * L * 4 + 4 * g_, 4)
+        want = pow(x0 + x1 * P, 4, P2)
+        if not (got < 6 * P2 and got % P2 == want):
+            bad += 1
+            if bad <= 3:
+                print(f"  lane {g_}: got {got:#x}\n   want {want:#x}")
+    print(f"m37 digits ({ab or 'default'}): 64 lanes, {bad} mismatches, {steps} wave-instructions emulated")
     return bad
 
 
