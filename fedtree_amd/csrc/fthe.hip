@@ -186,6 +186,20 @@ size_t rowio_chunk_lanes() {
     return v;
 }
 
+// Large CRT encrypts with device randomness pipelined across chunks: the p half of chunk i + 1 starts as soon as
+// the p half of chunk i has finished (the q half and the recombination of chunk i still running on the side
+// stream), so the chip never drains between chunks; two slot-region pairs alternate (15 GB more at P-2048).
+// Measured neutral (2.721 / 2.707M vs 2.729 / 2.706M encrypts/s, profiles/r05j_enc_pipe_ab.jsonl): the split
+// chunks already keep the chip full -- a chunk's p and q launches share it until the last round of waves -- so
+// it is opt-in, FTHE_ENC_PIPE=1 (bit-identical, tests/test_gpu_split_streams.py).
+bool enc_pipe() {
+    static const bool v = [] {
+        const char *e = getenv("FTHE_ENC_PIPE");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
 // the key holder's large encrypt batches with device randomness (the direct-y path bench.py times) launch
 // twice chunk_lanes() per exponentiation: 786,432 lanes = six rounds of the P-adic kernel instead of three,
 // +1.5% encrypts/s (1.8% at 1,572,864; profiles/r04q_chunk_ab.jsonl); FTHE_ENC_CHUNK overrides
@@ -255,6 +269,7 @@ struct fthe_ctx {
     hipStream_t copy = nullptr;               // host<->device staging copies, overlapped with compute
     hipStream_t side = nullptr;               // second compute stream: the q half of small decrypts
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_cb[2] = {};                 // pipelined CRT encrypts: chunk i's recombination done (region i & 1)
     int n_cu = 256;                           // compute units (small-batch spreading)
     int static_lds[MAX_VARIANTS] = {};        // per-variant static LDS bytes per workgroup
     PinBuf stage_out[2], stage_in[2];
@@ -549,6 +564,7 @@ extern "C" int fthe_ctx_create(int device, fthe_ctx **out) {
     HIPOK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIPOK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIPOK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    for (auto &ev : c->ev_cb) HIPOK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     for (int i = 0; i < 2; i++) {
         HIPOK(hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
         HIPOK(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
@@ -609,6 +625,7 @@ extern "C" void fthe_ctx_destroy(fthe_ctx *c) {
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    for (auto &ev : c->ev_cb) if (ev) (void)hipEventDestroy(ev);
     for (int i = 0; i < 2; i++) {
         if (c->ev_done[i]) (void)hipEventDestroy(c->ev_done[i]);
         if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
@@ -1883,9 +1900,11 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     const bool small_split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
     const bool big_split = !quad && !small_split && direct_y && vi >= 0 && split_all();
     const bool split = small_split || big_split;
+    // big split calls of more than one chunk: chunks pipelined over two slot-region pairs (enc_pipe)
+    const bool piped = big_split && !pipe && !k->padic_own_slots && enc_pipe() && count > enc_chunk_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, crt ? k->spq : k->sn2,
+    int rc = begin_call(c, k, count, Lc, piped ? 4 * nsl : split ? 2 * nsl : nsl, crt ? k->spq : k->sn2,
                         direct_y && !small_split && !quad ? enc_chunk_lanes() : !crt && k->nadic_b ? pub_chunk_lanes() : 0);
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
@@ -1897,7 +1916,7 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     // keeps the explicit r (A/B).  Injected r always takes both stages (bit-exact).
     // scratch: AoS r words for the device RNG
     const int wl = (kLatShape.S * kLatShape.B + 31) / 32;   // u32 words of an s80 row
-    if (!r && (rc = c->scratch.ensure(std::max((size_t)L * nw * 4 * (direct_y ? 2 : 1),
+    if (!r && (rc = c->scratch.ensure(std::max((size_t)L * nw * 4 * (direct_y ? 2 : 1) * (piped ? 2 : 1),
                                                quad ? (size_t)L * (2 * k->pq_w + 2 * wl) * 4 : (size_t)0))))
         return rc;
     RngKey rk{};
@@ -1944,6 +1963,55 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
         Lc.fill(SL_T1, k->c_qinvRp2);
     } else {
         Lc.fill(SL_C0, k->c_R2n2); Lc.fill(SL_C1, k->c_nRn2);
+    }
+    if (piped) {
+        // region pair b = chunk & 1: the p half (main stream) on Rp[b], the q half and the recombination (side
+        // stream) on Rq[b].  Chunk i's p half waits only for the recombination of chunk i - 2 (the last user of
+        // its region pair and of its y buffers), so it runs beside the q half of chunk i - 1.
+        Launch Rp[2] = {Lc, Lc}, Rq[2] = {Lq, Lq};
+        Rp[1].base = (uint8_t *)Lc.base + (size_t)2 * nsl * S * L * 4;
+        Rq[1].base = (uint8_t *)Lc.base + (size_t)3 * nsl * S * L * 4;
+        Rp[1].fill(SL_C0, k->c_R2p); Rp[1].fill(SL_C1, k->c_nRp);
+        Rp[1].fill(SL_C2, k->c_R2q); Rp[1].fill(SL_C3, k->c_nRq);
+        Rp[1].fill(SL_T1, k->c_qinvRp2);
+        Rq[1].fill(SL_C2, k->c_R2q); Rq[1].fill(SL_C3, k->c_nRq);
+        double mm_tail = 0;
+        size_t i = 0;
+        for (size_t off = 0; off < count; off += L, i++) {
+            const int b = (int)(i & 1);
+            const size_t cnt = std::min((size_t)L, count - off);
+            Launch &P = Rp[b], &Q = Rq[b];
+            P.live = Q.live = cnt;
+            uint32_t *yp = (uint32_t *)c->scratch.p + (size_t)b * 2 * L * k->pq_w, *yq = yp + (size_t)L * k->pq_w;
+            RngKey rq = rk; rq.nonce ^= kYqStream;
+            if (i >= 2) HIPOK(hipStreamWaitEvent(c->stream, c->ev_cb[b], 0));
+            hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->stream, k->d_pqwords, k->pq_w, (int)k->p.bits(),
+                               rk, m.idx0 + off, cnt, yp);
+            m.pack(c->stream, Lc.grid(), off, cnt, P.slot(SL_IN1), S, L, Lc.B);
+            pack_rows(c->stream, yp, k->pq_w, cnt, 0, P.slot(SL_T3), S, L, Lc.B);
+            if ((rc = enc_stage_b(P, k, 0, true, &Lpa))) return rc;
+            HIPOK(hipEventRecord(c->ev_fork, c->stream));
+            hipLaunchKernelGGL(k_rng_r, Lc.grid(), dim3(256), 0, c->side, k->d_pqwords + k->pq_w, k->pq_w,
+                               (int)k->q.bits(), rq, m.idx0 + off, cnt, yq);
+            m.pack(c->side, Lc.grid(), off, cnt, Q.slot(SL_IN1), S, L, Lc.B);
+            pack_rows(c->side, yq, k->pq_w, cnt, 0, Q.slot(SL_T4), S, L, Lc.B);
+            if ((rc = enc_stage_b(Q, k, 1, false, &Lpaq))) return rc;
+            HIPOK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+            Launch T = P;                  // the recombination: P's slots, on the side stream
+            T.st = c->side; T.mm = 0;
+            hipLaunchKernelGGL(k_crt_prep_q, Lc.grid(), dim3(256), 0, c->side, Q.slot(SL_OUTQ), k->cst(k->c_q2),
+                               k->cst(k->c_2p2), P.slot(SL_T0), S, L, Lc.B);
+            if ((rc = T.prog(k->pr_enc_tail, k->mp2))) return rc;
+            mm_tail += T.mm;
+            hipLaunchKernelGGL(k_canon, Lc.grid(), dim3(256), 0, c->side, P.slot(SL_T2), k->cst(k->c_p2), S, L, Lc.B);
+            mul_add_out(c->side, Lc.grid(), Q.slot(SL_OUTQ), S, k->cst(k->c_q2), S, P.slot(SL_T2), S, L, cnt,
+                        out + off * cw, cw, (uint64_t *)nullptr, Lc.B);
+            HIPOK(hipEventRecord(c->ev_cb[b], c->side));
+        }
+        HIPOK(hipEventRecord(c->ev_join, c->side));
+        HIPOK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        Lc.mm = Rp[0].mm + Rp[1].mm + Rq[0].mm + Rq[1].mm + mm_tail;
+        return end_call(c, Lc);
     }
     for (size_t off = 0; off < count; off += L) {
         size_t cnt = std::min((size_t)L, count - off);

@@ -73,23 +73,36 @@ def test_split_injected_r_golden(dev):
 _SPLIT_ALL_PROBE = r'''
 import hashlib, sys
 import numpy as np
+import torch
 sys.path.insert(0, sys.argv[1])
 sys.path.insert(0, sys.argv[1] + "/tests")
 from conftest import golden_key, load_golden
 from fedtree_amd.paillier import Device, Paillier
 p, q = golden_key(load_golden("ref_gmp_L2048.json"))
 pl = Paillier.from_primes(p, q, Device(0))
-m = np.random.default_rng(5).integers(0, 2**64, int(sys.argv[2]), dtype=np.uint64)
-c = pl.encrypt_u64(m, seed=91)
+n = int(sys.argv[2])
+m = np.random.default_rng(5).integers(0, 2**64, n, dtype=np.uint64)
+c = pl.encrypt_u64(m, seed=91)                       # host rows (the staged path)
 ok = bool(np.array_equal(pl.decrypt_u64(c), m))
-print(hashlib.sha256(c.tobytes()).hexdigest(), ok)
+md = torch.from_numpy(m.view(np.int64)).cuda()       # device-resident (the bench's path: chunks pipelined)
+cd = torch.empty((n, 2 * pl.n_words), dtype=torch.int32, device="cuda")
+pl.encrypt_u64_dev(md, cd, seed=91)
+pl.dev.sync()
+cdh = cd.cpu().numpy().view(np.uint32)
+low = torch.empty(n, dtype=torch.int64, device="cuda")
+pl.decrypt_u64_dev(cd, low)
+pl.dev.sync()
+ok = ok and bool(np.array_equal(low.cpu().numpy().view(np.uint64), m))
+print(hashlib.sha256(c.tobytes()).hexdigest(), hashlib.sha256(cdh.tobytes()).hexdigest(), ok)
 '''
 
 
 def test_split_all_large_calls_bit_identical(tmp_path):
     """Large CRT encrypts and decrypts run each chunk's p and q halves side by side on two streams (fthe.hip
-    split_all, the default); FTHE_SPLIT_ALL=0 runs them in turn on one stream.  Two chunks of 786,432 lanes and a
-    partial third: the seeded ciphertexts are byte-identical both ways and decrypt to their plaintexts."""
+    split_all, the default), and under FTHE_ENC_PIPE=1 device-resident encrypts pipeline the chunks over two
+    slot-region pairs (enc_pipe, opt-in); FTHE_SPLIT_ALL=0 runs the halves in turn on one stream.
+    Three chunks of 786,432 lanes and a partial fourth, host rows and device rows: the seeded ciphertexts are
+    byte-identical all three ways (and host = device) and decrypt to their plaintexts."""
     import os
     import subprocess
     import sys
@@ -97,10 +110,12 @@ def test_split_all_large_calls_bit_identical(tmp_path):
     probe = tmp_path / "probe.py"
     probe.write_text(_SPLIT_ALL_PROBE)
     outs = []
-    for v in ("0", "1"):
-        r = subprocess.run([sys.executable, str(probe), root, str(2 * 786432 + 5000)], capture_output=True, text=True,
-                           timeout=600, env=dict(os.environ, FTHE_SPLIT_ALL=v))
+    for split, piped in (("0", "0"), ("1", "0"), ("1", "1")):
+        r = subprocess.run([sys.executable, str(probe), root, str(3 * 786432 + 5000)], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ, FTHE_SPLIT_ALL=split, FTHE_ENC_PIPE=piped))
         assert r.returncode == 0, r.stderr[-3000:]
         outs.append(r.stdout.split())
-    assert outs[0][1] == "True" and outs[1][1] == "True"
-    assert outs[0][0] == outs[1][0]
+    for o in outs:
+        assert o[2] == "True"
+        assert o[0] == o[1]                               # host rows = device rows
+    assert outs[0][0] == outs[1][0] == outs[2][0]
