@@ -176,7 +176,7 @@ def gen_addb(name: str) -> str:
     # s[36:37] y index list (0: direct rows), s[38:39] carry scratch of the gathered addresses
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
     LIVE = "s[28:29]"
-    NSGPR = 68 if "stamp" in DBG else 40
+    NSGPR = 68 if "stamp" in DBG else 42          # s[40:41]: the product steps' carry-out sink
 
     e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
     e('.amdhsa_code_object_version 5')
@@ -518,6 +518,11 @@ def gen_addb(name: str) -> str:
     # the multiplier prefetch after the step's ninth multiply-add (timing knob pfN: after the first measured no
     # faster, profiles/r05f_addb_libs_ab.jsonl)
     KARA_PF = next((int(t[2:]) for t in DBG if t.startswith('pf') and t[2:].isdigit()), 8)
+    # P1 retires lane 0's column into its quad lane's register with one v_cndmask_b32 whose src0 is the DPP
+    # broadcast of lane 0 (vcc = the lanes that keep theirs: the steps' multiply-adds write their carry-outs,
+    # always 0, to s[40:41] instead of vcc); "nocnd" keeps the broadcast + v_cndmask_b32_e64 pair (A/B)
+    CND = "nocnd" not in DBG and "stamp" not in DBG            # (the stamp build's timers live in s[40:..])
+    CSINK = "s[40:41]" if CND else "vcc"
     HALF = S // 2                                 # 76
     XW = {"L": 46, "H": 65, "S": 84}              # 19-limb windows of xL, xH, xL + xH (later P0 / P2 / P1 high)
     HO2 = 104                                     # hand-off pair v[104:105] (v105 stays 0)
@@ -550,7 +555,7 @@ def gen_addb(name: str) -> str:
         for k in range(Q2):
             if "noprod" not in DBG:
                 src2 = pair(HO2) if k == Q2 - 1 else T2(u + k)
-                e(f'  v_mad_u64_u32 {T2(u + k)}, vcc, {ai}, {W(k)}, {src2}')
+                e(f'  v_mad_u64_u32 {T2(u + k)}, {CSINK}, {ai}, {W(k)}, {src2}')
             if k == 2:
                 e(f'  v_lshrrev_b64 {tmp}, {B}, {T2(u)}')
             if k == 5:
@@ -566,13 +571,18 @@ def gen_addb(name: str) -> str:
                 e('  s_mov_b64 exec, s[22:23]')
                 e(f'  ds_write_b32 v{V_LDSI}, {T2lo(u)} offset:{(u if mode == "P0" else HALF + u) * RB}')
                 e('  s_mov_b64 exec, -1')
-            if k == 13 and mode == "P1":
+            if k == 13 and mode == "P1" and not CND:
                 e(f'  v_mov_b32_dpp v{RT}, {T2lo(u)} quad_perm:[0,0,0,0] {DPP}')
             if k == 16 and mode == "P1":
-                e(f'  v_cndmask_b32_e64 v{P1L + u % Q2}, v{P1L + u % Q2}, v{RT}, s[38:39]')
+                if CND:
+                    e(f'  v_cndmask_b32_dpp v{P1L + u % Q2}, {T2lo(u)}, v{P1L + u % Q2}, vcc quad_perm:[0,0,0,0] {DPP}')
+                else:
+                    e(f'  v_cndmask_b32_e64 v{P1L + u % Q2}, v{P1L + u % Q2}, v{RT}, s[38:39]')
         e(f'  v_and_b32_dpp v{HO2}, {T2lo(u)}, v{VMASK} quad_perm:[1,2,3,0] {DPP}')
         if mode == "P1" and u % Q2 == Q2 - 1:
             e('  s_lshl_b64 s[38:39], s[38:39], 1')          # the next trip's quad lane
+            if CND:
+                e('  s_not_b64 vcc, s[38:39]')
         e(f'  s_waitcnt lgkmcnt({0 if mode == "P1" else 1})')
 
     def kara_pass(mode, W, out, top=None):
@@ -586,6 +596,8 @@ def gen_addb(name: str) -> str:
         if mode == "P1":
             e(f'  ds_read_b32 v{BI[0]}, v{V_LDSI} offset:{HALF * RB}')
             e('  s_mov_b64 s[38:39], s[22:23]')                  # trip 0: quad lane 0
+            if CND:
+                e('  s_not_b64 vcc, s[38:39]')
         if mode == "P2":
             e(f'  ds_read_b32 v{V_AI[0]}, v{V_LDSI} offset:{HALF * RB}')
         e('  s_waitcnt lgkmcnt(0)')
@@ -738,7 +750,91 @@ def gen_addb(name: str) -> str:
     e('  s_waitcnt lgkmcnt(0)')
 
     # ---- 5/6. the two MFMA products, each folded chunk by chunk into DQ (quad lane j: chunk j) ----------
+    # three accumulator sets (the third in GB, free outside the normalisation): the tiles of a chunk pair as one
+    # stream, tile n - 2 folded right after tile n's first MFMA, so its results have long been written and the
+    # fold waits only for the wait states still missing (as fthe_nadic_b76, gen_nadicb.py); "acc2" keeps two
+    # sets with the fold of tile n - 1 behind fixed s_nop padding (A/B)
+    ACCS = ACC + (GB,) if "acc2" not in DBG else ACC
+    NACC = len(ACCS)
+    XDL_WAIT = 19                                 # wait states after an MFMA before a VALU reads its result
+
+    def mfma_product3(prod):
+        A = V_A1 if prod == 1 else V_A2
+        KO = KO1 if prod == 1 else KO2
+        act = ACT1 if prod == 1 else ACT2
+        corr = 0 if prod == 1 else CORR2_OFF - CORR1_OFF
+        e(f'  v_mov_b32_e32 v{CR}, 0')
+        for jp in range(0, len(CHUNKS), 2):
+            t0 = CHUNKS[jp][0]
+            tiles = tuple(CHUNKS[jp]) + tuple(CHUNKS[jp + 1])
+            ops = [(n, t, kb) for n, t in enumerate(tiles) for kb in act[t]]
+            q = []                                   # outstanding LDS ops, oldest first (tags)
+
+            def issue(tag, ins):
+                e(ins)
+                q.append(tag)
+
+            def wait_for(tag):
+                if tag not in q:
+                    return
+                i = q.index(tag)
+                e(f'  s_waitcnt lgkmcnt({min(len(q) - i - 1, 15)})')
+                del q[:i + 1]
+
+            def read_a(x):
+                n, t, kb = ops[x]
+                off = KO + 16 * (4 * kb - t)
+                assert 0 <= off and off + 48 + 16 <= COPY
+                issue(('a', x), f'  ds_read_b128 {quad4(AOP[x % 4])}, v{A} offset:{off}')
+
+            def read_corr(n, t):
+                issue(('c', n), f'  ds_read_b128 {quad4(ACCS[n % NACC])}, v{V_C} offset:{corr + 64 * t}')
+
+            last_mfma = {}
+
+            def settle(n):
+                """wait states before a VALU read of tile n's accumulators: one per instruction issued since"""
+                since = sum(1 for ln in o[last_mfma[n] + 1:] if ln.startswith('  '))
+                need = XDL_WAIT - since
+                while need > 0:
+                    e(f'  s_nop {min(need, 8) - 1}')
+                    need -= 8
+
+            for n in range(min(NACC, len(tiles))):
+                read_corr(n, tiles[n])
+            for x in range(min(3, len(ops))):
+                read_a(x)
+            for x, (n, t, kb) in enumerate(ops):
+                first = x == 0 or ops[x - 1][0] != n
+                if first:
+                    wait_for(('c', n))
+                wait_for(('a', x))
+                if "nomfma" not in DBG:
+                    e(f'  v_mfma_i32_16x16x64_i8 {quad4(ACCS[n % NACC])}, {quad4(AOP[x % 4])}, {quad4(BQ + 4 * kb)}, '
+                      f'{quad4(ACCS[n % NACC])}')
+                last_mfma[n] = len(o) - 1
+                if x + 3 < len(ops):                 # the buffer MFMA x - 1 read at its issue
+                    read_a(x + 3)
+                if first and n >= NACC - 1:
+                    m = n - (NACC - 1)
+                    settle(m)
+                    fold_tile(ACCS[m % NACC], 4 * (tiles[m] - t0))
+                    q.append(('w', m))
+                    if m + NACC < len(tiles):
+                        read_corr(m + NACC, tiles[m + NACC])
+            for m in range(max(0, len(tiles) - (NACC - 1)), len(tiles)):
+                settle(m)
+                fold_tile(ACCS[m % NACC], 4 * (tiles[m] - t0))
+            e('  s_waitcnt lgkmcnt(0)')
+            e('// @phase norm')
+            if "nonorm" not in DBG:
+                norm_pair(jp, jp + 1)
+            e(f'// @phase prod{prod}')
+
     def mfma_product(prod):
+        if NACC == 3:
+            mfma_product3(prod)
+            return
         """The tiles of one product chunk by chunk: every A read is issued two MFMAs ahead into one of four
         buffers, each tile's corrections (srcC) into its accumulator set right after the fold of the tile
         that used the set last, and s_waitcnt lgkmcnt(n) waits for exactly the read an MFMA needs (LDS

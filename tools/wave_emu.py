@@ -214,6 +214,16 @@ class Wave:
                 assert self.exec >> sl & 1, "DPP source lane disabled"
                 self.v[dst][l] = old[sl] & om[l]
             return
+        if op == 'v_cndmask_b32_dpp':              # dst = vcc ? src1 : dpp(src0)
+            perm = [int(x) for x in re.search(r'quad_perm:\[([0-9,]+)\]', ' '.join(a)).group(1).split(',')]
+            assert a[3] == 'vcc'
+            src, s1, dst = self.rr(a[1])[1], self.rr(a[2])[1], self.rr(a[0])[1]
+            old, o1 = list(self.v[src]), list(self.v[s1])
+            for l in self.lanes():
+                sl = (l & ~3) + perm[l & 3]
+                assert self.exec >> sl & 1, "DPP source lane disabled"
+                self.v[dst][l] = o1[l] if (self.vcc >> l) & 1 else old[sl]
+            return
         if op == 'v_mov_b32_dpp':
             perm = [int(x) for x in re.search(r'quad_perm:\[([0-9,]+)\]', ' '.join(a)).group(1).split(',')]
             src = self.rr(a[1])[1]
@@ -441,15 +451,19 @@ class Wave:
                 self.vset(l, a[0], r)
             return
         if op in ('v_mad_u64_u32', 'v_mad_i64_i32'):
-            newvcc = self.vcc
+            cmask = 0                                   # the carry-out / overflow mask written to sdst (a[1])
             for l in lanes:
                 x, y = g(l, a[2]), g(l, a[3])
                 c = g(l, a[4], 2)
                 if op == 'v_mad_i64_i32':
                     r = s32(x) * s32(y) + s64(c)
+                    ov = not (-(1 << 63) <= r < (1 << 63))
                 else:
                     r = x * y + c
+                    ov = r >> 64 != 0
+                cmask |= int(ov) << l
                 self.vset(l, a[0], r & M64)
+            self.sset(a[1], cmask)
             return
         if op in ('v_sub_co_u32_e32', 'v_subb_co_u32_e32', 'v_subb_co_u32_e64'):
             nv = self.vcc
