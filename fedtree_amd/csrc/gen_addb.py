@@ -921,10 +921,19 @@ def gen_addb(name: str) -> str:
         e(f'  v_cndmask_b32_e64 v{CR2}, v{CR2}, 0, {LANE_MASK[jb]}')          # lane jb: 0
         e('  s_mov_b64 exec, s[16:17]')
         cv = f"v{CR2}"
+        ng = max(na, nb)
+        if "norm1" not in DBG:
+            cv = norm_two_chains(ja, jb, na, ng, cv)
+        else:
+            cv = norm_one_chain(ja, jb, na, nb, ng, cv)
+        e('  s_mov_b64 exec, s[16:17]')
+        e(f'  v_mov_b32_e32 v{CR}, {cv}')
+        e('  s_mov_b64 exec, -1')
+        lane_delivery(ja, jb, nb)
 
+    def norm_one_chain(ja, jb, na, nb, ng, cv):
         def rd(g):
             e(f'  ds_read_b128 v[{GB + 4 * ((g // 2) % 2)}:{GB + 4 * ((g // 2) % 2) + 3}], v{V_GR} offset:{8 * g}')
-        ng = max(na, nb)
         rd(0)
         rd(2)
         for g0 in range(0, ng, 2):
@@ -943,9 +952,91 @@ def gen_addb(name: str) -> str:
             if g0 + 4 < ng:
                 rd(g0 + 4)
         assert cv == f"v{FV + 1}"
+        return cv
+
+    def norm_two_chains(ja, jb, na, ng, cv):
+        """each lane's chain split in two interleaved halves (half the dependent v_mad_i64_i32 latency, as
+        fthe_nadic_b76's normalisation): A = groups 0..15 from the lane's carry-in, B = groups 16.. from 0; then
+        A's carry-out is added to B's lowest dword, the rare signed overflow rippling through B's dwords on a slow
+        path into B's carry-out, which is returned (the lane's final carry)"""
+        H = 16
+        q = []
+
+        def rd(g, tag):
+            b = GB + (8 if g >= H else 0) + 4 * ((g // 2) % 2)
+            e(f'  ds_read_b128 v[{b}:{b + 3}], v{V_GR} offset:{8 * g}')
+            q.append(tag)
+
+        def wait_for(tag):
+            if tag in q:
+                i = q.index(tag)
+                e(f'  s_waitcnt lgkmcnt({min(len(q) - i - 1, 15)})')
+                del q[:i + 1]
+
+        def link(g, cvx, tmp):
+            """group g into dword g: even g -> the pair (DQ g, DQ g+1), odd g through tmp; the next carry"""
+            src = pair(GB + (8 if g >= H else 0) + 4 * ((g // 2) % 2) + 2 * (g % 2))
+            if g % 2 == 0:
+                e(f'  v_mad_i64_i32 {pair(DQ + g)}, vcc, {cvx}, 1, {src}')
+                return f"v{DQ + g + 1}"
+            e(f'  v_mad_i64_i32 {pair(tmp)}, vcc, {cvx}, 1, {src}')
+            e(f'  v_mov_b32_e32 v{DQ + g}, v{tmp}')
+            return f"v{tmp + 1}"
+        for g in (0, 2, H, H + 2):
+            rd(g, g)
+        ca, cb = cv, "0"
+        for i in range(0, max(H, ng - H), 2):
+            if H + i == na and ng > na:               # only lane jb's chunk has groups here (A is done)
+                e(f'  s_mov_b64 exec, {LANE_MASK[jb]}')
+            if i < H:
+                wait_for(i)
+                ca = link(i, ca, FV)
+                ca = link(i + 1, ca, FV)
+                if i + 4 < H:
+                    rd(i + 4, i + 4)
+            if H + i < ng:
+                wait_for(H + i)
+                cb = link(H + i, cb, PG)
+                cb = link(H + i + 1, cb, PG)
+                if H + i + 4 < ng:
+                    rd(H + i + 4, H + i + 4)
+        assert ca == f"v{FV + 1}" and cb == f"v{PG + 1}"
         e('  s_mov_b64 exec, s[16:17]')
-        e(f'  v_mov_b32_e32 v{CR}, {cv}')
-        e('  s_mov_b64 exec, -1')
+        # A's carry into B's lowest dword (both lanes), the overflow rippling on a slow path
+        X, TP = CR + 1, V_TMP
+        lab = f'.Lnc{len(o)}'
+        e(f'  v_mov_b32_e32 v{TP}, v{DQ + H}')
+        e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+        e(f'  v_mad_i64_i32 {pair(TP)}, vcc, {ca}, 1, {pair(TP)}')
+        e(f'  v_mov_b32_e32 v{DQ + H}, v{TP}')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{TP + 1}')
+        e('  s_nop 4')
+        if "slowall" in DBG:                          # test build: every lane through the slow path (carry 0: no-op)
+            e('  s_mov_b64 vcc, exec')
+        else:
+            e(f'  s_cbranch_vccz {lab}_done')
+        e('  s_and_saveexec_b64 s[38:39], vcc')                              # the overflowing lanes
+        e(f'  v_mov_b32_e32 v{X}, v{TP + 1}')
+
+        def ripple(lo, hi):
+            for i in range(lo, hi):
+                e(f'  v_mov_b32_e32 v{TP}, v{DQ + i}')
+                e(f'  v_mov_b32_e32 v{TP + 1}, 0')
+                e(f'  v_mad_i64_i32 {pair(TP)}, vcc, v{X}, 1, {pair(TP)}')
+                e(f'  v_mov_b32_e32 v{DQ + i}, v{TP}')
+                e(f'  v_mov_b32_e32 v{X}, v{TP + 1}')
+        ripple(H + 1, na)
+        if ng > na:                                   # lane jb's dwords na.. (lane ja's carry goes in first)
+            e(f'  s_and_b64 s[40:41], exec, {LANE_MASK[ja]}')
+            e(f'  s_andn2_b64 exec, exec, {LANE_MASK[ja]}')
+            ripple(na, ng)
+            e('  s_or_b64 exec, exec, s[40:41]')
+        e(f'  v_add_u32_e32 {cb}, v{X}, {cb}')
+        e('  s_mov_b64 exec, s[38:39]')
+        e(f'{lab}_done:')
+        return cb
+
+    def lane_delivery(ja, jb, nb):
         # lane ja's carry-out into lane jb's lowest dword
         X, TP = CR + 1, V_TMP
         lab = f'.Lnp{len(o)}'
