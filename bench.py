@@ -753,6 +753,9 @@ def run(a, world):
                     "issue them (host rows in and out, one four-lane product launch per merged batch); the "
                     "batch entry points (merge, histogram, reduce_segments) are the throughput path; Python "
                     "threads (GIL between calls): the C++ OpenMP rate is histogram_loop_unchanged_callers"}
+        # the native tools below run the drop-in on this rank's GPU only (FTHE_DEVICES defaults to every visible
+        # GPU: on a multi-GPU node an N = 1 run would otherwise shard them over the whole node)
+        one_gpu_env = dict(os.environ, FTHE_DEVICES=str(local))
         # the same operators from C++ OpenMP threads, as FedTree's histogram loop issues them unchanged
         # (integration/ghpair_rate.cpp, hist_tree_builder.cpp:572-591): a child process, its own context
         exe = os.path.join(ROOT, "tools", "bin", "ghpair_rate")
@@ -768,7 +771,7 @@ def run(a, world):
         for thr in (16, 64):
             try:
                 r = subprocess.run([exe, str(KEY_BITS), str(thr), "8192", "16", "4096"], capture_output=True,
-                                   text=True, timeout=180)
+                                   text=True, timeout=180, env=one_gpu_env)
                 hl[f"threads_{thr}"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                     {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
             except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
@@ -778,7 +781,7 @@ def run(a, world):
         # mpz_t marshalling of every ciphertext (integration/ghpair_e2e.cpp; server.h:105-135)
         try:
             r = subprocess.run([os.path.join(ROOT, "tools", "bin", "ghpair_e2e"), str(KEY_BITS), "2000000", "2"],
-                               capture_output=True, text=True, timeout=240)
+                               capture_output=True, text=True, timeout=240, env=one_gpu_env)
             ge = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                 {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
         except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
