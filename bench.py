@@ -657,6 +657,16 @@ def run(a, world):
         pl.encrypt_u64_dev(m[:npub], c[:npub], seed=5, public=True)
         dev.sync()
         secondary["public_encrypt_per_s"] = round(npub / (lib.fthe_last_kernel_ms(dev.ctx) * 1e-3))
+        # fthe_nadic_b76's issue: its VALU wave-instructions per ciphertext (PMC, one 98,304-ciphertext launch) x 4
+        # cycles at this rate over every SIMD's cycles -- the public path's counterpart of roofline.issue_frac
+        pb = pmc.get("pub", {}).get("fthe_nadic_b76", {})
+        if pb.get("SQ_INSTS_VALU"):
+            per_ct = pb["SQ_INSTS_VALU"] / 98304
+            secondary["public_encrypt_issue"] = {
+                "valu_wave_instr_per_ciphertext": round(per_ct),
+                "valu_issue_frac": round(per_ct * secondary["public_encrypt_per_s"] * 4 / (1024 * 2.4e9), 4),
+                "valu_busy_pct": pb.get("VALUBusy"), "occupancy_pct": pb.get("OccupancyPercent"),
+                "source": f"profiles/{PMC_FILE} pub"}
         t0 = time.perf_counter()
         pl.set_fixed_base(None)
         fb_build_s = time.perf_counter() - t0
@@ -938,6 +948,12 @@ def run(a, world):
                                       "valu_macs_per_add": valu_macs,
                                       "executed_over_algorithmic_macs": round(valu_macs / (2 * 128 * 128 + 128), 3),
                                       "valu_frac_executed": round(rate * valu_macs / PEAK_MAC_S, 4),
+                                      # issue: the kernel's VALU wave-instructions per add (PMC) x 4 cycles at
+                                      # this rate over every SIMD's cycles (as roofline.issue_frac)
+                                      "valu_issue_frac": (round(pk["SQ_INSTS_VALU"] / pk["rows_out_per_launch"] * rate
+                                                                * 4 / (1024 * 2.4e9), 4)
+                                                          if pk.get("SQ_INSTS_VALU") and pk.get("rows_out_per_launch")
+                                                          else None),
                                       "valu_frac_survey_unit": round(rate * (2 * 128 * 128 + 128) / PEAK_MAC_S, 4),
                                       "matrix_core": {"i8_macs_per_add": round(i8_macs),
                                                       "frac_of_i8_dense_peak": round(rate * i8_macs * 2 / i8_peak, 4)}}
