@@ -218,6 +218,20 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e('  s_load_dwordx2 s[42:43], s[0:1], 0x20')                         # live ciphertexts, workgroups launched
     e('  s_waitcnt lgkmcnt(0)')
     e('  s_barrier')
+    # desyncN (timing knob): the waves w, w + 4, w + 8 of a workgroup share a SIMD; the second and third start
+    # N and 2N s_sleep 127 (~8K cycles each) late, so their matrix phases meet the others' product passes.
+    # Measured neutral to slower (659-661 vs 657.6-658.1 ms per 393,216, profiles/r05t_nadicb_desync_ab.jsonl):
+    # the persistent waves' batch draws already spread their phases, so off
+    DSN = next((int(t[6:]) for t in DBG if t.startswith('desync') and t[6:].isdigit()), 0)
+    if DSN:
+        e(f'  v_readfirstlane_b32 s44, v{V_LANE}')
+        e('  s_lshr_b32 s44, s44, 8')                                         # wave / 4 = slot on its SIMD
+        for k in (1, 2):
+            e(f'  s_cmp_lt_u32 s44, {k}')
+            e(f'  s_cbranch_scc1 .Ldesync_{k}')
+            for _ in range(DSN):
+                e('  s_sleep 127')
+            e(f'.Ldesync_{k}:')
     e('// @stampinit')
     e('  s_add_u32 s44, s42, 15')
     e('  s_lshr_b32 s44, s44, 4')                                         # batches of 16 ciphertexts
