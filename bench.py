@@ -287,7 +287,7 @@ def compact_line(full):
     ah = sec.get("p2048_add_hbm")
     if isinstance(ah, dict):
         sec["p2048_add_hbm"] = {k: ah[k] for k in ("algorithmic_GBps", "pmc_GBps_calibrated", "pmc_VALUBusy",
-                                                   "valu_frac_executed", "matrix_core") if k in ah}
+                                                   "valu_frac_executed", "valu_issue_frac", "matrix_core") if k in ah}
     for k in ("ghpair_e2e", "ghpair_e2e_sharded"):
         if isinstance(sec.get(k), dict):
             sec[k] = {x: sec[k][x] for x in ("encrypts_per_s", "decrypts_per_s", "ok", "shards", "error") if x in sec[k]}
