@@ -288,9 +288,10 @@ def compact_line(full):
     if isinstance(ah, dict):
         sec["p2048_add_hbm"] = {k: ah[k] for k in ("algorithmic_GBps", "pmc_GBps_calibrated", "pmc_VALUBusy",
                                                    "valu_frac_executed", "valu_issue_frac", "matrix_core") if k in ah}
-    for k in ("ghpair_e2e", "ghpair_e2e_sharded"):
+    for k in ("ghpair_e2e", "ghpair_e2e_sharded", "ghpair_e2e_node"):
         if isinstance(sec.get(k), dict):
-            sec[k] = {x: sec[k][x] for x in ("encrypts_per_s", "decrypts_per_s", "ok", "shards", "error") if x in sec[k]}
+            sec[k] = {x: sec[k][x] for x in ("encrypts_per_s", "decrypts_per_s", "ok", "shards", "pairs", "devices",
+                                              "error") if x in sec[k]}
     if isinstance(sec.get("wire"), dict):
         sec["wire"] = {k: v for k, v in sec["wire"].items() if k.endswith("_per_s") or k.endswith("_ok")
                        or k.endswith("_host")}
@@ -410,6 +411,59 @@ def rank_adds(call, count, world, rank, sync):
                     "aggregate = ranks x adds / slowest rank"}
 
 
+def host_mem_bytes():
+    """Host memory this process may still use: MemAvailable, bounded by the cgroup's limit less its usage."""
+    avail = None
+    try:
+        for ln in open("/proc/meminfo"):
+            if ln.startswith("MemAvailable:"):
+                avail = int(ln.split()[1]) * 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    try:
+        lim = open("/sys/fs/cgroup/memory.max").read().strip()
+        if lim != "max":
+            cur = int(open("/sys/fs/cgroup/memory.current").read())
+            room = int(lim) - cur
+            avail = room if avail is None else min(avail, room)
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+# host bytes per pair of a ghpair_e2e batch: two 4096-bit mpz (limbs + allocator), the GHPair, and the pinned
+# plaintext and ciphertext rows (2 x 8 B + 2 x 512 B)
+E2E_HOST_BYTES_PER_PAIR = 2300
+
+
+def node_e2e(a, world, devices, rehearse):
+    """ghpair_e2e over every device of the run in one process (integration/ghpair_e2e.cpp): 10M pairs per device
+    (FTHE_BENCH_NODE_PAIRS overrides), fewer when the host cannot hold the batch in 40% of its free memory; one rep,
+    every plaintext checked.  FTHE_BENCH_REHEARSE: every shard on device 0."""
+    per_dev = int(os.environ.get("FTHE_BENCH_NODE_PAIRS") or 10_000_000)
+    mem = host_mem_bytes()
+    if mem:
+        per_dev = min(per_dev, int(0.4 * mem / E2E_HOST_BYTES_PER_PAIR / world))
+    per_dev = max(per_dev, 1 << 14)
+    devs = ",".join("0" for _ in devices) if rehearse else ",".join(str(d) for d in sorted(devices))
+    exe = os.path.join(ROOT, "tools", "bin", "ghpair_e2e")
+    out = {"devices": devs, "pairs_per_device": per_dev, "host_mem_free_bytes": mem}
+    t0 = time.perf_counter()
+    try:
+        env = dict(os.environ, FTHE_SHIM_REPLICATE="1" if rehearse else "0")
+        r = subprocess.run([exe, str(KEY_BITS), str(per_dev * world), "1", devs], capture_output=True, text=True,
+                           timeout=900, env=env)
+        res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+            {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+    except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
+        res = {"error": repr(ex)[:300]}
+    out.update(res)
+    out["wall_s"] = round(time.perf_counter() - t0, 1)
+    if "encrypts_per_s" in out:
+        out["encrypts_per_s_per_device"] = round(out["encrypts_per_s"] / world)
+    return out
+
+
 def run(a, world):
     import torch
     import torch.distributed as dist
@@ -423,11 +477,14 @@ def run(a, world):
         local = 0
     if world > 1:
         torch.cuda.set_device(local)
+        # a long timeout: the ranks wait at the final barrier while rank 0 runs its CPU baseline and the node-wide
+        # drop-in pass (ghpair_e2e_node), minutes at N = 8
+        from datetime import timedelta
         if rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timedelta(minutes=60))
         else:
             # RCCL carries only the barriers and the max-over-ranks gathers: no data-path collective
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timedelta(minutes=60))
     from fedtree_amd.paillier import Device, Paillier
     from fedtree_amd.synth import logistic_gradients
     from fedtree_amd import _lib
@@ -777,11 +834,15 @@ def run(a, world):
                       "sub: the sibling subtraction (hist_tree_builder.cpp:672-680), OpenMP over 4,096 bins, "
                       "`dest[i] = father[i] - child[i]` through GHPair::operator- (2 x mul(x, 2^64-1) + 2 adds; a "
                       "single-element mul is a host mpz_powm, as paillier_gpu.cu:65-67), every bin decrypted; "
-                      "reference_sub_same_threads_per_s: mpz_powm + mpz_mul/mpz_mod on the same threads and operands"}
-        for thr in (16, 64):
+                      "reference_sub_same_threads_per_s: mpz_powm + mpz_mul/mpz_mod on the same threads and operands; "
+                      "both legs interleaved over 7 rounds at the lease's core count, rates from the medians, "
+                      "vs_reference_* the median per-round ratio"}
+        # at the lease's core count only (an oversubscribed 64-thread leg on a 16-core quota measured the host
+        # scheduler, 0.43-1.10x between runs); both legs interleaved, 7 rounds, the median per-round ratio
+        for thr in (host_cpu()["threads_used"],):
             try:
-                r = subprocess.run([exe, str(KEY_BITS), str(thr), "8192", "16", "4096"], capture_output=True,
-                                   text=True, timeout=180, env=one_gpu_env)
+                r = subprocess.run([exe, str(KEY_BITS), str(thr), "8192", "16", "4096", "7"], capture_output=True,
+                                   text=True, timeout=240, env=one_gpu_env)
                 hl[f"threads_{thr}"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
                     {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
             except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
@@ -1118,6 +1179,13 @@ def run(a, world):
             ca.cpu_scale = a.cpu_scale / 4             # N > 1: a quarter sample keeps the scaling runs short
         cpu = cpu_baseline(ca, pl, p1k_cpu, m, c, dev)
         cpu["n_gpus_of_run"] = world
+
+    if rank == 0 and world > 1 and not a.no_secondary:
+        # configs[4] through the class FedTree calls: Server::encrypt_gh_pairs / decrypt_gh_pairs on one
+        # SyncArray<GHPair> of N x (pairs per device), Paillier_HIP sharding it over every device of the run in one
+        # process (ShardPool: a worker thread, context and key replica per device, host rows in and out), in a
+        # fresh child while the other ranks wait at the final barrier (their own buffers stay allocated)
+        secondary["ghpair_e2e_node"] = node_e2e(a, world, [p["device"] for p in per_rank], rehearse)
 
     if rank == 0:
         line = {

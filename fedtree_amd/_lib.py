@@ -49,6 +49,7 @@ _PROTOS = {
     "fthe_ctx_sync": (_I, [_P]),
     "fthe_ctx_stream": (_P, [_P]),
     "fthe_ctx_device": (_I, [_P]),
+    "fthe_ctx_set_mem_limit": (_I, [_P, _SZ]),
     "fthe_host_alloc": (_I, [_SZ, _PP]),
     "fthe_debug_addb_image": (_I, [_P, _I, _P, _SZ, _P]),
     "fthe_debug_nadicb_image": (_I, [_P, _I, _P, _SZ, _P]),
@@ -67,6 +68,7 @@ _PROTOS = {
     "fthe_key_fixed_base_info": (_I, [_P, _P, _P, _P]),
     "fthe_key_fixed_base_exact": (_I, [_P, _P, _U64]),
     "fthe_key_fixed_base_exact_info": (_I, [_P, _I, _I, _P, _P]),
+    "fthe_key_fixed_base_exact_set": (_I, [_P, _P, _I, _P]),
     "fthe_key_fixed_base_exact_bases": (_I, [_P]),
     "fthe_next_prime": (_I, [_P, _I, _P, _I]),
     "fthe_key_public_bases": (_I, [_P, _U64, _P, _P, _P]),

@@ -143,7 +143,9 @@ size_t chunk_lanes() {
 // two streams, so the two launches share the chip: the waves of a batch that is not a whole number of
 // rounds per half (200,000 Paillier-1024 ciphertexts: 3,125 waves per half, 3,072 resident) fill one
 // tail instead of two -- 16.4 ms instead of 19.4 ms, and 91.7 ms instead of 106.7 ms at Paillier-2048
-// (profiles/r02zzn_split_*.jsonl).  Default: one chunk; FTHE_DEC_SPLIT overrides, 0 turns it off (A/B).
+// (profiles/r02zzn_split_*.jsonl).  Default: one chunk; FTHE_DEC_SPLIT overrides, 0 turns this small-batch split
+// off.  Larger calls split as well while split_all() is on (the default), so a one-stream A/B needs
+// FTHE_DEC_SPLIT=0 and FTHE_SPLIT_ALL=0 together.
 size_t dec_split_lanes() {
     static size_t v = [] {
         const char *e = getenv("FTHE_DEC_SPLIT");
@@ -281,6 +283,7 @@ struct fthe_ctx {
     uint32_t *d_jobctr = nullptr;             // job counters of persistent launches (one per launch, in turn)
     unsigned jobctr_i = 0;
     DevBuf slots, slots1, scratch, io[5];   // slots1: the small-modulus (mod p, q) programs
+    size_t mem_limit = 0;                   // fthe_ctx_set_mem_limit: cap on the slot region grown for a call
     DevBuf hb[6];                           // histogram CSR / segmented-product plan (device)
     DevBuf ezm;                             // zero-first folds: Enc(0) rows masked to the populated segments
     DevBuf dec[3];                          // decimal codec: 9-digit chunks, lengths, leading chunk / error flag
@@ -642,6 +645,12 @@ extern "C" int fthe_ctx_sync(fthe_ctx *c) {
 }
 extern "C" void *fthe_ctx_stream(fthe_ctx *c) { return c ? (void *)c->stream : nullptr; }
 extern "C" int fthe_ctx_device(fthe_ctx *c) { return c ? c->device : -1; }
+
+extern "C" int fthe_ctx_set_mem_limit(fthe_ctx *c, size_t bytes) {
+    if (!c) return FTHE_ERR_ARG;
+    c->mem_limit = bytes;
+    return FTHE_OK;
+}
 
 extern "C" double fthe_last_kernel_ms(fthe_ctx *c) {
     if (!c || !c->timed) return 0.0;
@@ -1675,7 +1684,9 @@ int begin_call(fthe_ctx *c, const fthe_key *k, size_t count, Launch &Lc, int nsl
     size_t L = std::min(ch, (count + q - 1) / q * q);
     if (L == 0) L = q;
     Lc.c = c; Lc.k = k; Lc.L = (int)L; Lc.S = sh.S; Lc.B = sh.B;
-    int rc = c->slots.ensure((size_t)nslots * sh.S * L * 4);
+    const size_t need = (size_t)nslots * sh.S * L * 4;
+    if (c->mem_limit && need > c->mem_limit && need > c->slots.n) return FTHE_ERR_NOMEM;
+    int rc = c->slots.ensure(need);
     Lc.base = c->slots.p;
     if (rc) return rc;
     HIPOK(hipEventRecord(c->ev0, c->stream));
@@ -1898,14 +1909,24 @@ static int encrypt_impl(fthe_key *k, fthe_ctx *c, MsgSrc m, size_t count, const 
     // (one chunk by construction: FTHE_CHUNK below the quad limit sends the batch down the other paths)
     const bool quad = direct_y && k->slat.S && count > 0 && count <= dec_quad_max() && count <= chunk_lanes();
     const bool small_split = !quad && direct_y && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
-    const bool big_split = !quad && !small_split && direct_y && vi >= 0 && split_all();
-    const bool split = small_split || big_split;
+    bool big_split = !quad && !small_split && direct_y && vi >= 0 && split_all();
     // big split calls of more than one chunk: chunks pipelined over two slot-region pairs (enc_pipe)
-    const bool piped = big_split && !pipe && !k->padic_own_slots && enc_pipe() && count > enc_chunk_lanes();
+    bool piped = big_split && !pipe && !k->padic_own_slots && enc_pipe() && count > enc_chunk_lanes();
     const int nsl = nslots_for(k);
     Launch Lc;
-    int rc = begin_call(c, k, count, Lc, piped ? 4 * nsl : split ? 2 * nsl : nsl, crt ? k->spq : k->sn2,
-                        direct_y && !small_split && !quad ? enc_chunk_lanes() : !crt && k->nadic_b ? pub_chunk_lanes() : 0);
+    auto begin = [&] {
+        return begin_call(c, k, count, Lc, piped ? 4 * nsl : (small_split || big_split) ? 2 * nsl : nsl,
+                          crt ? k->spq : k->sn2,
+                          direct_y && !small_split && !quad ? enc_chunk_lanes() : !crt && k->nadic_b ? pub_chunk_lanes() : 0);
+    };
+    int rc = begin();
+    // the extra regions of the pipelined / two-stream forms are a speed option (+1%): when the device (or the
+    // context's limit, fthe_ctx_set_mem_limit) cannot hold them, the call takes the one-region form, bit-identical
+    while (rc == FTHE_ERR_NOMEM && (piped || big_split)) {
+        if (piped) piped = false; else big_split = false;
+        rc = begin();
+    }
+    const bool split = small_split || big_split;
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     // Device-drawn randomness under CRT draws y_p, y_q uniform in [1,p), [1,q) and
@@ -2578,9 +2599,12 @@ void xb_pick_generator(gmp_randstate_t st, const mpz_t P, const std::vector<Mpz>
     }
 }
 
-int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
+// gam_in (nb_in bases per prime, [side][base][2 pq_w words]): the generators of another key of the same primes
+// (fthe_key_fixed_base_exact_info) instead of fresh ones -- a replica on another device draws the same r^n
+int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed, const uint32_t *gam_in = nullptr, int nb_in = 0) {
     fthe_key::ExactBase &X = k->xb;
     if (!k->priv) return FTHE_ERR_NOPRIV;
+    if (gam_in && nb_in != (k->order_known ? 1 : 3)) return FTHE_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipStreamSynchronize(c->stream));
     for (uint32_t **p : {&X.d_tab[0], &X.d_tab[1], &X.d_prog})
@@ -2617,15 +2641,24 @@ int xb_build(fthe_key *k, fthe_ctx *c, uint64_t seed) {
             std::copy(b.begin(), b.end(), dst + KB);
         };
         Mpz t[3];
-        if (k->order_known) xb_pick_generator(st, P, side ? k->qm1_factors : k->pm1_factors, t[0]);
-        else xb_pick_bases(st, P, t);
+        if (!gam_in) {
+            if (k->order_known) xb_pick_generator(st, P, side ? k->qm1_factors : k->pm1_factors, t[0]);
+            else xb_pick_bases(st, P, t);
+        }
         std::vector<uint32_t> tab;                        // 8-bit windows, base after base
-        for (int b = 0; b < X.nb; b++) {
-            mpz_powm(X.gam[side][b], t[b], P, D.m.N);
+        for (int b = 0; b < X.nb && rc == FTHE_OK; b++) {
+            if (gam_in) {
+                const size_t gw = 2 * (size_t)k->pq_w;
+                mpz_from_words(X.gam[side][b], gam_in + ((size_t)side * X.nb + b) * gw, (int)gw);
+                if (mpz_sgn(X.gam[side][b]) <= 0 || mpz_cmp(X.gam[side][b], D.m.N) >= 0) { rc = FTHE_ERR_ARG; break; }
+            } else {
+                mpz_powm(X.gam[side][b], t[b], P, D.m.N);
+            }
             std::vector<uint32_t> tb = X.padic ? fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, store_digits)
                                                : fb_table(X.gam[side][b], D.m.N, 2 * X.nwin, X.ew, fb_store_limbs(D.m));
             tab.insert(tab.end(), tb.begin(), tb.end());
         }
+        if (rc) break;
         uint32_t *d8 = nullptr;
         if ((rc = fb_upload(tab, &d8))) break;
         rc = fb_widen(k, c, X.padic ? A : D, k->spq, d8, X.nb * X.nwin, X.ew, false, &X.d_tab[side]);
@@ -2665,6 +2698,14 @@ extern "C" int fthe_key_fixed_base_exact(fthe_key *k, fthe_ctx *c, uint64_t seed
     HIPOK(hipSetDevice(c->device));
     HIPOK(hipDeviceSynchronize());            // no call may still read the old tables
     return xb_build(k, c, seed);
+}
+
+extern "C" int fthe_key_fixed_base_exact_set(fthe_key *k, fthe_ctx *c, int nb, const uint32_t *gammas) {
+    if (!k || !c || !gammas || k->device != c->device) return FTHE_ERR_ARG;
+    std::lock_guard<std::mutex> g(k->fb_mu);
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipDeviceSynchronize());            // no call may still read the old tables
+    return xb_build(k, c, 0, gammas, nb);
 }
 
 extern "C" int fthe_key_fixed_base_exact_info(fthe_key *k, int side, int base, uint32_t *gamma, int *exp_words) {
@@ -3100,11 +3141,15 @@ static int decrypt_impl(fthe_key *k, fthe_ctx *c, const uint32_t *ct, size_t cou
     // hand c^(P-1) mod P^2 back to the s74 layout for the unchanged L-function / CRT tail.
     const int vi = variant_index(k->spq.S);
     const bool quad = k->slat.S && count > 0 && count <= dec_quad_max() && count <= chunk_lanes();
-    const bool split = !quad && !short_pt && vi >= 0 &&
-                       (count * (size_t)kVariants[vi].lanes <= dec_split_lanes() || split_all());
+    const bool small_split = !quad && !short_pt && vi >= 0 && count * (size_t)kVariants[vi].lanes <= dec_split_lanes();
+    bool split = small_split || (!quad && !short_pt && vi >= 0 && split_all());
     const int nsl = nslots_for(k);
     Launch Lc;
     int rc = begin_call(c, k, count, Lc, split ? 2 * nsl : nsl, k->spq);
+    if (rc == FTHE_ERR_NOMEM && split && !small_split) {     // one region when two do not fit (as encrypt_impl)
+        split = false;
+        rc = begin_call(c, k, count, Lc, nsl, k->spq);
+    }
     if (rc) return rc;
     const int S = Lc.S, L = Lc.L, nw = k->n_words, cw = 2 * nw;
     Launch Lp4 = Lc, Lq4 = Lc;             // quad: s80 regions for the p and q halves (slots1)

@@ -82,6 +82,11 @@ class Device:
     def sync(self):
         _lib.check(self.lib.fthe_ctx_sync(self.ctx), "sync")
 
+    def set_mem_limit(self, nbytes):
+        """Cap the slot region a call may grow on this context (0: none); calls whose two-stream form does not
+        fit take the one-region form, bit-identical (include/fthe.h fthe_ctx_set_mem_limit)."""
+        _lib.check(self.lib.fthe_ctx_set_mem_limit(self.ctx, int(nbytes)), "set_mem_limit")
+
     # Stream order with torch: the engine runs on its own HIP stream, so a device-resident
     # call first waits for the work torch has queued on its current stream (the producers of
     # the inputs, e.g. a torch.zeros fill of the output), and torch's stream then waits for

@@ -71,6 +71,11 @@ void  fthe_ctx_destroy(fthe_ctx *ctx);
 int   fthe_ctx_sync(fthe_ctx *ctx);
 void *fthe_ctx_stream(fthe_ctx *ctx);       /* hipStream_t */
 int   fthe_ctx_device(fthe_ctx *ctx);
+/* Cap (bytes, 0 = none) on the slot region a call may grow on this context.  Large CRT encrypts and decrypts
+ * prefer two slot regions (both halves of a chunk on two streams, 7.4 GB at Paillier-2048); when the cap or
+ * the device cannot hold them they take the one-region form, bit-identical.  For many contexts on one GPU
+ * (the drop-in's per-thread and per-device contexts). */
+int   fthe_ctx_set_mem_limit(fthe_ctx *ctx, size_t bytes);
 /* Page-locked host memory for caller row buffers: host-resident calls then DMA straight from / into
  * it instead of staging through the context's pinned chunks (the drop-in class keeps one per thread for
  * encrypt / decrypt(SyncArray<GHPair>&), reused across calls: pinning is paid once). */
@@ -191,6 +196,12 @@ int fthe_key_fixed_base_info(fthe_key *key, int *alpha_bits_public, int *alpha_b
  *                                 words, nullable) and the words per exponent. */
 int fthe_key_fixed_base_exact(fthe_key *key, fthe_ctx *ctx, uint64_t seed);
 int fthe_key_fixed_base_exact_info(fthe_key *key, int side, int base, uint32_t *gamma, int *exp_words);
+/* (Re)build the exact tables from given generators instead of fresh ones: gammas = the nb gam of side 0, then
+ * the nb of side 1 (n_words words each, as fthe_key_fixed_base_exact_info returns them) of a key with the same
+ * primes -- a key replica on another device then draws r^n exactly as the original for the same exponents, so a
+ * seeded batch encrypt does not depend on how it was sharded (integration/paillier_hip.h key_on).  nb must be
+ * this key's bases per prime (3, or 1 for FTHE_KEYGEN_KNOWN_ORDER).  Not concurrent with calls using the key. */
+int fthe_key_fixed_base_exact_set(fthe_key *key, fthe_ctx *ctx, int nb, const uint32_t *gammas);
 /* bases per prime of the built exact tables: 3, or 1 for FTHE_KEYGEN_KNOWN_ORDER keys
  * (one generator); 0 before a build.  Injected exponents then take 2 * bases * (n_words/2)
  * words per ciphertext (y_{p,1..bases}, y_{q,1..bases}). */

@@ -10,9 +10,12 @@
 // and two adds per operator), timed beside the reference GPU build's own per-element work on the same threads
 // and operands (Paillier_GPU::mul = mpz_powm(x, 2^64 - 1, n^2), paillier_gpu.cu:65-67, then
 // Paillier_GPU::add = mpz_mul + mpz_mod, :57-61).  Checked: every difference decrypts to the codec difference.
-//   ghpair_rate [bits] [threads = features] [instances] [bins] [sub_bins]    -> one JSON line
+// Both legs run interleaved for `rounds` rounds (default 7) and the comparison is the median over rounds of the
+// per-round ratio reference time / operator time: a shared host's drift hits both legs of a round alike.
+//   ghpair_rate [bits] [threads = features] [instances] [bins] [sub_bins] [rounds]    -> one JSON line
 #include <omp.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -30,7 +33,27 @@ int main(int argc, char **argv) {
     const int N = argc > 3 ? std::atoi(argv[3]) : 512;
     const int B = argc > 4 ? std::atoi(argv[4]) : 16;
     const int SB = argc > 5 ? std::atoi(argv[5]) : 4096;
-    if (bits <= 0 || F <= 0 || N <= 0 || B <= 0 || SB < 0) return 2;
+    const int R = argc > 6 ? std::atoi(argv[6]) : 7;
+    if (bits <= 0 || F <= 0 || N <= 0 || B <= 0 || SB < 0 || R < 1) return 2;
+    auto median = [](std::vector<double> v) {
+        std::sort(v.begin(), v.end());
+        const size_t h = v.size() / 2;
+        return v.size() % 2 ? v[h] : 0.5 * (v[h - 1] + v[h]);
+    };
+    auto ratios = [](const std::vector<double> &num, const std::vector<double> &den) {
+        std::vector<double> r;
+        for (size_t i = 0; i < num.size() && i < den.size(); i++) r.push_back(num[i] / den[i]);
+        return r;
+    };
+    auto arr = [](const std::vector<double> &v) {
+        std::string o = "[";
+        char b[32];
+        for (size_t i = 0; i < v.size(); i++) {
+            std::snprintf(b, sizeof b, "%s%.4f", i ? ", " : "", v[i]);
+            o += b;
+        }
+        return o + "]";
+    };
     Paillier_HIP server;
     server.keygen(bits);
     SyncArray<GHPair> gh(N);
@@ -57,8 +80,8 @@ int main(int argc, char **argv) {
         (void)s;
     }
     // the reference's add on the same threads and operands (one mpz_mul + mpz_mod per ciphertext add),
-    // alternated with the operator loop: 3 rounds each, best of each reported (short runs on a shared
-    // host are noisy; every round of the operator loop starts from a fresh, unencrypted histogram)
+    // alternated with the operator loop, R rounds each, medians reported (short runs on a shared host are
+    // noisy; every round of the operator loop starts from a fresh, unencrypted histogram)
     auto ref_round = [&]() {
         const auto r0 = std::chrono::steady_clock::now();
 #pragma omp parallel for num_threads(F) schedule(static)
@@ -90,14 +113,12 @@ int main(int argc, char **argv) {
         }
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
-    double ref_s = 1e30, s = 1e30;
     std::vector<double> ref_all, op_all;
-    for (int rep = 0; rep < 3; rep++) {
+    for (int rep = 0; rep < R; rep++) {
         ref_all.push_back(ref_round());
         op_all.push_back(op_round());
-        ref_s = std::min(ref_s, ref_all.back());
-        s = std::min(s, op_all.back());
     }
+    const double ref_s = median(ref_all), s = median(op_all), vs_add = median(ratios(ref_all, op_all));
     // check: the codec sums (long)(x * 1e6) of each bin's members
     std::vector<int64_t> wg(hist.size(), 0), wh(hist.size(), 0);
     for (int fid = 0; fid < F; fid++)
@@ -122,7 +143,7 @@ int main(int argc, char **argv) {
             bad++;
     }
     // -- sibling subtraction: father - child per bin (both encrypted: the encrypted-rhs branch) --
-    double sub_s = 1e30, sub_ref_s = 1e30;
+    double sub_s = 0, sub_ref_s = 0, vs_sub = 0;
     std::vector<double> sub_all, sub_ref_all;
     int sub_bad = 0;
     if (SB > 0) {
@@ -173,12 +194,13 @@ int main(int argc, char **argv) {
             }
             return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         };
-        for (int rep = 0; rep < 3; rep++) {
+        for (int rep = 0; rep < R; rep++) {
             sub_ref_all.push_back(sub_ref_round());
             sub_all.push_back(sub_round());
-            sub_ref_s = std::min(sub_ref_s, sub_ref_all.back());
-            sub_s = std::min(sub_s, sub_all.back());
         }
+        sub_s = median(sub_all);
+        sub_ref_s = median(sub_ref_all);
+        vs_sub = median(ratios(sub_ref_all, sub_all));
         SyncArray<GHPair> dd(SB);
         for (int i = 0; i < SB; i++) dd.host_data()[i] = diff[i];
         server.decrypt(dd);
@@ -191,25 +213,19 @@ int main(int argc, char **argv) {
                 sub_bad++;
         }
     }
-    auto arr3 = [](const std::vector<double> &v) {
-        char b[96];
-        if (v.size() < 3) return std::string("[]");
-        std::snprintf(b, sizeof b, "[%.4f, %.4f, %.4f]", v[0], v[1], v[2]);
-        return std::string(b);
-    };
     const double sops = 2.0 * SB;   // ciphertext subtractions (g and h)
     const double ops = (double)F * N;
     std::printf("{\"bits\": %d, \"threads\": %d, \"instances\": %d, \"bins\": %d, \"operators\": %.0f, "
                 "\"ciphertext_adds\": %.0f, \"promotions\": %d, \"s\": %.4f, \"operators_per_s\": %.0f, "
                 "\"ciphertext_adds_per_s\": %.0f, \"reference_add_same_threads_per_s\": %.0f, "
-                "\"vs_reference_add\": %.3f, \"rounds_s\": [%.4f, %.4f, %.4f], \"reference_rounds_s\": [%.4f, %.4f, %.4f], "
+                "\"vs_reference_add\": %.3f, \"rounds\": %d, \"rounds_s\": %s, \"reference_rounds_s\": %s, "
                 "\"bad_bins\": %d, \"sub\": {\"bins\": %d, \"ciphertext_subs\": %.0f, \"s\": %.5f, "
                 "\"ciphertext_subs_per_s\": %.0f, \"reference_sub_same_threads_per_s\": %.0f, \"vs_reference_sub\": %.3f, "
                 "\"rounds_s\": %s, \"reference_rounds_s\": %s, \"bad_bins\": %d}, \"ok\": %s}\n",
                 bits, F, N, B, ops, 2 * ops, 2 * populated, s, ops / s, 2 * ops / s, 2 * ops / ref_s,
-                (2 * ops / s) / (2 * ops / ref_s), op_all[0], op_all[1], op_all[2], ref_all[0], ref_all[1], ref_all[2],
+                vs_add, R, arr(op_all).c_str(), arr(ref_all).c_str(),
                 bad, SB, sops, SB ? sub_s : 0.0, SB ? sops / sub_s : 0.0, SB ? sops / sub_ref_s : 0.0,
-                SB ? sub_ref_s / sub_s : 0.0, arr3(sub_all).c_str(), arr3(sub_ref_all).c_str(), sub_bad,
+                vs_sub, arr(sub_all).c_str(), arr(sub_ref_all).c_str(), sub_bad,
                 (bad || sub_bad) ? "false" : "true");
     return (bad || sub_bad) ? 1 : 0;
 }

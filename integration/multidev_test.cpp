@@ -7,7 +7,9 @@
 //                                              key holder and party; prints one digest line per call.  Run under
 //                                              FTHE_DEVICES=0 and FTHE_DEVICES=0,0 (two contexts on device 0,
 //                                              FTHE_SHARD_ROWS small) the digests must be equal: sharding does not
-//                                              change a ciphertext (tests/test_integration_shim.py).
+//                                              change a ciphertext (tests/test_integration_shim.py); on a node with
+//                                              several GPUs also under FTHE_DEVICES=0,1,..,k-1 (one shard, context
+//                                              and key replica per physical device: configs[4]'s path).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -124,6 +126,16 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < N; i++) hx.host_data()[i].encrypted = true;
     std::printf("party_encrypt_exact %016llx\n", (unsigned long long)digest(hx));
     party.enc_mode = Paillier_HIP::EncMode::Default;
+    // the key holder's exact fixed-base mode: tables from deterministic generators on the primary key; every
+    // replica takes the same generators (fthe_key_fixed_base_exact_set), so the digest does not depend on sharding
+    server.enc_mode = Paillier_HIP::EncMode::FixedBaseExact;
+    server.exact_tables(99);
+    SyncArray<GHPair> sx(N);
+    for (size_t i = 0; i < N; i++) sx.host_data()[i] = GHPair(val(i + 17, 1), val(i + 19, 0));
+    server.encrypt(sx);
+    for (size_t i = 0; i < N; i++) sx.host_data()[i].encrypted = true;
+    std::printf("server_encrypt_exact %016llx\n", (unsigned long long)digest(sx));
+    server.enc_mode = Paillier_HIP::EncMode::Default;
 
     // node histogram (zero first), the 3-party merge (zero first), sibling subtraction, prefix sums
     const int n_col = 3, missing = 255;
@@ -163,6 +175,9 @@ int main(int argc, char **argv) {
     server.decrypt(hx);
     for (size_t i = 0; i < N; i++)
         if (hx.host_data()[i].g != expect(val(i + 11, 0)) || hx.host_data()[i].h != expect(val(i + 13, 1))) bad++;
+    server.decrypt(sx);
+    for (size_t i = 0; i < N; i++)
+        if (sx.host_data()[i].g != expect(val(i + 17, 1)) || sx.host_data()[i].h != expect(val(i + 19, 0))) bad++;
     double want[16] = {0};
     for (size_t i = 0; i < N; i++)
         for (int f = 0; f < n_col; f++) {

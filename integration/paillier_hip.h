@@ -220,12 +220,23 @@ public:
         struct Join { std::mutex m; std::condition_variable cv; size_t left; std::vector<std::exception_ptr> err; } j;
         j.left = n - 1;
         j.err.resize(n);
-        for (size_t i = 1; i < n; i++)
-            worker(i).push([&j, &f, i, d = devs[i]] {
-                try { f(i, ctx_on(d)); } catch (...) { j.err[i] = std::current_exception(); }
-                std::lock_guard<std::mutex> lk(j.m);
-                if (--j.left == 0) j.cv.notify_all();
-            });
+        size_t queued = 1;
+        try {
+            for (; queued < n; queued++)
+                worker(queued).push([&j, &f, i = queued, d = devs[queued]] {
+                    try { f(i, ctx_on(d)); } catch (...) { j.err[i] = std::current_exception(); }
+                    std::lock_guard<std::mutex> lk(j.m);
+                    if (--j.left == 0) j.cv.notify_all();
+                });
+        } catch (...) {
+            // a push failed (the pool is stopping at exit): the jobs already queued still reference j and f, so
+            // wait for them before this frame unwinds; the shards never queued report the error
+            j.err[0] = std::current_exception();
+            std::unique_lock<std::mutex> lk(j.m);
+            j.left -= n - queued;
+            j.cv.wait(lk, [&] { return j.left == 0; });
+            std::rethrow_exception(j.err[0]);
+        }
         try { f(0, ctx_on(devs[0])); } catch (...) { j.err[0] = std::current_exception(); }
         {
             std::unique_lock<std::mutex> lk(j.m);
@@ -398,6 +409,7 @@ public:
         size_t n = message.size();
         if (n == 0) return;
         const int cw = 2 * fthe_key_n_words(key()), flags = eff_flags();
+        prepare_exact();
         fthe_shim::Pinned<uint64_t> mb(2 * n);
         fthe_shim::Pinned<uint32_t> cb(2 * n * (size_t)cw);
         uint64_t *m = mb.get();
@@ -619,6 +631,7 @@ public:
     // c[i] = Enc(m[i]) (fthe_encrypt_u64_at with this object's enc_mode and rng_seed)
     void encrypt_rows(const uint64_t *m, size_t count, uint32_t *c) {
         const int cw = 2 * fthe_key_n_words(key()), flags = eff_flags();
+        prepare_exact();
         for_shards(count, [&](fthe_ctx *ctx, fthe_key *k, size_t lo, size_t hi, unsigned) {
             fthe_shim::check(fthe_encrypt_u64_at(k, ctx, m + lo, hi - lo, nullptr, 0, rng_seed, lo, c + lo * cw, flags),
                              "encrypt");
@@ -667,13 +680,59 @@ public:
     // This key on the device of context c: the key itself on the primary device, else its replica there, made on
     // first use from p, q (key holder) or n and the published bases (public key) -- the same n, the same results.
     // FTHE_SHIM_REPLICATE=1 (tests): replicas on the primary device too, so a one-GPU box runs the replica path.
+    // A key holder's replica in FixedBaseExact mode also takes the key's own table generators
+    // (fthe_key_fixed_base_exact_set), so its r^n are the key's for the same exponents (exact_tables).
     fthe_key *key_on(fthe_ctx *c) {
         static const bool force = [] { const char *e = std::getenv("FTHE_SHIM_REPLICATE"); return e && *e == '1'; }();
         const int dv = fthe_ctx_device(c);
         fthe_key *k0 = key();
         if (dv == fthe_shim::primary_device() && !force) return k0;
         std::lock_guard<std::mutex> lk(rep_mu_);
-        for (auto &r : replicas_) if (r.first == dv) return r.second.get();
+        for (auto &r : replicas_)
+            if (r.first == dv) { sync_exact(k0, r.second.get(), c); return r.second.get(); }
+        fthe_key *k = new_replica(k0, c);
+        sync_exact(k0, k, c);
+        return k;
+    }
+
+    // Key holder, FixedBaseExact: (re)build this key's exact tables (fthe_key_fixed_base_exact; seed 0: fresh
+    // generators from /dev/urandom, nonzero: deterministic, for tests) -- the replicas on other devices follow on
+    // their next use.  Built on the first FixedBaseExact batch otherwise.
+    void exact_tables(uint64_t seed = 0) {
+        std::lock_guard<std::mutex> lk(rep_mu_);
+        fthe_shim::check(fthe_key_fixed_base_exact(key(), fthe_shim::thread_ctx(), seed), "fixed_base_exact");
+    }
+
+private:
+    // the replica's exact tables from k0's generators, when k0 has tables and the replica's differ
+    void sync_exact(fthe_key *k0, fthe_key *k, fthe_ctx *c) {
+        if (enc_mode != EncMode::FixedBaseExact || !fthe_key_has_private(k0)) return;
+        const int nb = fthe_key_fixed_base_exact_bases(k0);
+        if (!nb) return;
+        const size_t gw = (size_t)fthe_key_n_words(k0);
+        std::vector<uint32_t> g0(2 * nb * gw), g1(2 * nb * gw);
+        for (int s = 0; s < 2; s++)
+            for (int b = 0; b < nb; b++)
+                fthe_shim::check(fthe_key_fixed_base_exact_info(k0, s, b, &g0[(s * nb + b) * gw], nullptr), "exact_info");
+        if (fthe_key_fixed_base_exact_bases(k) == nb) {
+            for (int s = 0; s < 2; s++)
+                for (int b = 0; b < nb; b++)
+                    fthe_shim::check(fthe_key_fixed_base_exact_info(k, s, b, &g1[(s * nb + b) * gw], nullptr),
+                                     "exact_info");
+            if (g0 == g1) return;
+        }
+        fthe_shim::check(fthe_key_fixed_base_exact_set(k, c, nb, g0.data()), "exact_set");
+    }
+    // Key holder, FixedBaseExact: the key's own tables exist before the shards start, so no shard builds
+    // fresh ones beside another's use of them (run on the calling thread, before run_plan)
+    void prepare_exact() {
+        if (enc_mode != EncMode::FixedBaseExact || !fthe_key_has_private(key())) return;
+        std::lock_guard<std::mutex> lk(rep_mu_);
+        if (!fthe_key_fixed_base_exact_bases(key()))
+            fthe_shim::check(fthe_key_fixed_base_exact(key(), fthe_shim::thread_ctx(), 0), "fixed_base_exact");
+    }
+    fthe_key *new_replica(fthe_key *k0, fthe_ctx *c) {
+        const int dv = fthe_ctx_device(c);
         const int nw = fthe_key_n_words(k0);
         fthe_key *k = nullptr;
         if (fthe_key_has_private(k0)) {
@@ -694,6 +753,7 @@ public:
         return k;
     }
 
+public:
     uint32_t key_length;
     // The GHPair key (common.h:72; server.h:119 and party.h:124 assign it to every encrypted GHPair):
     // the public part of this object's engine key, whose add / mul / encrypt run on the engine.

@@ -119,3 +119,34 @@ def test_split_all_large_calls_bit_identical(tmp_path):
         assert o[2] == "True"
         assert o[0] == o[1]                               # host rows = device rows
     assert outs[0][0] == outs[1][0] == outs[2][0]
+
+
+def test_mem_limit_one_region_fallback():
+    """the two-stream form of a large CRT encrypt / decrypt needs a second slot region; when the
+    context's cap (fthe_ctx_set_mem_limit, standing in for a full device) cannot hold it, the call takes the
+    one-region form instead of failing.  Caps falling by 0.8x from 16 GB down to the first that cannot hold even
+    one region: every call above it returns the uncapped call's ciphertexts and plaintexts; the cap just above
+    the failure is < 2x the one-region size, so that call ran the fallback; the failing cap reports NOMEM."""
+    from fedtree_amd import _lib
+    from fedtree_amd.paillier import Device, Paillier
+    g = load_golden("ref_gmp_L2048.json")
+    p, q = golden_key(g)
+    n = SPLIT_MAX + 6789                          # above the small split: the large (split_all) form
+    m = np.random.default_rng(21).integers(0, 2**64, n, dtype=np.uint64)
+    want = Paillier.from_primes(p, q, Device(0)).encrypt_u64(m, seed=404)
+    cap, ok_caps, failed = 16 << 30, [], None
+    while cap > (64 << 20):
+        d = Device(0)
+        d.set_mem_limit(cap)
+        pl = Paillier.from_primes(p, q, d)
+        try:
+            c = pl.encrypt_u64(m, seed=404)
+        except _lib.FtheError as ex:
+            assert ex.status == _lib.FTHE_ERR_NOMEM, ex
+            failed = cap
+            break
+        assert np.array_equal(c, want), cap
+        assert np.array_equal(pl.decrypt_u64(c), m), cap
+        ok_caps.append(cap)
+        cap = int(cap * 0.8)
+    assert failed is not None and ok_caps and ok_caps[-1] < 2 * failed, (ok_caps, failed)

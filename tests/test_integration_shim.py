@@ -380,3 +380,49 @@ def test_ghpair_e2e_two_shards(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["ok"] and out["shards"] == 2
+
+
+def _gpu_count():
+    import torch                                   # device_count() does not initialise HIP on this image
+    return torch.cuda.device_count()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["physical", "emulated"])
+def test_sharded_drop_in_every_device(tmp_path, mode):
+    """configs[4]'s path through the class FedTree calls (Server::encrypt_gh_pairs / decrypt_gh_pairs,
+    server.h:105-135 -> Paillier_HIP -> ShardPool, paillier_gpu.cu:211-313): "physical" shards every batch call of
+    multidev_test over every visible GPU (FTHE_DEVICES=0,1,..,k-1: a worker thread, context and key replica per
+    device, fthe_shim::ctx_on(d != 0), key_on's replicas incl. the key holder's exact tables) and must give the
+    one-device run's digests byte for byte -- seeded encrypts (default, party published-bases exact, key-holder
+    exact), histogram, merges, subtracts, prefix -- with every decrypt checked; then ghpair_e2e round-trips
+    20,000 pairs per device over all of them.  Skipped with fewer than 2 GPUs.  "emulated" is the same over two
+    contexts on device 0 with every shard on a key replica (FTHE_SHIM_REPLICATE=1), the path a one-GPU box runs."""
+    import json
+    n = _gpu_count()
+    if mode == "physical" and n < 2:
+        pytest.skip(f"{n} GPU visible: the physical multi-device case needs 2 or more")
+    devs = ",".join(str(i) for i in range(n)) if mode == "physical" else "0,0"
+    g = load_golden("ref_gmp_L2048.json")
+    p, q = golden_key(g)
+    exe = str(tmp_path / "multidev_test")
+    _build(exe, "multidev_test.cpp")
+    outs = {}
+    for dl, rep in (("0", "0"), (devs, "0" if mode == "physical" else "1")):
+        env = dict(os.environ, FTHE_DEVICES=dl, FTHE_SHARD_ROWS="256", FTHE_SHIM_REPLICATE=rep)
+        r = subprocess.run([exe, "run", f"{p:x}", f"{q:x}", "3000"], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0 and "multidev OK" in r.stdout, dl + ": " + r.stdout[-3000:] + r.stderr[-3000:]
+        lines = r.stdout.strip().splitlines()
+        assert f"devices {len(dl.split(','))}" in lines
+        outs[dl] = [ln for ln in lines if not ln.startswith("devices")]
+    assert any(ln.startswith("server_encrypt_exact ") for ln in outs["0"])
+    assert outs[devs] == outs["0"], outs
+    exe2 = str(tmp_path / "ghpair_e2e")
+    _build(exe2, "ghpair_e2e.cpp", extra=("-fopenmp",))
+    k = len(devs.split(","))
+    r = subprocess.run([exe2, "2048", str(20000 * k), "1", devs], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, FTHE_SHIM_REPLICATE="0" if mode == "physical" else "1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"] and out["shards"] == k

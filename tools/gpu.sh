@@ -17,8 +17,9 @@
 #                         (tools/nadicb_ab.py; the PMC summary separates the kernels by name)
 #                  then: python tools/rocprof_summary.py pmc gpurun_out/TAG_pmc_W_* out.json (CPU side)
 #   opstrace       kernel trace of tools/prof_ops.py add,kway (the add / merge launch durations for pmc:add)
-#   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo)
-#   ghpair         tools/bin/ghpair_rate at 16 and 64 threads, tools/bin/ghpair_e2e
+#   rehearse       FTHE_BENCH_REHEARSE=1 bench.py --gpus 2 (two ranks on the one GPU over gloo; ghpair_e2e_node
+#                  over two contexts, NODE_PAIRS pairs per device, default 2M)
+#   ghpair         tools/bin/ghpair_rate twice at 16 threads (7 interleaved rounds each), tools/bin/ghpair_e2e
 #   marshal        tools/bin/marshal_rate: host mpz <-> row marshalling of 1, 2, 4, 8 concurrent shards (no kernels)
 #   ghsub          the operator- A/B: tools/bin/ghpair_rate at 16 threads, host powm vs FTHE_SHIM_MUL_ENGINE=1
 #   py:SCRIPT[,ARGS]  python SCRIPT ARGS (a tools/ measurement), appended to TAG_SCRIPT.jsonl
@@ -84,12 +85,13 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_ops_trace -o ops -- \
         python3 tools/prof_ops.py --n 1048576 --ops add,kway > ${O}_ops_trace.log 2>&1 || fail opstrace $? ${O}_ops_trace.log;;
     rehearse)
-      FTHE_BENCH_REHEARSE=1 timeout -k 10 600 python bench.py --gpus 2 --pairs 1048576 --steps 2 --warmup 1 \
+      FTHE_BENCH_REHEARSE=1 FTHE_BENCH_NODE_PAIRS=${NODE_PAIRS:-2000000} timeout -k 10 600 python bench.py --gpus 2 \
+        --pairs 1048576 --steps 2 --warmup 1 \
         > ${O}_rehearse_2rank_1gpu.json 2> ${O}_rehearse.err || fail rehearse $? ${O}_rehearse.err
       cut -c1-600 ${O}_rehearse_2rank_1gpu.json;;
     ghpair)
-      for t in 16 64; do
-        timeout -k 10 300 tools/bin/ghpair_rate 2048 $t 8192 16 4096 >> ${O}_ghpair_rate.jsonl 2>> ${O}_ghpair.err \
+      for t in 16 16; do
+        timeout -k 10 300 tools/bin/ghpair_rate 2048 $t 8192 16 4096 7 >> ${O}_ghpair_rate.jsonl 2>> ${O}_ghpair.err \
           || fail ghpair_rate $? ${O}_ghpair.err
       done
       timeout -k 10 300 tools/bin/ghpair_e2e 2048 2000000 2 >> ${O}_ghpair_e2e.jsonl 2>> ${O}_ghpair.err \
