@@ -68,8 +68,11 @@ LDS_CNT = LDS_WAVES + WAVES * WAVE_AREA      # the workgroup's batch counter (dw
 LDS_BYTES = LDS_CNT + 16                     # 153,872
 QROW = 656                                   # q staging row: 9 K-blocks of 64 bytes, stride = 4 (mod 32)
                                              # dwords: the quads' staging writes 4-way, not 16-way, per bank
-GROW = 560                                   # group staging row: two chunks' 64-68 int64 groups + pad (16-byte
-                                             # aligned: the normalisation reads two groups per ds_read_b128)
+GROW = 552                                   # group staging row: two chunks' 64-68 int64 groups; 138 dwords ==
+                                             # 10 (mod 32): the folds' 16-lane ds_write_b64 hit 32 distinct banks
+GCH = 264                                    # the pair's second chunk at byte 264 (66 dwords == 2 mod 64): with
+                                             # GROW the normalisation's ds_read_b64 are conflict-free too
+                                             # (tools/lds_conflicts.py; 16-byte rows for b128 reads cannot be)
 KB1, KB2 = 9, 9
 NQ1, NQ3 = 129, 129                          # q1, q3 dwords (rows >= N: q3 < 2^4098)
 MU_SHIFT = 4072 + 4128                       # mu = floor(2^(A + C) / N)
@@ -267,7 +270,8 @@ def gen_addb(name: str) -> str:
     e(f'  v_mul_u32_u24_e32 v{V_GR}, {GROW}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_GR}, s15, v{V_GR}')                        # group row c
     e(f'  v_and_b32_e32 v{V_TMP + 1}, 1, v{V_TID}')
-    e(f'  v_lshl_add_u32 v{V_GR}, v{V_TMP + 1}, 8, v{V_GR}')          # quad lanes 1, 3: the pair's 2nd chunk
+    e(f'  v_mul_u32_u24_e32 v{V_TMP + 1}, {GCH}, v{V_TMP + 1}')
+    e(f'  v_add_u32_e32 v{V_GR}, v{V_GR}, v{V_TMP + 1}')               # quad lanes 1, 3: the pair's 2nd chunk
     e(f'  v_mul_u32_u24_e32 v{V_Q3W}, {QROW}, v{V_TMP}')
     e(f'  v_add_u32_e32 v{V_Q3W}, s15, v{V_Q3W}')                      # staging row c (+ 128 j below)
     e(f'  v_and_b32_e32 v{V_SH}, 3, v{V_TID}')                         # j
@@ -275,6 +279,15 @@ def gen_addb(name: str) -> str:
     e(f'  v_add_u32_e32 v{V_Q3W}, v{V_Q3W}, v{V_TMP}')
     e(f'  v_subrev_u32_e32 v{V_Q3W}, 4, v{V_Q3W}')                    # + 128 j - 4 (dword 32 j - 1)
     e(f'  v_lshlrev_b32_e32 v{V_SH}, 1, v{V_SH}')                      # 2 j (the row-I/O shift)
+    if "ldsfree" in DBG:
+        # timing knock-out (wrong results): the staging / group addresses spread so that their LDS
+        # accesses have no bank conflicts -- the same instructions (the potential of a conflict-free layout)
+        e(f'  v_and_b32_e32 v{V_TMP}, 63, v{V_TID}')                   # lane
+        e(f'  v_lshl_add_u32 v{V_B}, v{V_TMP}, 4, s15')                # area + 16 lane
+        e(f'  v_lshl_add_u32 v{V_G}, v{V_TMP}, 3, s15')                # area + 8 lane
+        e(f'  v_lshl_add_u32 v{V_GR}, v{V_TMP}, 4, s15')               # area + 16 lane
+        e(f'  v_lshl_add_u32 v{V_Q3W}, v{V_TMP}, 3, s15')
+        e(f'  v_add_u32_e32 v{V_Q3W}, 0x184, v{V_Q3W}')               # area + 8 lane + 388 (== 4 mod 8, >= 380)
     e(f'  v_and_b32_e32 v{V_TID}, 63, v{V_TID}')
     e(f'  v_lshlrev_b32_e32 v{V_TID}, 7, v{V_TID}')                    # v0 = lane * 128 from here on
     e('.Lbatch:')
@@ -933,13 +946,15 @@ def gen_addb(name: str) -> str:
 
     def norm_one_chain(ja, jb, na, nb, ng, cv):
         def rd(g):
-            e(f'  ds_read_b128 v[{GB + 4 * ((g // 2) % 2)}:{GB + 4 * ((g // 2) % 2) + 3}], v{V_GR} offset:{8 * g}')
+            for hh in (0, 1):                             # groups g, g + 1: two ds_read_b64 (8-byte rows)
+                b = GB + 4 * ((g // 2) % 2) + 2 * hh
+                e(f'  ds_read_b64 v[{b}:{b + 1}], v{V_GR} offset:{8 * (g + hh)}')
         rd(0)
         rd(2)
         for g0 in range(0, ng, 2):
             if g0 == na and nb > na:                 # lane ja's chunk ends (its carry stays in FV + 1)
                 e(f'  s_mov_b64 exec, {LANE_MASK[jb]}')
-            e(f'  s_waitcnt lgkmcnt({1 if g0 + 2 < ng else 0})')
+            e(f'  s_waitcnt lgkmcnt({2 if g0 + 2 < ng else 0})')
             for g in (g0, g0 + 1):
                 src = pair(GB + 4 * ((g0 // 2) % 2) + 2 * (g - g0))
                 if g % 2 == 0:
@@ -964,12 +979,13 @@ def gen_addb(name: str) -> str:
 
         def rd(g, tag):
             b = GB + (8 if g >= H else 0) + 4 * ((g // 2) % 2)
-            e(f'  ds_read_b128 v[{b}:{b + 3}], v{V_GR} offset:{8 * g}')
-            q.append(tag)
+            for hh in (0, 1):                             # groups g, g + 1: two ds_read_b64 (8-byte rows)
+                e(f'  ds_read_b64 v[{b + 2 * hh}:{b + 2 * hh + 1}], v{V_GR} offset:{8 * (g + hh)}')
+                q.append(tag)
 
         def wait_for(tag):
             if tag in q:
-                i = q.index(tag)
+                i = len(q) - 1 - q[::-1].index(tag)       # the tag's last read
                 e(f'  s_waitcnt lgkmcnt({min(len(q) - i - 1, 15)})')
                 del q[:i + 1]
 
@@ -1069,7 +1085,7 @@ def gen_addb(name: str) -> str:
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 1}, s30, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 2}, s31, {pair(PG)}')
         e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 3}, s32, {pair(PG)}')
-        e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{8 * gl}')
+        e(f'  ds_write_b64 v{V_G}, {pair(PG)} offset:{8 * gl + (GCH - 256 if gl >= 32 else 0)}')
 
     e('// @phase prod1')
     mfma_product(1)

@@ -39,7 +39,9 @@ S, Q, B = 76, 19, 27
 MASK = (1 << B) - 1
 WAVES = int(os.environ.get("FTHE_GEN_NADICB_WAVES", "12"))   # timing builds only (FTHE_GEN_*: never in-tree)
 CT_PER_WAVE = 16
-RB = 68                          # A-column row: 16 ciphertexts x 4 B + pad (gen_quad's QUAD_ROWB)
+RB = 76                          # A-column row: 16 ciphertexts x 4 B + pad; 19 dwords: a quad's four write_rows
+                                 # lanes 19 x 19 k = 9 k dwords apart (68 B rows: 3 k, 2- to 3-way conflicts) and
+                                 # to_dwords' two lanes 18 apart (tools/lds_conflicts.py)
 ROWS = 2 * S                     # rows 0..75: y0 / x0 (then z1's retired limbs), 76..151: y1 (then z2's)
 # ---- Barrett constants (tools/nadicb_model.py) -------------------------------------------------------------
 A_BITS, C_BITS = 2016, 2112
@@ -74,11 +76,14 @@ CORR2_OFF = CORR1_OFF + TILES1 * 64
 IMG_BYTES = CORR2_OFF + TILES2 * 64
 N_OFF = IMG_BYTES                                     # n limbs (76 x u32) in ctx, not copied to LDS
 CTX_BYTES = N_OFF + 4 * S
-QROW = 400                       # q / r staging row: 80 dwords used; 100 dwords == 4 mod 32 (4-way stores)
-GROW = 624                       # group staging row: a product's 68 int64 groups (every chunk at once) + pad;
-                                 # 16-byte aligned rows for the normalisation's ds_read_b128 of two groups
-CSTRIDE = 272                    # chunk k's groups at 272 k: with GROW = 624 the normalisation's reads are
-                                 # conflict-free and the folds' writes 2-way (tools/lds_conflicts.py)
+QROW = 400                       # q / r staging row: 80 dwords used; 100 dwords == 4 mod 32 (4-way stores:
+                                 # the quad layout's lanes 32 dwords apart; 416 would free the B reads but make
+                                 # the 32-lane ds_write_b32 8-way, tools/lds_conflicts.py)
+GROW = 568                       # group staging row: a product's 68 int64 groups (every chunk at once); 142
+                                 # dwords == 2 (mod 4): the folds' 16-lane ds_write_b64 hit 32 distinct banks
+CSTRIDE = 264                    # chunk k's groups at 264 k: with GROW = 568 the normalisation's ds_read_b64
+                                 # are conflict-free too (16-byte rows for ds_read_b128 cannot give conflict-free
+                                 # writes; tools/lds_conflicts.py)
 QST_OFF = 0                      # staging areas inside the wave area (the A column is dead in the Barretts); the
 GST_OFF = 0                      # groups overlap the q staging, which the B operands have left before the MFMAs
 WAVE_AREA = max(ROWS * RB, QST_OFF + 16 * QROW, GST_OFF + 16 * GROW)
@@ -281,6 +286,15 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
     e(f'  v_add_u32_e32 v{V_B}, v{V_B}, v{V_A2X}')
     e(f'  v_lshlrev_b32_e32 v{V_SH}, 1, v{V_SH}')                      # 2 k
     e(f'  v_lshlrev_b32_e32 v{V_LANE}, 7, v{V_LANE}')                  # lane * 128: ROW = g*512 + k*128
+    if "ldsfree" in DBG:
+        # timing knock-out (wrong results): the staging / group addresses spread so that no LDS access of the
+        # Barrett phases has a bank conflict -- the same instructions at conflict-free addresses (the potential
+        # of a conflict-free staging layout)
+        e(f'  v_lshrrev_b32_e32 v{V_TMP}, 7, v{V_LANE}')                 # lane
+        e(f'  v_lshl_add_u32 v{V_QW}, v{V_TMP}, 3, v{V_A2X}')            # area + 8 lane (+ 128 k at the sites)
+        e(f'  v_lshl_add_u32 v{V_B}, v{V_TMP}, 4, v{V_A2X}')             # area + 16 lane
+        e(f'  v_lshl_add_u32 v{V_G}, v{V_TMP}, 3, v{V_A2X}')             # area + 8 lane
+        e(f'  v_lshl_add_u32 v{V_GR}, v{V_TMP}, 4, v{V_A2X}')            # area + 16 lane
     e('  s_add_u32 s36, s8, ' + hex(N_OFF))
     e('  s_addc_u32 s37, s9, 0')
 
@@ -778,7 +792,9 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
 
         def rd(c, p):                                     # pair p (groups 2 p, 2 p + 1) of chain c
             g0c, buf, _ = chains[c]
-            e(f'  ds_read_b128 {quad4(buf + 4 * (p % 2))}, v{V_GR} offset:{8 * (g0c + 2 * p)}')
+            for hh in (0, 1):                             # two ds_read_b64 (8-byte rows, conflict-free)
+                b = buf + 4 * (p % 2) + 2 * hh
+                e(f'  ds_read_b64 v[{b}:{b + 1}], v{V_GR} offset:{8 * (g0c + 2 * p + hh)}')
         npair = H // 2
         for p in (0, 1):
             rd(0, p)
@@ -786,7 +802,7 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         for p in range(npair):
             if 2 * p == sizes[2]:                         # lane 2's chunk ends: its carry stays in FV + 1
                 e(f'  s_mov_b64 exec, {L01}')
-            e(f'  s_waitcnt lgkmcnt({2 if p + 1 < npair else 0})')
+            e(f'  s_waitcnt lgkmcnt({4 if p + 1 < npair else 0})')
             for h in (0, 1):                              # even group of A, of B, then the odd groups
                 for c in (0, 1):
                     g0c, buf, fp = chains[c]
@@ -1038,8 +1054,11 @@ def gen_nadicb(name: str, waves: int = WAVES) -> str:
         e('  s_waitcnt lgkmcnt(0)')
         # lane k: positions 16 k .. 16 k + 16 into W (zb area is free now: r is staged)
         W = BQ                                                            # free after product 2
-        e(f'  v_lshlrev_b32_e32 v{V_TMP + 1}, 6, v{V_TMP}')
-        e(f'  v_add_u32_e32 v{V_TMP + 1}, v{V_TMP + 1}, v{V_QW}')         # position 16 k
+        if "ldsfree" in DBG:                                              # timing knock-out: aligned, spread
+            e(f'  v_mov_b32_e32 v{V_TMP + 1}, v{V_B}')
+        else:
+            e(f'  v_lshlrev_b32_e32 v{V_TMP + 1}, 6, v{V_TMP}')
+            e(f'  v_add_u32_e32 v{V_TMP + 1}, v{V_TMP + 1}, v{V_QW}')     # position 16 k
         for i in range(4):
             e(f'  ds_read_b128 v[{W + 4 * i}:{W + 4 * i + 3}], v{V_TMP + 1} offset:{16 * i}')
         e(f'  ds_read_b32 v{W + 16}, v{V_TMP + 1} offset:64')
