@@ -438,7 +438,8 @@ E2E_HOST_BYTES_PER_PAIR = 2300
 
 def node_e2e(a, world, devices, rehearse):
     """ghpair_e2e over every device of the run in one process (integration/ghpair_e2e.cpp): 10M pairs per device
-    (FTHE_BENCH_NODE_PAIRS overrides), fewer when the host cannot hold the batch in 40% of its free memory; one rep,
+    (FTHE_BENCH_NODE_PAIRS overrides), fewer when the host cannot hold the batch in 40% of its free memory; best of
+    two reps (the first pays the pinning, the key replicas and the mpz allocations),
     every plaintext checked.  FTHE_BENCH_REHEARSE: every shard on device 0."""
     per_dev = int(os.environ.get("FTHE_BENCH_NODE_PAIRS") or 10_000_000)
     mem = host_mem_bytes()
@@ -451,7 +452,7 @@ def node_e2e(a, world, devices, rehearse):
     t0 = time.perf_counter()
     try:
         env = dict(os.environ, FTHE_SHIM_REPLICATE="1" if rehearse else "0")
-        r = subprocess.run([exe, str(KEY_BITS), str(per_dev * world), "1", devs], capture_output=True, text=True,
+        r = subprocess.run([exe, str(KEY_BITS), str(per_dev * world), "2", devs], capture_output=True, text=True,
                            timeout=900, env=env)
         res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
             {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
