@@ -79,3 +79,35 @@ def test_generated_kernel_on_wave_emulator():
     0 (N - 1), 1 1 and random rows) and a partly live wave (13 of 16), every row vs x y mod N"""
     import wave_emu
     wave_emu.selftest()
+
+
+def test_slow_path_ripples_carry_real_values():
+    """the normalisation's rare slow paths (gen_addb.py norm_two_chains: chain A's carry into chain B's
+    lowest dword; lane_delivery: a lane's carry into the next lane's chunk) must be run with nonzero carries, not
+    only with the slowall build's carry 0.  The emulator selftest's structured rows ((N - 1)^2, 0 (N - 1), rows >= N
+    under n = 2^2047 + 1) overflow both joins: every slow-path multiply-add is counted with the lanes whose carry
+    register is nonzero, and the results stay exact.  The one ripple no input reaches is lane 3's four extra dwords
+    (N1 dwords 128..131, only after dwords 113..127 saturate): the same generated ripple code under one more EXEC
+    mask; structured quotients (4 special moduli x 96 patterns, x = 1 and y = k 2^4072 + e) never overflowed there."""
+    import collections
+    import gen_addb as ga
+    import wave_emu
+    asm = ga.gen_addb('fthe_addb_q152')
+    ins = [s for s in (ln.split('//')[0].strip() for ln in asm.splitlines())
+           if s and not s.endswith(':') and not s.startswith('.')]
+    carry = f"v{166 + 1}"                                   # gen_addb: X = CR + 1, the rippled carry
+    ripple = {i for i, s in enumerate(ins) if s.startswith('v_mad_i64_i32') and f", {carry}, 1," in s}
+    assert ripple
+    hits = collections.Counter()
+    orig = wave_emu.Wave.step
+
+    def step(self, op, a):
+        if self.pc - 1 in ripple:
+            hits[self.pc - 1] += sum(1 for ln in self.lanes() if self.vget(ln, a[2]) != 0)
+        return orig(self, op, a)
+    wave_emu.Wave.step = step
+    try:
+        wave_emu.selftest()                                 # asserts every row exact
+    finally:
+        wave_emu.Wave.step = orig
+    assert sum(hits.values()) > 100 and len([pc for pc, h in hits.items() if h]) > 30, hits

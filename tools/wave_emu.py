@@ -626,6 +626,31 @@ def run_workgroup(asm, lds_bytes, waves, mem, kernarg_addr, wg, nvgpr, finish=No
     return sum(w.count for w in ws)
 
 
+def addb_run(n, xs, ys, asm=None):
+    """one workgroup of fthe_addb_q152 (12 waves, wave 0 runs) on the rows xs, ys (len <= 16) under n: the output
+    rows as integers"""
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
+    sys.path.insert(0, here)
+    import gen_addb as ga
+    import addb_model as am
+    asm = asm or ga.gen_addb('fthe_addb_q152')
+    N = n * n
+    img = am.addb_image(N)
+    count = len(xs)
+    mem = Mem()
+    XB, YB, OB, KB, KA = 0x10000000, 0x20000000, 0x30000000, 0x40000000, 0x50000000
+    mem.alloc(b''.join(x.to_bytes(512, 'little') for x in xs), XB)
+    mem.alloc(b''.join(y.to_bytes(512, 'little') for y in ys), YB)
+    mem.alloc(bytes(512 * 16), OB)
+    mem.alloc(img, KB)
+    karg = XB.to_bytes(8, 'little') + YB.to_bytes(8, 'little') + OB.to_bytes(8, 'little') + \
+        KB.to_bytes(8, 'little') + count.to_bytes(4, 'little') + (1).to_bytes(4, 'little') + bytes(16)
+    mem.alloc(karg, KA)
+    run_workgroup(asm, ga.LDS_BYTES, ga.WAVES, mem, KA, 0, 168)
+    return [mem.read(OB + 512 * i, 512) for i in range(count)]
+
+
 def selftest(ntests=16, count0=None):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(here, '..', 'fedtree_amd', 'csrc'))
