@@ -47,7 +47,7 @@ MEASURED_MAD_S = 3.45e13                   # microbenchmark, 8 chains x 16 waves
 # over 2048-bit moduli (s = 64).
 W64 = 2 * 64 * 64 + 64
 ALG_MACS_PER_CRT_ENC = 2 * 1.2 * 2048 * W64          # 4.06e7
-PMC_FILE = "r05o_pmc.json"
+PMC_FILE = "r06q_pmc.json"
 
 
 def parse():
@@ -453,7 +453,7 @@ def node_e2e(a, world, devices, rehearse):
     try:
         env = dict(os.environ, FTHE_SHIM_REPLICATE="1" if rehearse else "0")
         r = subprocess.run([exe, str(KEY_BITS), str(per_dev * world), "2", devs], capture_output=True, text=True,
-                           timeout=900, env=env)
+                           timeout=420, env=env)
         res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
             {"error": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
     except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as ex:
