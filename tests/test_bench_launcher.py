@@ -84,3 +84,42 @@ def test_compact_line_fits_the_driver_record():
     cb = line["cpu_baseline"]
     assert cb["value"] == full["cpu_baseline"]["value"] and cb["cores"] and cb["kind"] and cb["sample"]
     assert "note" not in text
+
+
+def test_node_e2e_arguments_and_memory_cap(monkeypatch):
+    """bench.node_e2e (N > 1, rank 0 after the timed region): ghpair_e2e over the run's devices in one child process,
+    N x 10M pairs by default, capped so the batch (~2.3 KB of host memory per pair) stays within 40% of the free host
+    memory; under FTHE_BENCH_REHEARSE every shard on device 0 with key replicas forced.  The child is faked here."""
+    sys.path.insert(0, ROOT)
+    import bench
+    calls = []
+
+    class R:
+        returncode = 0
+        stdout = '{"encrypts_per_s": 1.0, "decrypts_per_s": 2.0, "ok": true, "shards": 4}\n'
+        stderr = ""
+
+    def fake_run(cmd, **kw):
+        calls.append((cmd, kw.get("env", {})))
+        return R()
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.delenv("FTHE_BENCH_NODE_PAIRS", raising=False)
+    monkeypatch.setattr(bench, "host_mem_bytes", lambda: 10 ** 15)
+    out = bench.node_e2e(None, 4, [3, 1, 0, 2], False)
+    cmd, env = calls[-1]
+    assert cmd[1:] == ["2048", str(4 * 10_000_000), "2", "0,1,2,3"] and env["FTHE_SHIM_REPLICATE"] == "0"
+    assert out["ok"] and out["shards"] == 4 and out["pairs_per_device"] == 10_000_000
+    assert out["encrypts_per_s_per_device"] == 0
+    monkeypatch.setattr(bench, "host_mem_bytes", lambda: 10 ** 9)          # 1 GB free: 0.4 GB / 2.3 KB / 2 devices
+    out = bench.node_e2e(None, 2, [0, 1], True)
+    cmd, env = calls[-1]
+    per = int(0.4 * 10 ** 9 / bench.E2E_HOST_BYTES_PER_PAIR / 2)
+    assert out["pairs_per_device"] == per and cmd[2] == str(2 * per)
+    assert cmd[4] == "0,0" and env["FTHE_SHIM_REPLICATE"] == "1"
+
+
+def test_host_mem_bytes_is_positive():
+    sys.path.insert(0, ROOT)
+    import bench
+    m = bench.host_mem_bytes()
+    assert m is None or m > 0
