@@ -486,6 +486,9 @@ def run(a, world):
         else:
             # RCCL carries only the barriers and the max-over-ranks gathers: no data-path collective
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timedelta(minutes=60))
+    # the final wait for rank 0's CPU baseline and node-wide drop-in pass on a CPU (gloo) group: an RCCL barrier would
+    # keep a spinning kernel on every other GPU while the node pass runs its shards there
+    cpu_group = dist.new_group(backend="gloo", timeout=timedelta(minutes=60)) if world > 1 and not rehearse else None
     from fedtree_amd.paillier import Device, Paillier
     from fedtree_amd.synth import logistic_gradients
     from fedtree_amd import _lib
@@ -1208,7 +1211,7 @@ def run(a, world):
         write_detail(line)
         print(compact_line(line), flush=True)
     if world > 1:
-        dist.barrier()                                 # the other ranks wait for rank 0's CPU stage
+        dist.barrier(group=cpu_group)                  # the other ranks wait for rank 0's CPU stage (gloo: no GPU)
         dist.destroy_process_group()
 
 
