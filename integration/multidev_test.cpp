@@ -168,6 +168,14 @@ int main(int argc, char **argv) {
     party.subtract(d, b, a);
     std::printf("subtract_big %016llx\n", (unsigned long long)digest(a));
 
+    // the root sum of Tree::init_CPU (tree.cpp:20-34), plain product and the reference's Enc(0)-first sequence
+    GHPair root = party.sum(gh), root0 = party.sum(gh, true);
+    std::printf("sum %016llx\n", (unsigned long long)fnv(fnv(1469598103934665603ull, hex(root.g_enc) + ":" + hex(root.h_enc)),
+                                                         hex(root0.g_enc) + ":" + hex(root0.h_enc)));
+    SyncArray<GHPair> rs(2);
+    rs.host_data()[0] = root;
+    rs.host_data()[1] = root0;
+
     // Server::decrypt_gh_pairs (server.h:123-135) of everything: the plaintexts
     server.decrypt(a);                                       // (gh + hist) - hist = gh
     for (size_t i = 0; i < N; i++)
@@ -191,6 +199,18 @@ int main(int argc, char **argv) {
     server.decrypt(d);
     for (size_t i = 0; i < N; i++)
         if (std::fabs(d.host_data()[i].g - (expect(val(i, 0)) + expect(val(i + 3, 1)))) > 2e-5) bad++;
+    server.dec_short = false;
+    server.decrypt(rs);                                      // the root sums: sum of the codec values mod 2^64
+    {
+        int64_t sg = 0, sh = 0;
+        for (size_t i = 0; i < N; i++) {
+            sg += (int64_t)fthe_shim::encode(val(i, 0));
+            sh += (int64_t)fthe_shim::encode(val(i, 1));
+        }
+        for (int r = 0; r < 2; r++)
+            if (rs.host_data()[r].g != fthe_shim::decode((uint64_t)sg) || rs.host_data()[r].h != fthe_shim::decode((uint64_t)sh))
+                bad++;
+    }
     std::printf("decrypt_checks bad=%d\n", bad);
     std::printf("devices %zu\n", fthe_shim::shard_devices().size());
     std::printf("multidev %s\n", bad ? "FAIL" : "OK");

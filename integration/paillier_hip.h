@@ -627,6 +627,55 @@ public:
         });
     }
 
+    // The N-to-1 root sum of Tree::init_CPU (tree.cpp:20-34: thrust::reduce of the gradients with GHPair::operator+):
+    // sum_gh = prod_i gh[i] for g and h.  Sharded over the devices by instance ranges: each shard's
+    // partial products of its g rows and h rows on its device (fthe_reduce_segments, one segment each), the <= 7
+    // partials combined on the host (x y mod n^2, the reference's own add).  zero_first: Enc(0) * prod, the
+    // reference's exact sequence (thrust's GHPair() initial value is an unencrypted zero, whose first + encrypts 0,
+    // SURVEY Q10).  Unencrypted entries are encrypted first, as the operators promote them.
+    GHPair sum(SyncArray<GHPair> &gh, bool zero_first = false) {
+        const size_t n = gh.size();
+        GHPair out;
+        if (n == 0) return out;                                  // the reference's GHPair(): an unencrypted zero
+        const size_t cw = 2 * (size_t)fthe_key_n_words(key());
+        std::vector<uint32_t> x = rows(gh);
+        auto plan = fthe_shim::shard_plan(n, fthe_shim::shard_devices().size(), fthe_shim::shard_min_rows());
+        std::vector<uint32_t> part(plan.size() * 2 * cw);
+        run_plan(plan, [&](fthe_ctx *ctx, fthe_key *kk, size_t lo, size_t hi, unsigned) {
+            const size_t i = (size_t)(std::find(plan.begin(), plan.end(), std::make_pair(lo, hi)) - plan.begin());
+            const int64_t ptr[2] = {0, (int64_t)(hi - lo)};
+            for (int pl = 0; pl < 2; pl++)                       // the g rows, then the h rows of [lo, hi)
+                fthe_shim::check(fthe_reduce_segments(kk, ctx, x.data() + (pl * n + lo) * cw, hi - lo, ptr, nullptr,
+                                                      1, part.data() + (2 * i + pl) * cw), "sum");
+        });
+        mpz_t acc[2], t;
+        for (int pl = 0; pl < 2; pl++) {
+            mpz_init(acc[pl]);
+            fthe_shim::from_words(acc[pl], part.data() + pl * cw, (int)cw);
+        }
+        mpz_init(t);
+        for (size_t i = 1; i < plan.size(); i++)
+            for (int pl = 0; pl < 2; pl++) {
+                fthe_shim::from_words(t, part.data() + (2 * i + pl) * cw, (int)cw);
+                paillier_cpu.add(acc[pl], acc[pl], t);
+            }
+        if (zero_first) {
+            uint64_t zero[2] = {0, 0};
+            std::vector<uint32_t> ez(2 * cw);
+            encrypt_rows(zero, 2, ez.data());
+            for (int pl = 0; pl < 2; pl++) {
+                fthe_shim::from_words(t, ez.data() + pl * cw, (int)cw);
+                paillier_cpu.add(acc[pl], t, acc[pl]);
+            }
+        }
+        std::vector<uint32_t> gw(cw), hw(cw);
+        fthe_shim::to_words(acc[0], gw.data(), (int)cw);
+        fthe_shim::to_words(acc[1], hw.data(), (int)cw);
+        set_enc(out, gw.data(), hw.data(), (int)cw);
+        mpz_clear(acc[0]); mpz_clear(acc[1]); mpz_clear(t);
+        return out;
+    }
+
     // ---- sharded engine calls on host rows (the helpers above; public for callers with rows in hand) ----
     // c[i] = Enc(m[i]) (fthe_encrypt_u64_at with this object's enc_mode and rng_seed)
     void encrypt_rows(const uint64_t *m, size_t count, uint32_t *c) {
