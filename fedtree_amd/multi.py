@@ -89,3 +89,14 @@ class ShardedPaillier:
 
     def reduce_kway(self, x):
         return np.concatenate(self._run(x.shape[1], lambda k, lo, hi: k.reduce_kway(x[:, lo:hi])))
+
+    def sum(self, x):
+        """The N-to-1 product of rows x (the root sum of Tree::init_CPU, tree.cpp:20-34, for one plane): each
+        device's partial product of its row range (one segment), then the <= 7 partials combined as a k-way
+        product on the first device (no collective, a few adds on one side)."""
+        x = np.ascontiguousarray(x, dtype=np.uint32)
+        parts = self._run(len(x), lambda k, lo, hi: k.reduce_segments(x[lo:hi], np.array([0, hi - lo])))
+        stack = np.stack([p[0] for p in parts])                 # (shards, row words)
+        if len(stack) == 1:
+            return stack[0]
+        return self.keys[0].reduce_kway(stack[:, None, :])[0]

@@ -315,6 +315,10 @@ def test_sharded_two_contexts(dev, coracle):
     assert np.array_equal(sp.sub_batch(c[:500], c[500:1000]), pl.sub_batch(c[:500], c[500:1000]))
     assert np.array_equal(sp.scalar_mul(c[:300], 12345), pl.scalar_mul(c[:300], 12345))
     assert np.array_equal(sp.decrypt_u64(c, short=True), m)
+    # the N-to-1 root sum (tree.cpp:20-34): per-context partial products, combined on one context = one product
+    root = sp.sum(c)
+    assert np.array_equal(root, pl.reduce_segments(c, np.array([0, len(c)]))[0])
+    assert int(pl.decrypt_u64(root[None, :])[0]) == int(m.sum(dtype=np.uint64))
     # parties: public-key copies with published bases on every context
     pub = ShardedPaillier(pl.public(), [Device(0), Device(0)], bases=pl.public_bases(seed=2))
     cp = pub.encrypt_u64(m, seed=6, fixed_base_exact=True)
