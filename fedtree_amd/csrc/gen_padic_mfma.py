@@ -105,6 +105,7 @@ def gen_padic_mfma(name: str) -> str:
     # product columns: NCOL adjacent columns side by side (one 64-bit accumulator chain each), two column
     # sets (the tails of one set run inside the next set's multiply-adds)
     NCOL = next((int(t[3:]) for t in AB.split(',') if t in ('col3', 'col4')), 2)
+    assert NCOL == 2 or not KARA, "col3 / col4 predate the Karatsuba cross term (wrong results, r06s): add nokara"
     ACC0 = 10 if NCOL == 2 else 2                # v[ACC0 .. ACC0 + 4 NCOL); below v20 either way
     CARRY = ACC0 + 4 * NCOL
     XA = 20                                      # x0 digit (v20..v56); Barrett: accumulators v20..v51
