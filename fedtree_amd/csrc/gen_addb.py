@@ -50,7 +50,9 @@ S, Q, B = 152, 38, 27
 MASK = (1 << B) - 1
 WAVES = 12                       # waves per workgroup (one workgroup per CU, 3 waves per SIMD)
 CT_PER_WAVE = 16
-RB = 68                          # A-column row: 16 ciphertexts x 4 B + pad (gen_quad's QUAD_ROWB)
+RB = 72                          # A-column row: 16 ciphertexts x 4 B + pad; 18 dwords: the window / z-limb
+                                 # accesses of a 32-lane group (4 quad lanes 19 or 38 rows apart) at most 2-way
+                                 # (68 B: 3-way; 76 B does not fit the LDS)
 COPY = 800                       # one byte-shifted copy of a constant (== 32 mod 256: conflict-free reads)
 KO1, KO2 = 64, 560               # copy offsets: y = KO + 16 (4 kb - t) + 16 h
 A1_OFF = 0
@@ -62,10 +64,6 @@ IMG_BYTES = CORR2_OFF + TILES2 * 64          # 29,824
 N_OFF = IMG_BYTES                            # N dwords in kctx (not copied to LDS)
 ONE_OFF = N_OFF + 512                        # the integer 1 as a row (gathered index < 0)
 KCTX_BYTES = ONE_OFF + 512
-WAVE_AREA = 10496                            # A column (152 x 68) / q staging (16 x 656) / groups (16 x 296)
-LDS_WAVES = IMG_BYTES
-LDS_CNT = LDS_WAVES + WAVES * WAVE_AREA      # the workgroup's batch counter (dword)
-LDS_BYTES = LDS_CNT + 16                     # 153,872
 QROW = 656                                   # q staging row: 9 K-blocks of 64 bytes, stride = 4 (mod 32)
                                              # dwords: the quads' staging writes 4-way, not 16-way, per bank
 GROW = 552                                   # group staging row: two chunks' 64-68 int64 groups; 138 dwords ==
@@ -73,6 +71,10 @@ GROW = 552                                   # group staging row: two chunks' 64
 GCH = 264                                    # the pair's second chunk at byte 264 (66 dwords == 2 mod 64): with
                                              # GROW the normalisation's ds_read_b64 are conflict-free too
                                              # (tools/lds_conflicts.py; 16-byte rows for b128 reads cannot be)
+WAVE_AREA = (max(S * RB, 16 * QROW, 16 * GROW) + 15) // 16 * 16   # A column (152 rows) / q staging / groups
+LDS_WAVES = IMG_BYTES
+LDS_CNT = LDS_WAVES + WAVES * WAVE_AREA      # the workgroup's batch counter (dword)
+LDS_BYTES = LDS_CNT + 16
 KB1, KB2 = 9, 9
 NQ1, NQ3 = 129, 129                          # q1, q3 dwords (rows >= N: q3 < 2^4098)
 MU_SHIFT = 4072 + 4128                       # mu = floor(2^(A + C) / N)
