@@ -397,7 +397,8 @@ def test_sharded_drop_in_every_device(tmp_path, mode):
     one-device run's digests byte for byte -- seeded encrypts (default, party published-bases exact, key-holder
     exact), histogram, merges, subtracts, prefix -- with every decrypt checked; then ghpair_e2e round-trips
     20,000 pairs per device over all of them.  Skipped with fewer than 2 GPUs.  "emulated" is the same over two
-    contexts on device 0 with every shard on a key replica (FTHE_SHIM_REPLICATE=1), the path a one-GPU box runs."""
+    contexts on device 0 with every shard on a key replica (FTHE_SHIM_REPLICATE=1), the path a one-GPU box runs, and
+    ghpair_e2e over eight contexts of device 0 (configs[4]'s eight shards and worker threads)."""
     import json
     n = _gpu_count()
     if mode == "physical" and n < 2:
@@ -420,8 +421,9 @@ def test_sharded_drop_in_every_device(tmp_path, mode):
     assert outs[devs] == outs["0"], outs
     exe2 = str(tmp_path / "ghpair_e2e")
     _build(exe2, "ghpair_e2e.cpp", extra=("-fopenmp",))
-    k = len(devs.split(","))
-    r = subprocess.run([exe2, "2048", str(20000 * k), "1", devs], capture_output=True, text=True, timeout=300,
+    e2e_devs = devs if mode == "physical" else ",".join(["0"] * 8)    # emulated: configs[4]'s eight shards
+    k = len(e2e_devs.split(","))
+    r = subprocess.run([exe2, "2048", str(20000 * k), "1", e2e_devs], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, FTHE_SHIM_REPLICATE="0" if mode == "physical" else "1"))
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
