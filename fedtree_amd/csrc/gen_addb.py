@@ -108,6 +108,43 @@ def band(nd, s0, k0):
     return not (hi < 0 or lo >= nd)
 
 
+# ---- the matrix-core product z = x y (section 2M, "mfz"; tools/addb_mfz_model.py is its bit-exact model) ------
+# one ciphertext at a time per wave: x, y in balanced base-256 digits (513 each); z's byte columns
+# c = i + 16 j + 256 u (MFMA row i, column j, block u) accumulate over tiles t the products of x digits
+# a = i + 64 t + k - MZ_DELTA (row i's Toeplitz window) and y digits b = c - a (independent of i)
+MZ_DELTA = -1
+MZ_XOFF = 64                                 # x staging: byte MZ_XOFF + a holds digit a (zero pad below / above)
+
+
+def _mz_valid(t, u):
+    for i in range(16):
+        for j in range(16):
+            c = i + 16 * j + 256 * u
+            a0 = i + 64 * t - MZ_DELTA
+            if max(max(0, c - 512), a0) <= min(min(512, c), a0 + 63):
+                return True
+    return False
+
+
+MZ_TILES = [(t, u) for t in range(-2, 10) for u in range(4) if _mz_valid(t, u)]          # 28
+MZ_TS = sorted({t for t, _ in MZ_TILES})                                                 # -1 .. 7
+_mz_btop = [256 * u + 16 * j - 64 * t - 16 * h + MZ_DELTA for t, u in MZ_TILES for j in range(16) for h in range(4)]
+MZ_RY = max(_mz_btop) + (15 - max(_mz_btop)) % 16    # yr byte p holds y digit RY - p (RY = 15 mod 16)
+MZ_YAREA = (MZ_RY - min(_mz_btop) + 31) // 16 * 16
+MZ_XAREA = (MZ_XOFF + 15 + 64 * MZ_TS[-1] + 48 - MZ_DELTA + 20 + 15) // 16 * 16
+# B fragments by v = 4 u - t (one 16-byte read per v serves every tile with that v): byte offset 64 (VMAX - v)
+MZ_V = sorted({4 * u - t for t, u in MZ_TILES})
+# wave-area layout of the product phase (it ends before the Barrett phases use the same bytes)
+MZ_XS = 0
+MZ_YS = MZ_XS + MZ_XAREA
+MZ_GS = MZ_YS + MZ_YAREA                     # 256 int64 groups
+MZ_ZS = MZ_GS + 2048                         # z: 256 dwords + a zero dword
+MZ_WS = MZ_ZS + 1040                         # z >> 4104: 128 dwords at byte 12 + 4 w
+MZ_SS = MZ_WS + 528                          # lane-to-lane carries: 65 dwords, slot 0 = 0
+MZ_END = MZ_SS + 272
+assert MZ_RY >= 515 and (MZ_RY - MZ_DELTA) % 16 == 0 and (MZ_RY - 127) % 16 == 0 and len(MZ_TILES) == 28
+assert all(x % 16 == 0 for x in (MZ_YS, MZ_GS, MZ_ZS, MZ_WS, MZ_SS)) and MZ_YS + MZ_YAREA <= 2048
+
 ND1, ND2 = 515, 513                          # balanced digits of mu and N
 ACT1 = [[kb for kb in range(KB1) if band(ND1, 512 + 16 * t, 64 * kb)] for t in range(TILES1)]
 ACT2 = [[kb for kb in range(KB2) if band(ND2, 16 * t, 64 * kb)] for t in range(TILES2)]
@@ -123,6 +160,11 @@ def gen_addb(name: str) -> str:
     # the product z = x y as one level of Karatsuba (three 76 x 76-limb products, section 2K below) instead of
     # 152 x 152 operand scanning; "nokara" keeps the latter (a correct schedule, for the A/B)
     KARA = "nokara" not in DBG
+    # the product z = x y on the matrix cores, one ciphertext at a time (section 2M), switch "mfz": bit-exact,
+    # 60% fewer VALU instructions per add, but 13-15% fewer adds/s than the VALU Karatsuba product (680-685M vs
+    # 775-780M at 1M adds, profiles/r06x_addb_lib_ab.jsonl): its per-ciphertext loop is latency-bound, so off
+    MFZ = "mfz" in DBG
+    MZ_YI = 80                                    # y's dwords (quad layout), in place: balanced, then reversed
     o = []
     e = o.append
     DPP = "row_mask:0xf bank_mask:0xf"
@@ -181,7 +223,7 @@ def gen_addb(name: str) -> str:
     # s[36:37] y index list (0: direct rows), s[38:39] carry scratch of the gathered addresses
     LANE_MASK = {3: "s[20:21]", 0: "s[22:23]", 1: "s[24:25]", 2: "s[26:27]"}
     LIVE = "s[28:29]"
-    NSGPR = 68 if "stamp" in DBG else 42          # s[40:41]: the product steps' carry-out sink
+    NSGPR = 68 if "stamp" in DBG else 50 if MFZ else 42   # s[40:41]: the product steps' carry-out sink; MFZ: s42..s48
 
     e('.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
     e('.amdhsa_code_object_version 5')
@@ -438,21 +480,23 @@ def gen_addb(name: str) -> str:
     e('// @phase load')
     # ---- 1. x -> X limbs; y -> limbs -> the wave's A column (rows 38j + k of column c) ------------------
     # both rows in flight at once (one memory latency per batch), then y's limbs (via X) to the A column
+    YW = MZ_YI if MFZ else WY                     # the matrix-core product keeps y's dwords at v80 (section 2M)
     issue_row('s[4:5]', 's[34:35]', W0, GA)
-    issue_row('s[6:7]', 's[36:37]', WY, GA + 2)
+    issue_row('s[6:7]', 's[36:37]', YW, GA + 2)
     e('  s_waitcnt vmcnt(0)')
     e('  s_not_b64 exec, exec')                                          # dead lanes: zero operands
     e('  s_cbranch_execz .Lrows_live')                                   # (only in a partial batch)
     for i in range(33):
         e(f'  v_mov_b32_e32 v{W0 + i}, 0')
-        e(f'  v_mov_b32_e32 v{WY + i}, 0')
+        e(f'  v_mov_b32_e32 v{YW + i}, 0')
     e('.Lrows_live:')
     e('  s_mov_b64 exec, -1')
-    convert_row(WY, X)
-    for k in range(Q):
-        e(f'  ds_write_b32 v{V_ZR}, {X(k)} offset:{k * RB}')
-    convert_row(W0, X)
-    e('  s_waitcnt lgkmcnt(0)')
+    if not MFZ:
+        convert_row(WY, X)
+        for k in range(Q):
+            e(f'  ds_write_b32 v{V_ZR}, {X(k)} offset:{k * RB}')
+        convert_row(W0, X)
+        e('  s_waitcnt lgkmcnt(0)')
 
     def classic_product():
         e('// @phase product')
@@ -724,18 +768,273 @@ def gen_addb(name: str) -> str:
                 e(f'  v_cndmask_b32_e64 {X(Q2 * half + k)}, {tb}, {ta}, s[16:17]')   # lanes 0, 1: block 2
         e('  s_waitcnt lgkmcnt(0)')
 
-    if KARA:
-        kara_product()
+    # ---- 2M. z = x y on the matrix cores (MFZ; tools/addb_mfz_model.py).  Both rows become balanced base-256
+    #          digits in place (x + 0x80..80, every byte XORed with 0x80; the carry out is digit 512), y's dwords
+    #          are reversed and byte-swapped; then per ciphertext c of the batch (a loop of 16): its quad stages
+    #          x (forward) and y (reversed) in the wave's area, every lane builds its nine A fragments (row i:
+    #          digits i + 64 t + k + 1, a dword-aligned five-dword read funnel-shifted by v_alignbyte_b32), reads
+    #          the 13 B fragments (one aligned 16-byte read per v = 4 u - t) and issues the 28 MFMAs into four
+    #          accumulator sets (column blocks u); each lane folds its four rows into an int64 group, lane l
+    #          normalises groups 4 l .. 4 l + 3 and the carries move lane to lane through LDS until none is left;
+    #          z (256 dwords) and z >> 4104 (128) go to LDS, from where the quad reads ZL / ZL128 / WD. ---------
+    def mfz_product():
+        e('// @phase product')
+        XI, YI = W0, MZ_YI                        # 32 dwords each (+ the digit-512 slot: v78 / v112)
+        CXI, CYI = XI + 32, YI + 32
+        DA = (114, 118, 122, 126)                 # accumulators of the column blocks u = 0..3
+        AT = {t: 8 + 4 * n for n, t in enumerate(MZ_TS)}       # A fragments v8..v43
+        R4 = (44, 45, 79)                         # the A reads' fifth dwords
+        BB = (130, 134, 148)                      # B fragments (three buffers)
+        V_AX, V_S, V_BY, V_GW, V_GR, V_SS, V_ZA, V_WA, V_XS, V_YS, V_QZ, V_QW = \
+            146, 147, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161
+        V_WB = 113
+        CIN, SG, C1, NXT = 164, 165, 166, 167
+        CO, BIN, TT = 114, 115, 116               # conversion scratch (the accumulators are free then)
+        GQ = 8                                    # the four groups of a lane (pairs v8..v15, A fragments dead)
+        WW = 16                                   # its four W dwords
+        assert AT[MZ_TS[-1]] + 4 <= 44 and len(MZ_TS) == 9
+        # ---- balanced digits (all 16 ciphertexts at once, quad layout) ----
+        VK = 117                                  # 0x80808080 (v_addc reads vcc: no SGPR beside it)
+        e(f'  v_mov_b32_e32 v{VK}, s33')
+        for R, cx in ((XI, CXI), (YI, CYI)):
+            lab = f'.Lmzb{R}'
+            e(f'  v_add_co_u32_e32 v{R}, vcc, s33, v{R}')
+            for i in range(1, 32):
+                e(f'  v_addc_co_u32_e32 v{R + i}, vcc, v{VK}, v{R + i}, vcc')
+            e(f'  v_cndmask_b32_e64 v{CO}, 0, 1, vcc')
+            e(f'  v_mov_b32_e32 v{cx}, 0')
+            e(f'{lab}_loop:')
+            e(f'  v_add_u32_e32 v{cx}, v{cx}, v{CO}')                 # lane 3: the carry out (digit 512)
+            e('  s_nop 1')
+            e(f'  v_mov_b32_dpp v{BIN}, v{CO} quad_perm:[0,0,1,2] {DPP}')
+            e(f'  v_cndmask_b32_e64 v{BIN}, v{BIN}, 0, s[22:23]')     # lane 0 receives none
+            e(f'  v_mov_b32_e32 v{CO}, 0')
+            e(f'  v_cmp_ne_u32_e32 vcc, 0, v{BIN}')
+            e('  s_nop 4')
+            e(f'  s_cbranch_vccz {lab}_done')
+            e(f'  v_add_co_u32_e32 v{R}, vcc, v{R}, v{BIN}')
+            e('  s_nop 4')
+            e(f'  s_cbranch_vccz {lab}_loop')                          # absorbed by dword 0 everywhere (usual)
+            e('  s_and_saveexec_b64 s[38:39], vcc')
+            for i in range(1, 32):
+                e(f'  v_addc_co_u32_e32 v{R + i}, vcc, 0, v{R + i}, vcc')
+            e(f'  v_cndmask_b32_e64 v{CO}, 0, 1, vcc')
+            e('  s_mov_b64 exec, s[38:39]')
+            e(f'  s_branch {lab}_loop')
+            e(f'{lab}_done:')
+            for i in range(32):
+                e(f'  v_xor_b32_e32 v{R + i}, s33, v{R + i}')
+        # y reversed and byte-swapped: YI[m] = bswap(y dword 31 - m of the lane)
+        e('  s_mov_b32 s48, 0x10203')
+        for m in range(16):
+            e(f'  v_perm_b32 v{TT}, v{YI + m}, v{YI + m}, s48')
+            e(f'  v_perm_b32 v{YI + m}, v{YI + 31 - m}, v{YI + 31 - m}, s48')
+            e(f'  v_mov_b32_e32 v{YI + 31 - m}, v{TT}')
+        # ---- per-lane addresses (l the lane, i = l & 15, h = l >> 4, q = l & 3) ----
+        T0, T1, T2, T3 = 8, 9, 10, 11
+        e(f'  v_lshrrev_b32_e32 v{T0}, 7, v{V_TID}')                  # l
+        e(f'  v_and_b32_e32 v{T1}, 15, v{T0}')                         # i
+        e(f'  v_lshrrev_b32_e32 v{T2}, 4, v{T0}')                      # h
+        e(f'  v_lshl_add_u32 v{T3}, v{T2}, 4, v{T1}')                  # i + 16 h
+        e(f'  v_add_u32_e32 v{T3}, {MZ_XOFF - MZ_DELTA}, v{T3}')
+        e(f'  v_lshrrev_b32_e32 v{T3}, 2, v{T3}')
+        e(f'  v_lshl_add_u32 v{V_AX}, v{T3}, 2, s15')
+        e(f'  v_subrev_u32_e32 v{V_AX}, {64 - MZ_XS}, v{V_AX}')       # tile t at offset 64 (t + 1)
+        e(f'  v_add_u32_e32 v{V_S}, {MZ_XOFF - MZ_DELTA}, v{T1}')
+        e(f'  v_and_b32_e32 v{V_S}, 3, v{V_S}')                        # the byte shift
+        e(f'  v_lshlrev_b32_e32 v{T3}, 4, v{T2}')
+        e(f'  v_lshlrev_b32_e32 v{V_BY}, 4, v{T1}')
+        e(f'  v_sub_u32_e32 v{V_BY}, v{T3}, v{V_BY}')                  # 16 h - 16 j
+        e(f'  v_add_u32_e32 v{V_BY}, {MZ_YS + MZ_RY - MZ_DELTA - 64 * MZ_V[-1]}, v{V_BY}')
+        e(f'  v_add_u32_e32 v{V_BY}, s15, v{V_BY}')
+        e(f'  v_lshlrev_b32_e32 v{V_GW}, 3, v{T2}')
+        e(f'  v_lshl_add_u32 v{V_GW}, v{T1}, 5, v{V_GW}')
+        e(f'  v_add_u32_e32 v{V_GW}, {MZ_GS}, v{V_GW}')
+        e(f'  v_add_u32_e32 v{V_GW}, s15, v{V_GW}')                    # group 4 j + h (+ 64 u)
+        e(f'  v_mov_b32_e32 v{V_WB}, s15')
+        for reg, sh, base in ((V_GR, 5, MZ_GS), (V_SS, 2, MZ_SS), (V_ZA, 4, MZ_ZS), (V_WA, 4, MZ_WS + 12 - 512)):
+            e(f'  v_lshlrev_b32_e32 v{reg}, {sh}, v{T0}')
+            e(f'  v_add3_u32 v{reg}, v{reg}, v{V_WB}, {base}' if 0 <= base <= 64 else
+              f'  v_add_u32_e32 v{reg}, {base}, v{reg}')
+            if not 0 <= base <= 64:
+                e(f'  v_add_u32_e32 v{reg}, s15, v{reg}')
+        e(f'  v_and_b32_e32 v{T3}, 3, v{T0}')                          # q
+        e(f'  v_lshlrev_b32_e32 v{T3}, 7, v{T3}')                      # 128 q
+        e(f'  v_add_u32_e32 v{V_XS}, {MZ_XS + MZ_XOFF}, v{T3}')
+        e(f'  v_add_u32_e32 v{V_XS}, s15, v{V_XS}')
+        e(f'  v_sub_u32_e32 v{V_YS}, v{V_WB}, v{T3}')
+        e(f'  v_add_u32_e32 v{V_YS}, {MZ_YS + MZ_RY - 127 - 16}, v{V_YS}')
+        e(f'  v_add_u32_e32 v{V_QZ}, {MZ_ZS}, v{T3}')
+        e(f'  v_add_u32_e32 v{V_QZ}, s15, v{V_QZ}')
+        e(f'  v_add_u32_e32 v{V_QW}, {MZ_WS}, v{T3}')
+        e(f'  v_add_u32_e32 v{V_QW}, s15, v{V_QW}')
+        # ---- zero the staging pads: [XS, YS + YAREA) and the two zero slots ----
+        for k in range(4):
+            e(f'  v_mov_b32_e32 v{DA[0] + k}, 0')
+        e(f'  v_lshrrev_b32_e32 v{T3}, 3, v{V_TID}')                  # 16 l
+        e(f'  v_add_u32_e32 v{T3}, s15, v{T3}')
+        e(f'  ds_write_b128 v{T3}, {quad4(DA[0])} offset:{MZ_XS}')
+        e(f'  ds_write_b128 v{T3}, {quad4(DA[0])} offset:{MZ_XS + 1024}')
+        e(f'  ds_write_b32 v{V_WB}, v{DA[0]} offset:{MZ_ZS + 1024}')
+        e(f'  ds_write_b32 v{V_WB}, v{DA[0]} offset:{MZ_SS}')
+        e('  s_mov_b32 s46, 0')
+        e('  s_mov_b32 s47, -1')                                       # lanes 32..63
+        e('  s_mov_b64 s[44:45], 0xf')                                 # the quad of ciphertext c
+        e('  s_mov_b32 s42, 16')
+        e('.Lmz_ct:')
+        # ---- stage ciphertext c: x forward at XS + XOFF, y reversed (digit b at YS + RY - b) ----
+        e('  s_mov_b64 exec, s[44:45]')
+        for k in range(8):
+            e(f'  ds_write_b128 v{V_XS}, {quad4(XI + 4 * k)} offset:{16 * k}')
+            e(f'  ds_write_b128 v{V_YS}, {quad4(YI + 4 * k)} offset:{16 + 16 * k}')
+        e('  s_and_b64 exec, s[44:45], s[20:21]')                      # quad lane 3: the digits 512
+        e(f'  ds_write_b32 v{V_XS}, v{CXI} offset:{512 - 384}')
+        e(f'  v_lshlrev_b32_e32 v{TT}, 24, v{CYI}')
+        e(f'  ds_write_b32 v{V_YS}, v{TT} offset:{MZ_RY - 515 - (MZ_RY - 127 - 16 - 384)}')
+        e('  s_mov_b64 exec, -1')
+        # ---- A fragments: three reads per tile, then the funnel shift ----
+        q = []
+
+        def issue(tag, ins):
+            e(ins)
+            q.append(tag)
+
+        def wait_for(tag):
+            if tag in q:
+                i = len(q) - 1 - q[::-1].index(tag)
+                e(f'  s_waitcnt lgkmcnt({min(len(q) - i - 1, 15)})')
+                del q[:i + 1]
+        for n, t in enumerate(MZ_TS):
+            d = 16 * (t + 1)
+            a = AT[t]
+            issue(('a', t), f'  ds_read2_b32 v[{a}:{a + 1}], v{V_AX} offset0:{d} offset1:{d + 1}')
+            issue(('a', t), f'  ds_read2_b32 v[{a + 2}:{a + 3}], v{V_AX} offset0:{d + 2} offset1:{d + 3}')
+            issue(('a', t), f'  ds_read_b32 v{R4[n % 3]}, v{V_AX} offset:{4 * (d + 4)}')
+            if n >= 2:
+                tp = MZ_TS[n - 2]
+                wait_for(('a', tp))
+                ap, r4 = AT[tp], R4[(n - 2) % 3]
+                for k in range(4):
+                    hi = f"v{ap + k + 1}" if k < 3 else f"v{r4}"
+                    e(f'  v_alignbyte_b32 v{ap + k}, {hi}, v{ap + k}, v{V_S}')
+        for n in range(len(MZ_TS) - 2, len(MZ_TS)):
+            tp = MZ_TS[n]
+            wait_for(('a', tp))
+            ap, r4 = AT[tp], R4[n % 3]
+            for k in range(4):
+                hi = f"v{ap + k + 1}" if k < 3 else f"v{r4}"
+                e(f'  v_alignbyte_b32 v{ap + k}, {hi}, v{ap + k}, v{V_S}')
+        # ---- B fragments and the MFMAs, by v = 4 u - t ----
+        vs = MZ_V
+        first = set()
+        last_mfma = {}
+
+        def read_b(n):
+            issue(('b', n), f'  ds_read_b128 {quad4(BB[n % 3])}, v{V_BY} offset:{64 * (vs[-1] - vs[n])}')
+        read_b(0)
+        read_b(1)
+        e('  s_nop 1')                                                 # VALU-written A -> MFMA operand
+        last_v = {u: max(4 * uu - t for t, uu in MZ_TILES if uu == u) for u in range(4)}
+        folded = []
+
+        def fold(u):
+            since = sum(1 for ln in o[last_mfma[u] + 1:] if ln.startswith('  '))
+            need = 19 - since                                          # XDL -> VALU read (as XDL_WAIT)
+            while need > 0:
+                e(f'  s_nop {min(need, 8) - 1}')
+                need -= 8
+            acc = DA[u]
+            e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc}, 1, 0')
+            e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 1}, s30, {pair(PG)}')
+            e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 2}, s31, {pair(PG)}')
+            e(f'  v_mad_i64_i32 {pair(PG)}, vcc, v{acc + 3}, s32, {pair(PG)}')
+            issue(('w', u), f'  ds_write_b64 v{V_GW}, {pair(PG)} offset:{512 * u}')
+            folded.append(u)
+        for n, v in enumerate(vs):
+            wait_for(('b', n))
+            for t, u in MZ_TILES:
+                if 4 * u - t != v:
+                    continue
+                src_c = quad4(DA[u]) if u in first else '0'
+                first.add(u)
+                e(f'  v_mfma_i32_16x16x64_i8 {quad4(DA[u])}, {quad4(AT[t])}, {quad4(BB[n % 3])}, {src_c}')
+                last_mfma[u] = len(o) - 1
+            if n + 2 < len(vs):
+                read_b(n + 2)
+            for u in range(4):                    # a block two v-steps past its last MFMA: fold it meanwhile
+                if u not in folded and last_v[u] <= v - 2:
+                    fold(u)
+        # ---- fold: rows 4 h' .. 4 h' + 3 of block u -> group 4 j + h' + 64 u ----
+        for u in range(4):
+            if u not in folded:
+                fold(u)
+        # ---- normalisation: lane l chains groups 4 l .. 4 l + 3 (carry-in 0) ----
+        e(f'  ds_read_b128 v[{GQ}:{GQ + 3}], v{V_GR}')
+        e(f'  ds_read_b128 v[{GQ + 4}:{GQ + 7}], v{V_GR} offset:16')
+        e('  s_waitcnt lgkmcnt(0)')
+        for k in range(1, 4):
+            e(f'  v_mad_i64_i32 {pair(GQ + 2 * k)}, s[40:41], v{GQ + 2 * k - 1}, 1, {pair(GQ + 2 * k)}')
+        dws = [GQ, GQ + 2, GQ + 4, GQ + 6]                             # z dwords 4 l .. 4 l + 3
+        # the carries, lane to lane (slot l + 1 <- lane l; lane 0 reads slot 0 = 0), until none is left
+        WSHR = f'wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0'
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{CIN}, v{GQ + 7} {WSHR}')                # lane l - 1's carry (lane 0: 0)
+        e('.Lmz_cy:')
+        e(f'  v_cmp_ne_u32_e32 vcc, 0, v{CIN}')
+        e('  s_nop 4')
+        e('  s_cbranch_vccz .Lmz_cy_done')
+        e(f'  v_mov_b32_e32 v{C1}, v{CIN}')
+        for dd in dws:                                                 # add the signed carry, ripple its sign
+            e(f'  v_add_co_u32_e32 v{dd}, vcc, v{dd}, v{C1}')
+            e(f'  v_ashrrev_i32_e32 v{SG}, 31, v{C1}')
+            e(f'  v_addc_co_u32_e32 v{C1}, vcc, 0, v{SG}, vcc')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{CIN}, v{C1} {WSHR}')
+        e('  s_branch .Lmz_cy')
+        e('.Lmz_cy_done:')
+        # ---- z -> LDS; z >> 4104 (lanes 32..63) -> LDS; the quad of c reads ZL, ZL128, WD ----
+        e(f'  ds_write2_b32 v{V_ZA}, v{dws[0]}, v{dws[1]} offset0:0 offset1:1')
+        e(f'  ds_write2_b32 v{V_ZA}, v{dws[2]}, v{dws[3]} offset0:2 offset1:3')
+        e('  s_nop 1')
+        e(f'  v_mov_b32_dpp v{NXT}, v{dws[0]} wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0')   # lane l + 1's
+        for k in range(4):
+            hi = f"v{dws[k + 1]}" if k < 3 else f"v{NXT}"
+            e(f'  v_alignbit_b32 v{WW + k}, {hi}, v{dws[k]}, 8')
+        e('  s_mov_b64 exec, s[46:47]')
+        e(f'  ds_write2_b32 v{V_WA}, v{WW}, v{WW + 1} offset0:0 offset1:1')
+        e(f'  ds_write2_b32 v{V_WA}, v{WW + 2}, v{WW + 3} offset0:2 offset1:3')
+        e('  s_mov_b64 exec, s[44:45]')
+        e('  s_waitcnt lgkmcnt(0)')
+        for k in range(8):
+            e(f'  ds_read_b128 {quad4(ZLB + 4 * k)}, v{V_QZ} offset:{16 * k}')
+        e(f'  ds_read_b32 v{ZL128}, v{V_WB} offset:{MZ_ZS + 512}')
+        e(f'  ds_read_b32 v{WD}, v{V_QW} offset:12')
+        for k in range(7):
+            e(f'  ds_read_b128 {quad4(WD + 1 + 4 * k)}, v{V_QW} offset:{16 + 16 * k}')
+        e(f'  ds_read_b64 v[{WD + 29}:{WD + 30}], v{V_QW} offset:128')
+        e(f'  ds_read_b32 v{WD + 31}, v{V_QW} offset:136')
+        e('  s_mov_b64 exec, -1')
+        e('  s_lshl_b64 s[44:45], s[44:45], 4')
+        e('  s_sub_u32 s42, s42, 1')
+        e('  s_cmp_lg_u32 s42, 0')
+        e('  s_cbranch_scc1 .Lmz_ct')
+        e('  s_waitcnt lgkmcnt(0)')
+
+    if MFZ:
+        mfz_product()
     else:
-        classic_product()
-    limbs_to_words(X, lambda i: f"v{WD + i}", f"v{ZL128}", f"v{V_AI[0]}")
-    for k in range(Q):
-        e(f'  ds_read_b32 {X(k)}, v{V_ZR} offset:{k * RB}')
-    e('  s_waitcnt lgkmcnt(0)')
-    for k in range(Q):                            # the limbs were stored with their carries above bit 27
-        e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, {X(k)}')
-    limbs_to_words(X, lambda i: f"v{ZLB + i}", f"v{V_AI[1]}", f"v{V_AI[0]}")
-    e(f'  v_lshrrev_b32_e32 v{ZL128}, 19, {X(Q - 1)}')                # lane 3: bits 4096..4103 (limb 151 >> 19)
+        if KARA:
+            kara_product()
+        else:
+            classic_product()
+        limbs_to_words(X, lambda i: f"v{WD + i}", f"v{ZL128}", f"v{V_AI[0]}")
+        for k in range(Q):
+            e(f'  ds_read_b32 {X(k)}, v{V_ZR} offset:{k * RB}')
+        e('  s_waitcnt lgkmcnt(0)')
+        for k in range(Q):                            # the limbs were stored with their carries above bit 27
+            e(f'  v_and_b32_e32 {X(k)}, {hex(MASK)}, {X(k)}')
+        limbs_to_words(X, lambda i: f"v{ZLB + i}", f"v{V_AI[1]}", f"v{V_AI[0]}")
+        e(f'  v_lshrrev_b32_e32 v{ZL128}, 19, {X(Q - 1)}')                # lane 3: bits 4096..4103 (limb 151 >> 19)
 
     if "nobarrett" in DBG:
         e('  s_branch .Ldbg_sub')

@@ -111,3 +111,33 @@ def test_slow_path_ripples_carry_real_values():
     finally:
         wave_emu.Wave.step = orig
     assert sum(hits.values()) > 100 and len([pc for pc, h in hits.items() if h]) > 30, hits
+
+
+def test_matrix_core_product_model():
+    """tools/addb_mfz_model.py (the "mfz" product of gen_addb.py section 2M): z = x y from the 28 i8 MFMA tiles over
+    balanced digits, the dword-aligned A windows with their byte funnel shift, the reversed y staging, the groups and
+    the lane-to-lane carries, against Python integers on extreme and random operands"""
+    import addb_mfz_model as mm
+    import gen_addb as ga
+    assert (mm.DELTA, mm.XOFF, mm.TILES, mm.RY) == (ga.MZ_DELTA, ga.MZ_XOFF, ga.MZ_TILES, ga.MZ_RY)
+    rng = random.Random(23)
+    for x, y in [((1 << 4096) - 1, (1 << 4096) - 1), (int('80' * 512, 16), int('7f' * 512, 16)), (0, 3)] + \
+            [(rng.getrandbits(4096), rng.getrandbits(4096)) for _ in range(4)]:
+        assert mm.product(x, y)[0] == x * y
+
+
+def test_matrix_core_product_kernel_on_wave_emulator(monkeypatch):
+    """the "mfz" build of fthe_addb_q152 (the product on the matrix cores, a measured A/B variant: bit-exact on the
+    GPU, slower) on the emulator: 16 adds incl. (N - 1)^2, 0 y, 1 1 and the all-ones rows >= N"""
+    import gen_addb as ga
+    import wave_emu
+    monkeypatch.setenv("FTHE_GEN_ADDB_DBG", "mfz")
+    asm = ga.gen_addb('fthe_addb_q152')
+    assert '.Lmz_ct' in asm
+    rng = random.Random(29)
+    n = am.rand_n(rng)
+    N = n * n
+    xs = [N - 1, 0, 1, (1 << 4096) - 1] + [rng.randrange(N) for _ in range(12)]
+    ys = [N - 1, 5, 1, (1 << 4096) - 1] + [rng.randrange(N) for _ in range(12)]
+    out = wave_emu.addb_run(n, xs, ys, asm)
+    assert out == [x * y % N for x, y in zip(xs, ys)]

@@ -224,6 +224,15 @@ class Wave:
                 assert self.exec >> sl & 1, "DPP source lane disabled"
                 self.v[dst][l] = o1[l] if (self.vcc >> l) & 1 else old[sl]
             return
+        if op == 'v_mov_b32_dpp' and ('wave_shr:1' in a or 'wave_shl:1' in a):
+            # whole-wave shift by one lane; bound_ctrl:0 (the BC bit): the lane without a source gets 0
+            assert 'bound_ctrl:0' in a and self.exec == ALL, "wave shift: full EXEC and bound_ctrl:0"
+            src, dst = self.rr(a[1])[1], self.rr(a[0])[1]
+            old = list(self.v[src])
+            d = -1 if 'wave_shr:1' in a else 1
+            for l in range(64):
+                self.v[dst][l] = old[l + d] if 0 <= l + d < 64 else 0
+            return
         if op == 'v_mov_b32_dpp':
             perm = [int(x) for x in re.search(r'quad_perm:\[([0-9,]+)\]', ' '.join(a)).group(1).split(',')]
             src = self.rr(a[1])[1]
@@ -317,6 +326,22 @@ class Wave:
                 self.lds[addr:addr + 4] = ((old + self.vget(l, a[2])) & 0xffffffff).to_bytes(4, 'little')
                 self.vset(l, a[0], old)
             return
+        if op == 'ds_read2_b32':                   # vdst pair <- dwords at vaddr + 4 offset0 / + 4 offset1
+            o0 = o1 = 0
+            for t in a[2:]:
+                if t.startswith('offset0:'):
+                    o0 = int(t[8:], 0)
+                elif t.startswith('offset1:'):
+                    o1 = int(t[8:], 0)
+            for l in self.lanes():
+                base = self.vget(l, a[1])
+                vals = []
+                for oo in (o0, o1):
+                    addr = base + 4 * oo
+                    assert 0 <= addr and addr + 4 <= len(self.lds) and addr % 4 == 0, f"LDS read2 at {addr}"
+                    vals.append(int.from_bytes(self.lds[addr:addr + 4], 'little'))
+                self.vset(l, a[0], vals[0] | vals[1] << 32)
+            return
         if op == 'ds_write2_b32':                  # two dwords at vaddr + 4 offset0 / + 4 offset1
             o0 = o1 = 0
             for t in a[3:]:
@@ -377,7 +402,7 @@ class Wave:
                 self.vset(l, data_tok, self.mem.read(addr, width))
 
     def mfma(self, a):
-        D, A, Bt, C = (self.rr(t) for t in a)
+        D, A, Bt, C = (self.rr(t) for t in a)      # C None: the inline constant 0
         Am = [[0] * 64 for _ in range(16)]
         Bm = [[0] * 16 for _ in range(64)]
         for l in range(64):
@@ -395,7 +420,7 @@ class Wave:
         for l in range(64):
             h, col = l >> 4, l & 15
             for g in range(4):
-                c = s32(self.v[C[1] + g][l])
+                c = s32(self.v[C[1] + g][l]) if C is not None else 0
                 newd[(g, l)] = (out[4 * h + g][col] + c) & M32
         for (g, l), val in newd.items():
             self.v[D[1] + g][l] = val
@@ -560,6 +585,14 @@ class Wave:
             elif op == 'v_bfe_u32':
                 off, w = g(l, a[2]) & 31, g(l, a[3]) & 31
                 r = (g(l, a[1]) >> off) & ((1 << w) - 1)
+            elif op == 'v_alignbyte_b32':
+                r = (((g(l, a[1]) << 32) | g(l, a[2])) >> (8 * (g(l, a[3]) & 3)))
+            elif op == 'v_perm_b32':                 # byte k = selector byte k of {src0, src1} (0..3: src1)
+                both, sel, r = (g(l, a[1]) << 32) | g(l, a[2]), g(l, a[3]), 0
+                for k in range(4):
+                    sb = (sel >> (8 * k)) & 0xff
+                    assert sb < 8, "v_perm_b32 selector"
+                    r |= ((both >> (8 * sb)) & 0xff) << (8 * k)
             elif op == 'v_alignbit_b32':
                 r = (((g(l, a[1]) << 32) | g(l, a[2])) >> (g(l, a[3]) & 31))
             elif op == 'v_lshl_add_u64':
