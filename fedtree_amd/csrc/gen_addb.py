@@ -161,7 +161,7 @@ def gen_addb(name: str) -> str:
     # 152 x 152 operand scanning; "nokara" keeps the latter (a correct schedule, for the A/B)
     KARA = "nokara" not in DBG
     # the product z = x y on the matrix cores, one ciphertext at a time (section 2M), switch "mfz": bit-exact,
-    # 60% fewer VALU instructions per add, but 13-15% fewer adds/s than the VALU Karatsuba product (680-685M vs
+    # 70% fewer VALU instructions per add, but 13-15% fewer adds/s than the VALU Karatsuba product (680-685M vs
     # 775-780M at 1M adds, profiles/r06x_addb_lib_ab.jsonl): its per-ciphertext loop is latency-bound, so off
     MFZ = "mfz" in DBG
     MZ_YI = 80                                    # y's dwords (quad layout), in place: balanced, then reversed
@@ -957,7 +957,8 @@ def gen_addb(name: str) -> str:
                     continue
                 src_c = quad4(DA[u]) if u in first else '0'
                 first.add(u)
-                e(f'  v_mfma_i32_16x16x64_i8 {quad4(DA[u])}, {quad4(AT[t])}, {quad4(BB[n % 3])}, {src_c}')
+                if "mzmfma" not in DBG:           # timing knock-out (wrong results): no MFMAs
+                    e(f'  v_mfma_i32_16x16x64_i8 {quad4(DA[u])}, {quad4(AT[t])}, {quad4(BB[n % 3])}, {src_c}')
                 last_mfma[u] = len(o) - 1
             if n + 2 < len(vs):
                 read_b(n + 2)
@@ -968,6 +969,8 @@ def gen_addb(name: str) -> str:
         for u in range(4):
             if u not in folded:
                 fold(u)
+        if "mznorm" in DBG:                       # timing knock-out (wrong results): no normalisation / delivery
+            e('  s_branch .Lmz_next')
         # ---- normalisation: lane l chains groups 4 l .. 4 l + 3 (carry-in 0) ----
         e(f'  ds_read_b128 v[{GQ}:{GQ + 3}], v{V_GR}')
         e(f'  ds_read_b128 v[{GQ + 4}:{GQ + 7}], v{V_GR} offset:16')
@@ -1013,6 +1016,7 @@ def gen_addb(name: str) -> str:
             e(f'  ds_read_b128 {quad4(WD + 1 + 4 * k)}, v{V_QW} offset:{16 + 16 * k}')
         e(f'  ds_read_b64 v[{WD + 29}:{WD + 30}], v{V_QW} offset:128')
         e(f'  ds_read_b32 v{WD + 31}, v{V_QW} offset:136')
+        e('.Lmz_next:')
         e('  s_mov_b64 exec, -1')
         e('  s_lshl_b64 s[44:45], s[44:45], 4')
         e('  s_sub_u32 s42, s42, 1')
