@@ -138,12 +138,11 @@ MZ_V = sorted({4 * u - t for t, u in MZ_TILES})
 MZ_XS = 0
 MZ_YS = MZ_XS + MZ_XAREA
 MZ_GS = MZ_YS + MZ_YAREA                     # 256 int64 groups
-MZ_ZS = MZ_GS + 2048                         # z: 256 dwords + a zero dword
-MZ_WS = MZ_ZS + 1040                         # z >> 4104: 128 dwords at byte 12 + 4 w
-MZ_SS = MZ_WS + 528                          # lane-to-lane carries: 65 dwords, slot 0 = 0
-MZ_END = MZ_SS + 272
+MZ_ZS = MZ_GS + 2048                         # z: 256 dwords
+MZ_WS = MZ_ZS + 1024                         # z >> 4104: 128 dwords at byte 12 + 4 w
+MZ_END = MZ_WS + 528
 assert MZ_RY >= 515 and (MZ_RY - MZ_DELTA) % 16 == 0 and (MZ_RY - 127) % 16 == 0 and len(MZ_TILES) == 28
-assert all(x % 16 == 0 for x in (MZ_YS, MZ_GS, MZ_ZS, MZ_WS, MZ_SS)) and MZ_YS + MZ_YAREA <= 2048
+assert all(x % 16 == 0 for x in (MZ_YS, MZ_GS, MZ_ZS, MZ_WS)) and MZ_YS + MZ_YAREA <= 2048
 
 ND1, ND2 = 515, 513                          # balanced digits of mu and N
 ACT1 = [[kb for kb in range(KB1) if band(ND1, 512 + 16 * t, 64 * kb)] for t in range(TILES1)]
@@ -775,7 +774,7 @@ def gen_addb(name: str) -> str:
     #          digits i + 64 t + k + 1, a dword-aligned five-dword read funnel-shifted by v_alignbyte_b32), reads
     #          the 13 B fragments (one aligned 16-byte read per v = 4 u - t) and issues the 28 MFMAs into four
     #          accumulator sets (column blocks u); each lane folds its four rows into an int64 group, lane l
-    #          normalises groups 4 l .. 4 l + 3 and the carries move lane to lane through LDS until none is left;
+    #          normalises groups 4 l .. 4 l + 3 and the carries move lane to lane (DPP wave_shr) until none is left;
     #          z (256 dwords) and z >> 4104 (128) go to LDS, from where the quad reads ZL / ZL128 / WD. ---------
     def mfz_product():
         e('// @phase product')
@@ -785,8 +784,8 @@ def gen_addb(name: str) -> str:
         AT = {t: 8 + 4 * n for n, t in enumerate(MZ_TS)}       # A fragments v8..v43
         R4 = (44, 45, 79)                         # the A reads' fifth dwords
         BB = (130, 134, 148)                      # B fragments (three buffers)
-        V_AX, V_S, V_BY, V_GW, V_GR, V_SS, V_ZA, V_WA, V_XS, V_YS, V_QZ, V_QW = \
-            146, 147, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161
+        V_AX, V_S, V_BY, V_GW, V_GR, V_ZA, V_WA, V_XS, V_YS, V_QZ, V_QW = \
+            146, 147, 152, 153, 154, 156, 157, 158, 159, 160, 161
         V_WB = 113
         CIN, SG, C1, NXT = 164, 165, 166, 167
         CO, BIN, TT = 114, 115, 116               # conversion scratch (the accumulators are free then)
@@ -852,7 +851,7 @@ def gen_addb(name: str) -> str:
         e(f'  v_add_u32_e32 v{V_GW}, {MZ_GS}, v{V_GW}')
         e(f'  v_add_u32_e32 v{V_GW}, s15, v{V_GW}')                    # group 4 j + h (+ 64 u)
         e(f'  v_mov_b32_e32 v{V_WB}, s15')
-        for reg, sh, base in ((V_GR, 5, MZ_GS), (V_SS, 2, MZ_SS), (V_ZA, 4, MZ_ZS), (V_WA, 4, MZ_WS + 12 - 512)):
+        for reg, sh, base in ((V_GR, 5, MZ_GS), (V_ZA, 4, MZ_ZS), (V_WA, 4, MZ_WS + 12 - 512)):
             e(f'  v_lshlrev_b32_e32 v{reg}, {sh}, v{T0}')
             e(f'  v_add3_u32 v{reg}, v{reg}, v{V_WB}, {base}' if 0 <= base <= 64 else
               f'  v_add_u32_e32 v{reg}, {base}, v{reg}')
@@ -868,15 +867,13 @@ def gen_addb(name: str) -> str:
         e(f'  v_add_u32_e32 v{V_QZ}, s15, v{V_QZ}')
         e(f'  v_add_u32_e32 v{V_QW}, {MZ_WS}, v{T3}')
         e(f'  v_add_u32_e32 v{V_QW}, s15, v{V_QW}')
-        # ---- zero the staging pads: [XS, YS + YAREA) and the two zero slots ----
+        # ---- zero the staging pads: [XS, YS + YAREA) ----
         for k in range(4):
             e(f'  v_mov_b32_e32 v{DA[0] + k}, 0')
         e(f'  v_lshrrev_b32_e32 v{T3}, 3, v{V_TID}')                  # 16 l
         e(f'  v_add_u32_e32 v{T3}, s15, v{T3}')
         e(f'  ds_write_b128 v{T3}, {quad4(DA[0])} offset:{MZ_XS}')
         e(f'  ds_write_b128 v{T3}, {quad4(DA[0])} offset:{MZ_XS + 1024}')
-        e(f'  ds_write_b32 v{V_WB}, v{DA[0]} offset:{MZ_ZS + 1024}')
-        e(f'  ds_write_b32 v{V_WB}, v{DA[0]} offset:{MZ_SS}')
         e('  s_mov_b32 s46, 0')
         e('  s_mov_b32 s47, -1')                                       # lanes 32..63
         e('  s_mov_b64 s[44:45], 0xf')                                 # the quad of ciphertext c
